@@ -1,0 +1,160 @@
+/*
+ * waveformer_hip.h -- C-ABI of the MI355X (gfx950) WaveFormer hot-path library
+ * (libwaveformer_hip.so).
+ *
+ * The library is the drop-in boundary for the WaveFormer encoder/decoder hot path
+ * (SURVEY.md section 8a rows a1-a11).  Every entry point:
+ *   - takes device pointers, int64 sizes and a hipStream_t (passed as void*),
+ *   - never allocates (scratch is caller-owned; see the *_workspace_bytes queries),
+ *   - is stream-ordered and reentrant (no mutable global state except the thread-local
+ *     error string),
+ *   - returns 0 on success, a positive hipError_t from the launch, or a negative
+ *     WF_E* library code; wf_last_error() returns the message of the last failure on
+ *     the calling thread.
+ *
+ * Tensor layouts (all row-major / C-contiguous unless a stride argument says otherwise):
+ *   "channel-last"  (B, D, H, W, C)   -- the residual stream, LL bands, attention rasters
+ *   "bands"         (8, B, d, h, w, C) -- band 0 = LL ('aaa'), bands 1..7 = the ptwt detail
+ *                                         keys 'aad','ada','add','daa','dad','dda','ddd'
+ *                                         (key char i <-> axis (D,H,W)[i]; 'a' low, 'd' high)
+ *   "NCDHW"         (B, C, D, H, W)    -- PyTorch / MONAI convolution layout
+ * Activations are fp32 except the GEMM operands, which the kernels round to bf16
+ * (fp32 accumulation; LayerNorm, softmax and residual adds stay fp32).
+ * Weights passed as `*_bf16` are nn.Linear / 1x1x1-Conv3d weights [N][K] rounded to bf16
+ * (wf_cast_f32_to_bf16); every other parameter is the fp32 module tensor as-is.
+ */
+#ifndef WAVEFORMER_HIP_H
+#define WAVEFORMER_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WF_ABI_VERSION 1
+
+enum {
+  WF_OK = 0,
+  WF_E_SHAPE = -1,    /* a size or stride is unsupported (message names it) */
+  WF_E_NULLPTR = -2,  /* a required pointer is NULL */
+  WF_E_LAUNCH = -3    /* kernel launch failed (message has the HIP error string) */
+};
+
+int wf_abi_version(void);
+const char* wf_last_error(void);
+
+/* ---- utilities ------------------------------------------------------------------ */
+
+/* out[i] = bf16(in[i]) (round-to-nearest-even). Weight preparation; no reference analogue. */
+int wf_cast_f32_to_bf16(const float* in, uint16_t* out, int64_t n, void* stream);
+
+/* ---- a10: PatchEmbed -------------------------------------------------------------- */
+/* Replaces monai PatchEmbed.proj = Conv3d(Cin, Cout, k=2, s=2) as called at
+ * network_models/waveformer.py:281 (monai/networks/blocks/patchembedding.py:214).
+ * x: NCDHW (B, Cin, 2D, 2H, 2W); w: (Cout, Cin, 2, 2, 2) fp32; bias: (Cout);
+ * out: channel-last (B, D, H, W, Cout)  (== the rearrange at waveformer.py:286).        */
+int wf_patch_embed_fwd(const float* x, const float* w, const float* bias, float* out,
+                       int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W,
+                       void* stream);
+
+/* ---- a1: 1-level Haar analysis ----------------------------------------------------- */
+/* Replaces ptwt.wavedec3(x, 'db1', level=1, mode='zero') at network_models/wave_helper.py:350,
+ * including the NDHWC<->NCDHW permutes around it (wave_helper.py:484,486).
+ * x: channel-last (B, D, H, W, C), D/H/W even. If ln_w != NULL the input is first
+ * LayerNorm'ed over C with (ln_w, ln_b, ln_eps) -- Block.norm1 (wave_helper.py:477) fused.
+ * bands: (8, B, D/2, H/2, W/2, C); band 0 is the LL that feeds the window attention.      */
+int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float* ln_b, float ln_eps,
+                      float* bands, int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                      void* stream);
+
+/* ---- a11: multi-level Haar synthesis ------------------------------------------------- */
+/* Replaces ptwt.waverec3((LL,) + hf, 'db1') at network_models/idwt_upsample.py:160 and the
+ * torch.cat((out, skip), dim=1) after it (:163): the reconstruction is written into channels
+ * [0, C) of an NCDHW output whose batch stride is out_bstride elements.
+ * ll: NCDHW (B, C, d, h, w) at the coarsest level (batch stride ll_bstride).
+ * det[l*7 + k], l = 0..levels-1 coarse->fine, k = detail key 0..6 ('aad'..'ddd'):
+ *   element (b, c, z, y, x) of level l lives at det[l*7+k][b*det_s[4l+0] + c*det_s[4l+1]
+ *   + z*det_s[4l+2] + (y*W_l + x)*det_s[4l+3]]  (W_l = w * 2^l); channel-last band views and
+ *   contiguous NCDHW tensors are both expressible.  levels in [1, 4].
+ * out: (B, >=C, d*2^levels, h*2^levels, w*2^levels).                                     */
+int wf_idwt3d_haar(const float* ll, int64_t ll_bstride, const float* const* det,
+                   const int64_t* det_s, int levels, float* out, int64_t out_bstride,
+                   int64_t B, int64_t C, int64_t d, int64_t h, int64_t w, void* stream);
+
+/* ---- a2: relative-position bias ------------------------------------------------------ */
+/* bias[h][i][j] = table[index[i][j]][h]  (attention.py:94-97), index is the int64
+ * relative_position_index buffer (N, N), table (T, heads).                                */
+int wf_rel_pos_bias(const float* table, const int64_t* index, float* bias, int64_t N,
+                    int64_t heads, int64_t table_rows, void* stream);
+
+/* ---- a3/a4/a5: windowed multi-head self-attention ------------------------------------- */
+/* Replaces Block.window_partition (wave_helper.py:450-461) + Attention.forward
+ * (attention.py:83-104) + the window "reverse" reshape (wave_helper.py:498-499, quirk Q1).
+ * x: channel-last raster (B, D1, H1, W1, C); windows of ws^3 tokens are gathered with the
+ * (B, D/ws, H/ws, W/ws) window-major order of window_partition.  If ln_w != NULL the tokens
+ * are LayerNorm'ed first (Block.norm1 for level-0 blocks, wave_helper.py:477).
+ * out: (B*nW*N, C) fp32 in window-major order, which IS the (B, D1, H1, W1, C) raster that
+ * the reference's reshape produces (Q1).  raster_rows: x is (B*D1*H1*W1, C); when
+ * D1=H1=W1=ws=N^(1/3) and x is a plain (B_, N, C) token batch this is Attention.forward.
+ * wqkv_bf16 (3C, C), bqkv (3C) or NULL, bias (heads, N, N) from wf_rel_pos_bias,
+ * wproj_bf16 (C, C), bproj (C).  scale = qk_scale or head_dim^-0.5.
+ * workspace: wf_window_attention_workspace_bytes(...) bytes, 256-B aligned.               */
+int64_t wf_window_attention_workspace_bytes(int64_t B, int64_t C, int64_t D1, int64_t H1,
+                                            int64_t W1);
+int wf_window_attention_fwd(const float* x, const float* ln_w, const float* ln_b, float ln_eps,
+                            const uint16_t* wqkv_bf16, const float* bqkv,
+                            const float* bias, const uint16_t* wproj_bf16, const float* bproj,
+                            float* out, void* workspace, int64_t B, int64_t C, int64_t D1,
+                            int64_t H1, int64_t W1, int64_t ws, int64_t heads, float scale,
+                            void* stream);
+
+/* ---- a6: multi-scale fuse ------------------------------------------------------------- */
+/* Replaces the F.interpolate(trilinear, align_corners=False) + sum + shortcut of
+ * wave_helper.py:500-508 and computes the per-position LayerNorm statistics that Block.norm2
+ * (wave_helper.py:509) needs.
+ * src[s]: channel-last (B, sd[s], sh[s], sw[s], C), s < nsrc <= 4; a source whose size equals
+ * (D,H,W) is added as-is (level-0 path, wave_helper.py:505).  shortcut, out: (B, D, H, W, C).
+ * stats: (B*D*H*W, 2) = {mean, rstd} of out rows with eps ln_eps.                          */
+int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, int nsrc,
+                  const float* shortcut, float* out, float* stats, float ln_eps, int64_t B,
+                  int64_t C, int64_t D, int64_t H, int64_t W, void* stream);
+
+/* ---- a7/a8: CCF_FFN + the Block's norm2 and double residual (quirk Q4) ---------------- */
+/* Replaces attn_fused + mlp(norm2(attn_fused)) (wave_helper.py:509) with CCF_FFN.forward
+ * (wave_helper.py:260-294): pwconv(1x1x1, bias) -> LN(4C, eps1) -> GELU(erf) ->
+ * dwconv(3^3, groups=4C, pad 1, bias) -> LN(4C, eps1) -> GELU -> fc(Linear, bias) -> +input.
+ * xh: channel-last (B, D, H, W, C).  If stats != NULL the FFN input is
+ * n2 = LN(xh; stats, n2_w, n2_b) and out = xh + n2 + ffn(n2) (Block, Q4);
+ * if stats == NULL the input is xh itself and out = xh + ffn(xh) (bare CCF_FFN.forward).
+ * pw_bf16 (4C, C), pw_b (4C), ln1_w/b (4C), dw_w (4C, 27) fp32, dw_b (4C), ln2_w/b (4C),
+ * fc_bf16 (C, 4C), fc_b (C).  workspace: wf_ccf_ffn_workspace_bytes(...) bytes.          */
+int64_t wf_ccf_ffn_workspace_bytes(int64_t B, int64_t C, int64_t hidden, int64_t D, int64_t H,
+                                   int64_t W);
+int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* n2_w, const float* n2_b,
+                   const uint16_t* pw_bf16, const float* pw_b, const float* ln1_w,
+                   const float* ln1_b, float eps1, const float* dw_w, const float* dw_b,
+                   const float* ln2_w, const float* ln2_b, float eps2,
+                   const uint16_t* fc_bf16, const float* fc_b, float* out, void* workspace,
+                   int64_t B, int64_t C, int64_t hidden, int64_t D, int64_t H, int64_t W,
+                   void* stream);
+
+/* ---- a9: PatchMerging (quirk Q3) ------------------------------------------------------ */
+/* Replaces PatchMerging.forward (wave_helper.py:173-194): the 8-way strided gather with its
+ * duplicated sub-lattices, LN(8C, eps) and Linear(8C -> 2C, no bias).
+ * x: channel-last (B, D, H, W, C) (D, H, W even); out: channel-last (B, D/2, H/2, W/2, 2C). */
+int wf_patch_merging_fwd(const float* x, const float* ln_w, const float* ln_b, float eps,
+                         const uint16_t* red_bf16, float* out, int64_t B, int64_t C,
+                         int64_t D, int64_t H, int64_t W, void* stream);
+
+/* ---- a10: stage output projection (quirk Q5) ----------------------------------------- */
+/* Replaces MultiscaleTransformer.proj_out (waveformer.py:182-204) together with the
+ * rearrange to NCDHW before it (waveformer.py:289): non-affine LayerNorm over C with eps,
+ * x channel-last (B, S, C) (S = D*H*W) -> out NCDHW (B, C, S).  normalize=0 only transposes. */
+int wf_proj_out_fwd(const float* x, float* out, int normalize, float eps, int64_t B,
+                    int64_t C, int64_t S, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WAVEFORMER_HIP_H */

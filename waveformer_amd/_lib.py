@@ -1,0 +1,84 @@
+"""ctypes binding of libwaveformer_hip.so (the C-ABI declared in include/waveformer_hip.h).
+
+This is the reference-side FFI a Python caller uses: every entry point takes raw device
+pointers, int64 sizes and a hipStream_t, and returns an int status.  `call()` turns a non-zero
+status into RuntimeError carrying `wf_last_error()`.
+
+There is deliberately no fallback: if the library cannot be loaded every op raises, so a GPU
+run can never silently take another path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("WAVEFORMER_HIP_LIB", os.path.join(_HERE, "libwaveformer_hip.so"))
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I = ctypes.c_int
+_F = ctypes.c_float
+
+# name -> (restype, argtypes); must match include/waveformer_hip.h
+SIGNATURES = {
+    "wf_abi_version": (_I, []),
+    "wf_last_error": (ctypes.c_char_p, []),
+    "wf_cast_f32_to_bf16": (_I, [_P, _P, _I64, _P]),
+    "wf_patch_embed_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_dwt3d_haar_fwd": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_rel_pos_bias": (_I, [_P, _P, _P, _I64, _I64, _I64, _P]),
+    "wf_window_attention_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64]),
+    "wf_window_attention_fwd": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P,
+                                     _I64, _I64, _I64, _I64, _I64, _I64, _I64, _F, _P]),
+    "wf_msfuse_fwd": (_I, [_P, _P, _I, _P, _P, _P, _F, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_ccf_ffn_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I64]),
+    "wf_ccf_ffn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _F, _P, _P,
+                            _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_patch_merging_fwd": (_I, [_P, _P, _P, _F, _P, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_proj_out_fwd": (_I, [_P, _P, _I, _F, _I64, _I64, _I64, _P]),
+}
+
+_lock = threading.Lock()
+_lib = None
+_err = None
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes library; raises LibraryMissing if unavailable."""
+    global _lib, _err
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            _err = f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            raise LibraryMissing(_err)
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        ver = lib.wf_abi_version()
+        if ver != 1:
+            raise LibraryMissing(f"{p}: ABI version {ver}, expected 1")
+        _lib = lib
+        return _lib
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.wf_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def query(name: str, *args) -> int:
+    return int(getattr(load(), name)(*args))

@@ -1,0 +1,286 @@
+// attention.hip -- windowed multi-head self-attention.
+//
+// Reference: network_models/attention.py:83-104 (Attention.forward), driven by
+// Block.multi_scale_forward (wave_helper.py:482-499): window_partition -> qkv -> q*scale ->
+// q@k^T + relative_position_bias -> softmax -> @v -> proj, then the window "reverse" that is
+// a plain reshape (quirk Q1).  Here:
+//   qkv  : gemm_ares with the window gather (and norm1 for level-0 blocks) in its loader
+//   core : one workgroup = (window b_, head h, 64 queries); flash-style loop over 64-key
+//          tiles staged in LDS.  S^T = K.Q^T is computed "swapped" (keys on the MFMA rows,
+//          queries on the lanes) so the fp32 accumulator of S^T is, register for register,
+//          the B operand of O^T = V^T.P^T after bf16 rounding -- P never leaves registers and
+//          the softmax column reductions are 2 lane shuffles.  v_mfma_f32_16x16x16_bf16
+//          covers head_dim in 16-wide steps (head_dim is 16 at the default widths).
+//   proj : gemm_ares; rows stay in window-major order, which is exactly the reference's
+//          reshaped raster (Q1).
+#include "kernels.hpp"
+
+namespace wf {
+
+constexpr int kQB = 64;  // queries per workgroup (16 per wave)
+constexpr int kKT = 64;  // keys per LDS tile
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_core_kernel(const uint16_t* __restrict__ qkv,
+                                                        const float* __restrict__ bias,
+                                                        uint16_t* __restrict__ out, int N,
+                                                        int heads, float scale_log2) {
+  constexpr int NC = HD / 16;  // 16-wide head_dim chunks
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[kKT * (HD + 4)];  // [key][hd]
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[HD * (kKT + 4)];  // [hd][key]
+  constexpr int KS = HD + 4, VS = kKT + 4;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int qb = blockIdx.x, h = blockIdx.y;
+  const int64_t bw = blockIdx.z;
+  const int C = heads * HD;
+  const int64_t row0 = bw * N;  // first token row of this window
+  const int ld = 3 * C;
+  const int q = qb * kQB + wid * 16 + (lane & 15);  // this lane's query (column)
+  const bool qv = q < N;
+  const int g4 = 4 * (lane >> 4);
+
+  // Q^T fragments (B operand): lane holds Q[q][c*16 + g4 + j], j < 4
+  bf16x4 qf[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (qv)
+      qf[c] = *reinterpret_cast<const bf16x4*>(qkv + (row0 + q) * ld + h * HD + c * 16 + g4);
+    else
+      qf[c] = bf16x4{0, 0, 0, 0};
+  }
+  f32x4 o[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) o[c] = f32x4{0, 0, 0, 0};
+  float mrun = -INFINITY, lrun = 0.f;
+  const float* brow = bias + ((int64_t)h * N + (qv ? q : 0)) * N;
+
+  for (int k0 = 0; k0 < N; k0 += kKT) {
+    __syncthreads();
+    // stage K rows and V^T for keys k0..k0+63 (16-B chunks of 8 head_dim values)
+    for (int it = tid; it < kKT * (HD / 8); it += 256) {
+      const int kr = it / (HD / 8), ch = it % (HD / 8);
+      const int key = k0 + kr;
+      bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (key < N) {
+        const uint16_t* src = qkv + (row0 + key) * ld + h * HD + ch * 8;
+        kv = *reinterpret_cast<const bf16x8*>(src + C);
+        vv = *reinterpret_cast<const bf16x8*>(src + 2 * C);
+      }
+      *reinterpret_cast<bf16x8*>(Ks + kr * KS + ch * 8) = kv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * VS + kr] = (uint16_t)vv[j];
+    }
+    __syncthreads();
+
+    // S^T for 4 sub-tiles of 16 keys: rows key = k0 + kt*16 + g4 + i, column = query
+    f32x4 s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      s[kt] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const bf16x4 a =
+            *reinterpret_cast<const bf16x4*>(Ks + (kt * 16 + (lane & 15)) * KS + c * 16 + g4);
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, qf[c], s[kt], 0, 0, 0);
+      }
+    }
+    // scale + relative-position bias (log2 domain), key mask
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const int kb = k0 + kt * 16 + g4;
+      f32x4 bv;
+      if (kb + 3 < N) {
+        bv = *reinterpret_cast<const f32x4*>(brow + kb);
+      } else {
+        bv.x = kb + 0 < N ? brow[kb + 0] : 0.f;
+        bv.y = kb + 1 < N ? brow[kb + 1] : 0.f;
+        bv.z = kb + 2 < N ? brow[kb + 2] : 0.f;
+        bv.w = kb + 3 < N ? brow[kb + 3] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float t = s[kt][i] * scale_log2 + bv[i] * 1.4426950408889634f;
+        t = (kb + i < N) ? t : -INFINITY;
+        s[kt][i] = t;
+        tmax = fmaxf(tmax, t);
+      }
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mnew = fmaxf(mrun, tmax);
+    const float alpha = exp2f(mrun - mnew);  // mrun = -inf on the first tile -> 0
+    mrun = mnew;
+    float psum = 0.f;
+    bf16x4 pf[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = exp2f(s[kt][i] - mnew);
+        psum += p;
+        pf[kt][i] = (short)f2bf(p);
+      }
+    }
+    lrun = lrun * alpha + psum;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      o[c] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const bf16x4 a =
+            *reinterpret_cast<const bf16x4*>(Vt + (c * 16 + (lane & 15)) * VS + kt * 16 + g4);
+        o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pf[kt], o[c], 0, 0, 0);
+      }
+    }
+  }
+  // full column sums: the 4 lane groups hold disjoint key subsets
+  lrun += __shfl_xor(lrun, 16, 64);
+  lrun += __shfl_xor(lrun, 32, 64);
+  if (qv) {
+    const float inv = 1.f / lrun;
+    uint16_t* dst = out + (row0 + q) * C + h * HD + g4;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      bf16x4 r;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = (short)f2bf(o[c][i] * inv);
+      *reinterpret_cast<bf16x4*>(dst + c * 16) = r;
+    }
+  }
+}
+
+int launch_attn_core(const uint16_t* qkv, const float* bias, uint16_t* out, int64_t Bw, int N,
+                     int heads, int hd, float scale, hipStream_t s) {
+  if (Bw <= 0) return WF_OK;
+  if (Bw > 65535) return fail(WF_E_SHAPE, "attention: more than 65535 windows per call");
+  dim3 grid((unsigned)cdiv(N, kQB), (unsigned)heads, (unsigned)Bw);
+  const float sl2 = scale * 1.4426950408889634f;
+#define WF_ATTN_CASE(HDV)                                                                 \
+  case HDV:                                                                               \
+    hipLaunchKernelGGL(attn_core_kernel<HDV>, grid, dim3(256), 0, s, qkv, bias, out, N,   \
+                       heads, sl2);                                                       \
+    break;
+  switch (hd) {
+    WF_ATTN_CASE(16)
+    WF_ATTN_CASE(32)
+    WF_ATTN_CASE(48)
+    WF_ATTN_CASE(64)
+    WF_ATTN_CASE(96)
+    WF_ATTN_CASE(128)
+    WF_ATTN_CASE(192)
+    WF_ATTN_CASE(384)
+    default:
+      return fail(WF_E_SHAPE, "attention: head_dim must be one of 16,32,48,64,96,128,192,384");
+  }
+#undef WF_ATTN_CASE
+  return check_launch("attention core");
+}
+
+__global__ void rel_pos_bias_kernel(const float* __restrict__ table, const int64_t* __restrict__ index,
+                                    float* __restrict__ bias, int64_t NN, int heads) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NN) return;
+  const int64_t r = index[i];
+  for (int h = 0; h < heads; ++h) bias[h * NN + i] = table[r * heads + h];
+}
+
+}  // namespace wf
+
+using namespace wf;
+
+extern "C" int wf_rel_pos_bias(const float* table, const int64_t* index, float* bias, int64_t N,
+                               int64_t heads, int64_t table_rows, void* stream) {
+  WF_REQUIRE(N >= 1 && heads >= 1 && table_rows >= 1, "empty bias");
+  WF_REQUIRE_PTR(table);
+  WF_REQUIRE_PTR(index);
+  WF_REQUIRE_PTR(bias);
+  const int64_t NN = N * N;
+  hipLaunchKernelGGL(rel_pos_bias_kernel, dim3((unsigned)cdiv(NN, 256)), dim3(256), 0,
+                     (hipStream_t)stream, table, index, bias, NN, (int)heads);
+  return check_launch("wf_rel_pos_bias");
+}
+
+extern "C" int64_t wf_window_attention_workspace_bytes(int64_t B, int64_t C, int64_t D1,
+                                                       int64_t H1, int64_t W1) {
+  const int64_t rows = B * D1 * H1 * W1;
+  const int64_t qkv = ((rows * 3 * C * 2) + 255) & ~(int64_t)255;
+  const int64_t ao = ((rows * C * 2) + 255) & ~(int64_t)255;
+  return qkv + ao;
+}
+
+extern "C" int wf_window_attention_fwd(const float* x, const float* ln_w, const float* ln_b,
+                                       float ln_eps, const uint16_t* wqkv_bf16,
+                                       const float* bqkv, const float* bias,
+                                       const uint16_t* wproj_bf16, const float* bproj, float* out,
+                                       void* workspace, int64_t B, int64_t C, int64_t D1,
+                                       int64_t H1, int64_t W1, int64_t ws, int64_t heads,
+                                       float scale, void* stream) {
+  WF_REQUIRE(B >= 1 && C >= 8 && C % 8 == 0, "C must be a positive multiple of 8");
+  WF_REQUIRE(ws >= 1 && D1 % ws == 0 && H1 % ws == 0 && W1 % ws == 0,
+             "the raster must tile into ws^3 windows (window_partition, wave_helper.py:459)");
+  WF_REQUIRE(heads >= 1 && C % heads == 0, "dim must be divisible by num_heads");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(wqkv_bf16);
+  WF_REQUIRE_PTR(bias);
+  WF_REQUIRE_PTR(wproj_bf16);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE_PTR(workspace);
+  if (ln_w) WF_REQUIRE_PTR(ln_b);
+  const int64_t N = ws * ws * ws;
+  const int64_t rows = B * D1 * H1 * W1;
+  const int64_t Bw = rows / N;
+  hipStream_t s = (hipStream_t)stream;
+  uint16_t* qkv = reinterpret_cast<uint16_t*>(workspace);
+  uint16_t* ao = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(workspace) +
+                                             (((rows * 3 * C * 2) + 255) & ~(int64_t)255));
+  // 1. qkv = Linear(window_partition(norm1?(x)))
+  GemmArgs g{};
+  g.a_src = x;
+  g.a_bf16 = 0;
+  g.a_C = (int)C;
+  g.a_nseg = 1;
+  g.a_map = MAP_WINDOW;
+  g.mB = (int)B;
+  g.mD = (int)D1;
+  g.mH = (int)H1;
+  g.mW = (int)W1;
+  g.mws = (int)ws;
+  g.a_ln = ln_w ? LN_COMPUTE : LN_NONE;
+  g.a_ln_w = ln_w;
+  g.a_ln_b = ln_b;
+  g.a_eps = ln_eps;
+  g.w = wqkv_bf16;
+  g.M = rows;
+  g.N = (int)(3 * C);
+  g.K = (int)C;
+  g.epi = EPI_STORE;
+  g.bias = bqkv;
+  g.out = qkv;
+  g.out_bf16 = 1;
+  g.ldo = 3 * C;
+  int rc = launch_gemm(g, s, "wf_window_attention_fwd(qkv)");
+  if (rc) return rc;
+  // 2. softmax(q k^T * scale + bias) v
+  rc = launch_attn_core(qkv, bias, ao, Bw, (int)N, (int)heads, (int)(C / heads), scale, s);
+  if (rc) return rc;
+  // 3. proj; window-major rows == the reshaped raster (Q1)
+  GemmArgs p{};
+  p.a_src = ao;
+  p.a_bf16 = 1;
+  p.a_C = (int)C;
+  p.a_nseg = 1;
+  p.a_map = MAP_IDENTITY;
+  p.a_ln = LN_NONE;
+  p.w = wproj_bf16;
+  p.M = rows;
+  p.N = (int)C;
+  p.K = (int)C;
+  p.epi = EPI_STORE;
+  p.bias = bproj;
+  p.out = out;
+  p.out_bf16 = 0;
+  p.ldo = C;
+  return launch_gemm(p, s, "wf_window_attention_fwd(proj)");
+}

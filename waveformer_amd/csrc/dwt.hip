@@ -1,0 +1,266 @@
+// dwt.hip -- 3D Haar analysis (a1) and multi-level synthesis (a11) for gfx950.
+//
+// Reference arithmetic: ptwt 0.1.9 wavedec3 / waverec3 with wavelet 'db1', mode 'zero'
+// (call sites network_models/wave_helper.py:350 and network_models/idwt_upsample.py:160).
+// For even sizes the 'zero' padding is empty and one level is, per axis,
+//   analysis  a = (x[2n] + x[2n+1]) / sqrt2,  d = (x[2n] - x[2n+1]) / sqrt2
+//   synthesis x[2n] = (a + d) / sqrt2,        x[2n+1] = (a - d) / sqrt2
+// (pywt dec_lo/dec_hi/rec_lo/rec_hi of 'haar').  ptwt applies the 3D outer-product filter
+// in one conv, i.e. each coefficient is (signed sum of 8 voxels) * (1/sqrt2)^3; the kernels
+// below do the same: 3 butterfly stages without scaling, then one multiply by 2^-1.5.
+//
+// HBM roofline: both kernels are pure streaming (8 fp32 in -> 8 fp32 out per 2x2x2 cube).
+#include "rowgroup.hpp"
+
+namespace wf {
+
+constexpr float kHaar3 = 0.35355339059327373f;  // (1/sqrt 2)^3
+
+// Forward: one row group per OUTPUT position; lanes over channels.
+// x (B,D,H,W,C) channel-last -> bands (8,B,D/2,H/2,W/2,C); band k bits (bd,bh,bw) = k>>2,k>>1,k.
+template <int G, int V, bool LN>
+__global__ __launch_bounds__(256) void dwt3d_haar_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ ln_w, const float* __restrict__ ln_b,
+    float ln_eps, float* __restrict__ bands, int B, int C, int D, int H, int W) {
+  const int C4 = C >> 2;
+  const int d = D >> 1, h = H >> 1, w = W >> 1;
+  const int64_t P = (int64_t)d * h * w;           // output positions per batch
+  const int64_t total = (int64_t)B * P;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane & (G - 1);
+  const int groups_per_block = blockDim.x / G;
+  const int64_t gid0 = (int64_t)blockIdx.x * groups_per_block + threadIdx.x / G;
+  const int64_t gstride = (int64_t)gridDim.x * groups_per_block;
+  const int64_t band_stride = total * C;          // elements per band
+
+  bool live[V];
+  f32x4 gw[V], gb[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int c4 = gl + j * G;
+    live[j] = c4 < C4;
+    if (LN) {
+      gw[j] = live[j] ? reinterpret_cast<const f32x4*>(ln_w)[c4] : f32x4{0, 0, 0, 0};
+      gb[j] = live[j] ? reinterpret_cast<const f32x4*>(ln_b)[c4] : f32x4{0, 0, 0, 0};
+    }
+  }
+
+  for (int64_t g = gid0; g < total; g += gstride) {
+    const int b = (int)(g / P);
+    int64_t p = g - (int64_t)b * P;
+    const int ox = (int)(p % w);
+    p /= w;
+    const int oy = (int)(p % h);
+    const int oz = (int)(p / h);
+
+    f32x4 v[8][V];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int iz = 2 * oz + (n >> 2), iy = 2 * oy + ((n >> 1) & 1), ix = 2 * ox + (n & 1);
+      const f32x4* row = reinterpret_cast<const f32x4*>(
+          x + ((((int64_t)b * D + iz) * H + iy) * W + ix) * C);
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[n][j] = live[j] ? row[gl + j * G] : f32x4{0, 0, 0, 0};
+    }
+    if (LN) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        float mean, rstd;
+        row_stats<G, V>(v[n], live, (float)C, ln_eps, mean, rstd);
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[n][j] = (v[n][j] - mean) * rstd * gw[j] + gb[j];
+      }
+    }
+    // butterflies along x (n bit0), y (bit1), z (bit2); slot index becomes the band index
+#pragma unroll
+    for (int bit = 1; bit < 8; bit <<= 1) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        if (!(n & bit)) {
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            f32x4 s0 = v[n][j], s1 = v[n | bit][j];
+            v[n][j] = s0 + s1;
+            v[n | bit][j] = s0 - s1;
+          }
+        }
+      }
+    }
+    const int64_t obase = g * C;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      f32x4* dst = reinterpret_cast<f32x4*>(bands + k * band_stride + obase);
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        if (live[j]) dst[gl + j * G] = v[k][j] * kHaar3;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Inverse: multi-level, fused.  One workgroup = one row (b, z1, y1, all x1) of the FINEST
+// detail grid and a block of CB channels.  Phase 1 (lanes over channels, matching the
+// channel-last detail bands of the forward kernel): every (c, x1) item rebuilds the level-
+// (L-1) LL value by walking the coarser levels, then the 8 outputs of its 2x2x2 cube into
+// LDS.  Phase 2 (lanes over x): rows of 2*w1 contiguous floats go to the NCDHW output.
+// ---------------------------------------------------------------------------------------
+constexpr int kMaxLevels = 4;
+struct IdwtArgs {
+  const float* ll;
+  int64_t ll_bstride;
+  const float* det[kMaxLevels * 7];
+  int64_t ds[kMaxLevels * 4];  // per level: batch, channel, z, (y*W_l+x) strides
+  float* out;
+  int64_t out_bstride;
+  int levels, B, C, d, h, w, CB;
+};
+
+__device__ __forceinline__ float idwt_coef(const IdwtArgs& a, int l, int k, int b, int c,
+                                           int z, int y, int x) {
+  const int64_t Wl = (int64_t)a.w << l;
+  const int64_t off = b * a.ds[4 * l] + c * a.ds[4 * l + 1] + z * a.ds[4 * l + 2] +
+                      ((int64_t)y * Wl + x) * a.ds[4 * l + 3];
+  return a.det[l * 7 + k][off];
+}
+
+__global__ __launch_bounds__(256) void idwt3d_haar_kernel(IdwtArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds_out[];  // [CB][2][2][2*w1]
+  const int L = a.levels;
+  const int w1 = a.w << (L - 1), h1 = a.h << (L - 1), d1 = a.d << (L - 1);
+  const int Wo = 2 * w1, Ho = 2 * h1, Do = 2 * d1;
+  int row = blockIdx.x;                 // over B * d1 * h1
+  const int y1 = row % h1;
+  row /= h1;
+  const int z1 = row % d1;
+  const int b = row / d1;
+  const int c0 = blockIdx.y * a.CB;
+  const int CB = min(a.CB, a.C - c0);
+
+  for (int item = threadIdx.x; item < CB * w1; item += blockDim.x) {
+    const int cl = item % CB, x1 = item / CB;
+    const int c = c0 + cl;
+    // coarsest LL (NCDHW, contiguous spatial)
+    const int zc = z1 >> (L - 1), yc = y1 >> (L - 1), xc = x1 >> (L - 1);
+    float ll = a.ll[b * a.ll_bstride + (int64_t)c * a.d * a.h * a.w +
+                    ((int64_t)zc * a.h + yc) * a.w + xc];
+    // levels 0..L-2 produce the LL of the next level at the ancestor of (z1,y1,x1)
+    for (int l = 0; l < L - 1; ++l) {
+      const int sh = L - 1 - l;             // ancestor at level l is (z1,y1,x1) >> sh
+      const int zl = z1 >> sh, yl = y1 >> sh, xl = x1 >> sh;
+      const int sz = (z1 >> (sh - 1)) & 1, sy = (y1 >> (sh - 1)) & 1, sx = (x1 >> (sh - 1)) & 1;
+      float acc = ll;
+#pragma unroll
+      for (int k = 1; k < 8; ++k) {
+        const int bd = (k >> 2) & 1, bh = (k >> 1) & 1, bw = k & 1;
+        const int neg = (bd & sz) ^ (bh & sy) ^ (bw & sx);
+        const float cv = idwt_coef(a, l, k - 1, b, c, zl, yl, xl);
+        acc += neg ? -cv : cv;
+      }
+      ll = acc * kHaar3;
+    }
+    // finest level: all 8 outputs of the cube via inverse butterflies
+    float v[8];
+    v[0] = ll;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v[k] = idwt_coef(a, L - 1, k - 1, b, c, z1, y1, x1);
+#pragma unroll
+    for (int bit = 1; bit < 8; bit <<= 1) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        if (!(n & bit)) {
+          const float s0 = v[n], s1 = v[n | bit];
+          v[n] = s0 + s1;
+          v[n | bit] = s0 - s1;
+        }
+      }
+    }
+    // slot n now holds sub-position (sz,sy,sx) = (n>>2, n>>1 & 1, n & 1)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int sz = n >> 2, sy = (n >> 1) & 1, sx = n & 1;
+      lds_out[((cl * 2 + sz) * 2 + sy) * Wo + 2 * x1 + sx] = v[n] * kHaar3;
+    }
+  }
+  __syncthreads();
+  const int64_t plane = (int64_t)Do * Ho * Wo;
+  float* obase = a.out + b * a.out_bstride;
+  const int nrows = CB * 4;
+  for (int item = threadIdx.x; item < nrows * Wo; item += blockDim.x) {
+    const int xo = item % Wo, r = item / Wo;
+    const int cl = r >> 2, sz = (r >> 1) & 1, sy = r & 1;
+    const int zo = 2 * z1 + sz, yo = 2 * y1 + sy;
+    obase[(int64_t)(c0 + cl) * plane + ((int64_t)zo * Ho + yo) * Wo + xo] = lds_out[r * Wo + xo];
+  }
+}
+
+}  // namespace wf
+
+using namespace wf;
+
+extern "C" int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float* ln_b,
+                                 float ln_eps, float* bands, int64_t B, int64_t C, int64_t D,
+                                 int64_t H, int64_t W, void* stream) {
+  WF_REQUIRE(B >= 1 && C >= 4 && C % 4 == 0, "need B >= 1 and C a positive multiple of 4");
+  WF_REQUIRE(D >= 2 && H >= 2 && W >= 2 && D % 2 == 0 && H % 2 == 0 && W % 2 == 0,
+             "D, H, W must be even (ptwt 'zero' mode with odd sizes is not supported)");
+  WF_REQUIRE((int64_t)B * D * H * W * C < ((int64_t)1 << 31) * 4, "tensor too large");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(bands);
+  const bool ln = ln_w != nullptr;
+  if (ln) WF_REQUIRE_PTR(ln_b);
+  const int64_t total = B * (D / 2) * (H / 2) * (W / 2);
+  return dispatch_gv(C / 4, [&](auto G_, auto V_) -> int {
+    constexpr int G = decltype(G_)::value, V = decltype(V_)::value;
+    const int gpb = 256 / G;
+    int64_t blocks = cdiv(total, gpb);
+    if (blocks > 8192) blocks = 8192;
+    if (ln)
+      hipLaunchKernelGGL((dwt3d_haar_fwd_kernel<G, V, true>), dim3((unsigned)blocks), dim3(256),
+                         0, (hipStream_t)stream, x, ln_w, ln_b, ln_eps, bands, (int)B, (int)C,
+                         (int)D, (int)H, (int)W);
+    else
+      hipLaunchKernelGGL((dwt3d_haar_fwd_kernel<G, V, false>), dim3((unsigned)blocks), dim3(256),
+                         0, (hipStream_t)stream, x, ln_w, ln_b, ln_eps, bands, (int)B, (int)C,
+                         (int)D, (int)H, (int)W);
+    return check_launch("wf_dwt3d_haar_fwd");
+  });
+}
+
+extern "C" int wf_idwt3d_haar(const float* ll, int64_t ll_bstride, const float* const* det,
+                              const int64_t* det_s, int levels, float* out, int64_t out_bstride,
+                              int64_t B, int64_t C, int64_t d, int64_t h, int64_t w,
+                              void* stream) {
+  WF_REQUIRE(levels >= 1 && levels <= kMaxLevels, "levels must be in [1, 4]");
+  WF_REQUIRE(B >= 1 && C >= 1 && d >= 1 && h >= 1 && w >= 1, "empty tensor");
+  WF_REQUIRE_PTR(ll);
+  WF_REQUIRE_PTR(det);
+  WF_REQUIRE_PTR(det_s);
+  WF_REQUIRE_PTR(out);
+  IdwtArgs a{};
+  a.ll = ll;
+  a.ll_bstride = ll_bstride;
+  for (int i = 0; i < levels * 7; ++i) {
+    WF_REQUIRE_PTR(det[i]);
+    a.det[i] = det[i];
+  }
+  for (int i = 0; i < levels * 4; ++i) a.ds[i] = det_s[i];
+  a.out = out;
+  a.out_bstride = out_bstride;
+  a.levels = levels;
+  a.B = (int)B;
+  a.C = (int)C;
+  a.d = (int)d;
+  a.h = (int)h;
+  a.w = (int)w;
+  const int64_t w1 = w << (levels - 1), h1 = h << (levels - 1), d1 = d << (levels - 1);
+  WF_REQUIRE(w1 <= 4096, "row too long");
+  // LDS budget 48 KB: CB * 8 * w1 floats
+  int64_t cb = (48 * 1024 / 4) / (8 * w1);
+  if (cb < 1) cb = 1;
+  if (cb > C) cb = C;
+  a.CB = (int)cb;
+  const size_t lds = (size_t)cb * 8 * w1 * sizeof(float);
+  dim3 grid((unsigned)(B * d1 * h1), (unsigned)cdiv(C, cb));
+  hipLaunchKernelGGL(idwt3d_haar_kernel, grid, dim3(256), lds, (hipStream_t)stream, a);
+  return check_launch("wf_idwt3d_haar");
+}

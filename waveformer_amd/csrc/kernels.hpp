@@ -1,0 +1,58 @@
+// kernels.hpp -- internal launchers shared by the C-ABI translation units.
+#pragma once
+#include "wf_common.hpp"
+
+namespace wf {
+
+// ---- A-resident MFMA GEMM:  out[m, n] = epilogue( sum_k A[m, k] * Wt[n, k] ) -------------
+// A rows are produced by a loader (gather + optional LayerNorm + bf16 rounding) into LDS once
+// per workgroup; the weight Wt [N][K] (bf16) streams from L2.
+enum RowMap { MAP_IDENTITY = 0, MAP_WINDOW = 1, MAP_MERGE = 2 };
+enum LnMode { LN_NONE = 0, LN_GIVEN = 1, LN_COMPUTE = 2 };
+enum EpiMode { EPI_STORE = 0, EPI_LN_GELU = 1, EPI_RESID = 2 };
+
+struct GemmArgs {
+  // ---- A loader
+  const void* a_src;     // fp32 or bf16 rows
+  int a_bf16;            // 1: a_src is bf16
+  int a_C;               // contiguous segment (channels) per source row
+  int a_nseg;            // K = a_nseg * a_C
+  int a_map;             // RowMap
+  int mB, mD, mH, mW, mws;  // geometry of the source raster for MAP_WINDOW / MAP_MERGE
+  int a_ln;              // LnMode
+  const float* a_stats;  // LN_GIVEN: (M, 2) {mean, rstd}
+  const float* a_ln_w;
+  const float* a_ln_b;
+  float a_eps;
+  // ---- B
+  const uint16_t* w;     // [N][K] bf16
+  // ---- problem
+  int64_t M;
+  int N, K;
+  // ---- epilogue
+  int epi;               // EpiMode
+  const float* bias;     // (N) or NULL
+  void* out;             // fp32 or bf16 rows of stride ldo
+  int out_bf16;
+  int64_t ldo;
+  const float* e_ln_w;   // EPI_LN_GELU: LN over N (gamma, beta, eps)
+  const float* e_ln_b;
+  float e_eps;
+  const float* r_x;      // EPI_RESID: residual rows (M, N) fp32
+  const float* r_stats;  //   if non-NULL also add LN(r_x; r_stats, r_ln_w, r_ln_b)
+  const float* r_ln_w;
+  const float* r_ln_b;
+};
+
+int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);
+
+// ---- windowed attention core over a (B_, N, 3C) bf16 qkv buffer -------------------------
+int launch_attn_core(const uint16_t* qkv, const float* bias, uint16_t* out, int64_t Bw, int N,
+                     int heads, int hd, float scale, hipStream_t s);
+
+// ---- depthwise 3^3 conv + bias + LayerNorm + GELU over a channel-last bf16 volume -------
+int launch_dwconv_ln_gelu(const uint16_t* in, const float* w, const float* b,
+                          const float* ln_w, const float* ln_b, float eps, uint16_t* out,
+                          int B, int Hd, int D, int H, int W, hipStream_t s);
+
+}  // namespace wf

@@ -1,0 +1,282 @@
+// misc.hip -- PatchEmbed (a10), the multi-scale fuse (a6) and the stage output projection
+// (a10, quirk Q5).  All three are HBM-streaming row kernels over channel-last data.
+#include <math.h>
+
+#include "rowgroup.hpp"
+
+namespace wf {
+
+// ---------------------------------------------------------------------------------------
+// PatchEmbed: Conv3d(Cin, Cout, k=2, s=2) on NCDHW input -> channel-last output.
+// monai/networks/blocks/patchembedding.py:214 via network_models/waveformer.py:281,286.
+// Workgroup = one output row (b, z, y): the 2x2 input rows of every input channel are staged
+// in LDS (coalesced along x), the weights next to them; outputs are written channel-last.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out, int Cin,
+                                                          int Cout, int D, int H, int W) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int W2 = 2 * W, H2 = 2 * H, D2 = 2 * D;
+  float* slab = sm;                       // [Cin][2][2][W2]
+  float* ws = slab + (size_t)Cin * 4 * W2;  // [Cout][Cin*8]
+  float* bs = ws + (size_t)Cout * Cin * 8;
+  int r = blockIdx.x;
+  const int y = r % H;
+  r /= H;
+  const int z = r % D;
+  const int b = r / D;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < Cin * 4 * W2; i += blockDim.x) {
+    const int xx = i % W2;
+    int t = i / W2;
+    const int dy = t & 1, dz = (t >> 1) & 1, ci = t >> 2;
+    slab[i] = x[((((int64_t)b * Cin + ci) * D2 + 2 * z + dz) * H2 + 2 * y + dy) * W2 + xx];
+  }
+  for (int i = tid; i < Cout * Cin * 8; i += blockDim.x) ws[i] = w[i];
+  for (int i = tid; i < Cout; i += blockDim.x) bs[i] = bias ? bias[i] : 0.f;
+  __syncthreads();
+  float* orow = out + (((int64_t)b * D + z) * H + y) * W * (int64_t)Cout;
+  for (int i = tid; i < W * Cout; i += blockDim.x) {
+    const int co = i % Cout, xo = i / Cout;
+    float acc = bs[co];
+    const float* wr = ws + (size_t)co * Cin * 8;
+    for (int ci = 0; ci < Cin; ++ci) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // weight index (dz, dy, dx) = (k>>2, k>>1 & 1, k & 1)
+        const int dz = k >> 2, dy = (k >> 1) & 1, dx = k & 1;
+        acc += wr[ci * 8 + k] * slab[((ci * 2 + dz) * 2 + dy) * W2 + 2 * xo + dx];
+      }
+    }
+    orow[i] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Multi-scale fuse: out = shortcut + sum_s trilinear(src_s -> (D,H,W)), plus LN stats.
+// Index/weight math is PyTorch's upsample_trilinear3d with align_corners=False and an
+// explicit output size: scale = in/out, src = max(scale*(o+0.5)-0.5, 0), i0 = floor(src),
+// i1 = i0 + (i0 < in-1), l1 = src - i0; identity when in == out.  The 8 corners are combined
+// depth-outermost like ATen's CPU Interpolate<3> recursion.
+// ---------------------------------------------------------------------------------------
+struct MsfuseArgs {
+  const float* src[4];
+  int sd[4], sh[4], sw[4];
+  int nsrc;
+  const float* shortcut;
+  float* out;
+  float* stats;
+  float eps;
+  int B, C, D, H, W;
+};
+
+__device__ __forceinline__ void lin_index(int o, int in, int out, int& i0, int& i1, float& l0,
+                                          float& l1) {
+  if (in == out) {
+    i0 = i1 = o;
+    l0 = 1.f;
+    l1 = 0.f;
+    return;
+  }
+  const float scale = (float)in / (float)out;
+  float s = __fmul_rn(scale, (float)o + 0.5f) - 0.5f;
+  s = s < 0.f ? 0.f : s;
+  i0 = min((int)floorf(s), in - 1);
+  l1 = fminf(fmaxf(s - (float)i0, 0.f), 1.f);
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l0 = 1.f - l1;
+}
+
+template <int G, int V>
+__global__ __launch_bounds__(256) void msfuse_kernel(MsfuseArgs a) {
+  const int C = a.C, C4 = C >> 2;
+  const int64_t P = (int64_t)a.D * a.H * a.W;
+  const int64_t total = (int64_t)a.B * P;
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
+  const int gpb = blockDim.x / G;
+  bool live[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) live[j] = gl + j * G < C4;
+  for (int64_t g = (int64_t)blockIdx.x * gpb + threadIdx.x / G; g < total;
+       g += (int64_t)gridDim.x * gpb) {
+    const int b = (int)(g / P);
+    int64_t p = g - (int64_t)b * P;
+    const int x = (int)(p % a.W);
+    p /= a.W;
+    const int y = (int)(p % a.H);
+    const int z = (int)(p / a.H);
+    f32x4 acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = f32x4{0, 0, 0, 0};
+    for (int s = 0; s < a.nsrc; ++s) {
+      const int sd = a.sd[s], sh = a.sh[s], sw = a.sw[s];
+      int z0, z1, y0, y1, x0, x1;
+      float wz0, wz1, wy0, wy1, wx0, wx1;
+      lin_index(z, sd, a.D, z0, z1, wz0, wz1);
+      lin_index(y, sh, a.H, y0, y1, wy0, wy1);
+      lin_index(x, sw, a.W, x0, x1, wx0, wx1);
+      const f32x4* base = reinterpret_cast<const f32x4*>(a.src[s] + (int64_t)b * sd * sh * sw * C);
+      auto at = [&](int zz, int yy, int xx, int c4) {
+        return base[(((int64_t)zz * sh + yy) * sw + xx) * C4 + c4];
+      };
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        if (!live[j]) continue;
+        const int c4 = gl + j * G;
+        const f32x4 t00 = at(z0, y0, x0, c4) * wx0 + at(z0, y0, x1, c4) * wx1;
+        const f32x4 t01 = at(z0, y1, x0, c4) * wx0 + at(z0, y1, x1, c4) * wx1;
+        const f32x4 t10 = at(z1, y0, x0, c4) * wx0 + at(z1, y0, x1, c4) * wx1;
+        const f32x4 t11 = at(z1, y1, x0, c4) * wx0 + at(z1, y1, x1, c4) * wx1;
+        const f32x4 t0 = t00 * wy0 + t01 * wy1;
+        const f32x4 t1 = t10 * wy0 + t11 * wy1;
+        acc[j] += t0 * wz0 + t1 * wz1;
+      }
+    }
+    const f32x4* sc = reinterpret_cast<const f32x4*>(a.shortcut + g * C);
+    f32x4* dst = reinterpret_cast<f32x4*>(a.out + g * C);
+    f32x4 v[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      v[j] = live[j] ? sc[gl + j * G] + acc[j] : f32x4{0, 0, 0, 0};
+      if (live[j]) dst[gl + j * G] = v[j];
+    }
+    if (a.stats) {
+      float mean, rstd;
+      row_stats<G, V>(v, live, (float)C, a.eps, mean, rstd);
+      if (gl == 0) {
+        a.stats[2 * g] = mean;
+        a.stats[2 * g + 1] = rstd;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// proj_out: channel-last (B, S, C) -> [non-affine LayerNorm] -> NCDHW (B, C, S).
+// Tile = TP positions of one batch; row groups normalise into an LDS [C][TP+1] image, then
+// lanes run along positions so every NCDHW row segment is written contiguously.
+// ---------------------------------------------------------------------------------------
+template <int G, int V>
+__global__ __launch_bounds__(256) void proj_out_kernel(const float* __restrict__ x,
+                                                       float* __restrict__ out, int normalize,
+                                                       float eps, int B, int C, int64_t S,
+                                                       int TP) {
+  extern __shared__ __attribute__((aligned(16))) float T[];  // [C][TP+1]
+  const int C4 = C >> 2;
+  const int64_t ntile = (S + TP - 1) / TP;
+  const int b = (int)(blockIdx.x / ntile);
+  const int64_t s0 = (blockIdx.x % ntile) * TP;
+  const int np = (int)min((int64_t)TP, S - s0);
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
+  const int gpb = blockDim.x / G;
+  bool live[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) live[j] = gl + j * G < C4;
+  for (int p = threadIdx.x / G; p < TP; p += gpb) {
+    const bool pv = p < np;  // uniform per group; padded groups still join the shuffles
+    const f32x4* row = reinterpret_cast<const f32x4*>(x + ((int64_t)b * S + s0 + (pv ? p : 0)) * C);
+    f32x4 v[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) v[j] = live[j] ? row[gl + j * G] : f32x4{0, 0, 0, 0};
+    if (normalize) {
+      float mean, rstd;
+      row_stats<G, V>(v, live, (float)C, eps, mean, rstd);
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[j] = (v[j] - mean) * rstd;
+    }
+    if (pv) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        if (!live[j]) continue;
+        const int c = 4 * (gl + j * G);
+        T[(c + 0) * (TP + 1) + p] = v[j].x;
+        T[(c + 1) * (TP + 1) + p] = v[j].y;
+        T[(c + 2) * (TP + 1) + p] = v[j].z;
+        T[(c + 3) * (TP + 1) + p] = v[j].w;
+      }
+    }
+  }
+  __syncthreads();
+  float* ob = out + (int64_t)b * C * S + s0;
+  for (int i = threadIdx.x; i < C * np; i += blockDim.x) {
+    const int c = i / np, p = i - c * np;
+    ob[(int64_t)c * S + p] = T[c * (TP + 1) + p];
+  }
+}
+
+}  // namespace wf
+
+using namespace wf;
+
+extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* bias, float* out,
+                                  int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H,
+                                  int64_t W, void* stream) {
+  WF_REQUIRE(B >= 1 && Cin >= 1 && Cout >= 1 && D >= 1 && H >= 1 && W >= 1, "empty tensor");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(w);
+  WF_REQUIRE_PTR(out);
+  const size_t lds = ((size_t)Cin * 8 * W + (size_t)Cout * Cin * 8 + Cout) * sizeof(float);
+  WF_REQUIRE(lds <= 64 * 1024, "PatchEmbed row tile exceeds 64 KB of LDS");
+  hipLaunchKernelGGL(patch_embed_kernel, dim3((unsigned)(B * D * H)), dim3(256), lds,
+                     (hipStream_t)stream, x, w, bias, out, (int)Cin, (int)Cout, (int)D, (int)H,
+                     (int)W);
+  return check_launch("wf_patch_embed_fwd");
+}
+
+extern "C" int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, int nsrc,
+                             const float* shortcut, float* out, float* stats, float ln_eps,
+                             int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                             void* stream) {
+  WF_REQUIRE(nsrc >= 0 && nsrc <= 4, "at most 4 sources");
+  WF_REQUIRE(B >= 1 && C >= 4 && C % 4 == 0, "C must be a positive multiple of 4");
+  WF_REQUIRE_PTR(shortcut);
+  WF_REQUIRE_PTR(out);
+  MsfuseArgs a{};
+  for (int s = 0; s < nsrc; ++s) {
+    WF_REQUIRE_PTR(src[s]);
+    a.src[s] = src[s];
+    a.sd[s] = (int)src_dhw[3 * s];
+    a.sh[s] = (int)src_dhw[3 * s + 1];
+    a.sw[s] = (int)src_dhw[3 * s + 2];
+    WF_REQUIRE(a.sd[s] >= 1 && a.sh[s] >= 1 && a.sw[s] >= 1, "empty source");
+  }
+  a.nsrc = nsrc;
+  a.shortcut = shortcut;
+  a.out = out;
+  a.stats = stats;
+  a.eps = ln_eps;
+  a.B = (int)B;
+  a.C = (int)C;
+  a.D = (int)D;
+  a.H = (int)H;
+  a.W = (int)W;
+  const int64_t total = B * D * H * W;
+  return dispatch_gv(C / 4, [&](auto G_, auto V_) -> int {
+    constexpr int G = decltype(G_)::value, V = decltype(V_)::value;
+    int64_t blocks = cdiv(total, 256 / G);
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL((msfuse_kernel<G, V>), dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, a);
+    return check_launch("wf_msfuse_fwd");
+  });
+}
+
+extern "C" int wf_proj_out_fwd(const float* x, float* out, int normalize, float eps, int64_t B,
+                               int64_t C, int64_t S, void* stream) {
+  WF_REQUIRE(B >= 1 && S >= 1 && C >= 4 && C % 4 == 0, "C must be a positive multiple of 4");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(out);
+  int64_t TP = (48 * 1024 / 4) / C - 1;  // LDS [C][TP+1] within 48 KB
+  if (TP > 64) TP = 64;
+  if (TP < 1) TP = 1;
+  if (TP > S) TP = S;
+  const size_t lds = (size_t)C * (TP + 1) * sizeof(float);
+  const int64_t blocks = B * cdiv(S, TP);
+  return dispatch_gv(C / 4, [&](auto G_, auto V_) -> int {
+    constexpr int G = decltype(G_)::value, V = decltype(V_)::value;
+    hipLaunchKernelGGL((proj_out_kernel<G, V>), dim3((unsigned)blocks), dim3(256), lds,
+                       (hipStream_t)stream, x, out, normalize, eps, (int)B, (int)C, S, (int)TP);
+    return check_launch("wf_proj_out_fwd");
+  });
+}

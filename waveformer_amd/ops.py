@@ -1,0 +1,304 @@
+"""Python wrappers over the C-ABI (include/waveformer_hip.h).
+
+Each wrapper validates device / dtype / shape / contiguity on the host (the C side re-checks
+sizes), allocates outputs with the PyTorch caching allocator, and launches on
+torch.cuda.current_stream().  They are the only way the modules in
+`waveformer_amd.network_models` reach the GPU kernels; there is no CPU or eager-PyTorch
+fallback -- a CPU tensor or a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import weakref
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+
+DETAIL_KEYS = ("aad", "ada", "add", "daa", "dad", "dda", "ddd")  # ptwt key order, band 1..7
+
+
+# ------------------------------------------------------------------------------------------
+# helpers
+# ------------------------------------------------------------------------------------------
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _check(t: torch.Tensor, name: str, dtype=torch.float32, contiguous=True) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor, got {type(t)}")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{name}: waveformer_amd kernels run on the GPU only (got a {t.device} tensor); "
+            "move the module and inputs to cuda")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if contiguous and not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous tensor")
+
+
+_bf16_cache: "weakref.WeakKeyDictionary[torch.Tensor, Tuple[int, int, torch.Tensor]]" = \
+    weakref.WeakKeyDictionary()
+
+
+def bf16_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None) -> torch.Tensor:
+    """bf16 copy of an fp32 weight (made by the wf_cast kernel), cached until p changes."""
+    key = p
+    ent = _bf16_cache.get(key)
+    ver = p._version
+    if ent is not None and ent[0] == ver and ent[1] == p.data_ptr():
+        return ent[2]
+    src = p.detach()
+    _check(src, "weight")
+    out = torch.empty(src.shape if shape is None else shape, dtype=torch.bfloat16,
+                      device=src.device)
+    _lib.call("wf_cast_f32_to_bf16", src.data_ptr(), out.data_ptr(), src.numel(), _stream())
+    _bf16_cache[key] = (ver, p.data_ptr(), out)
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# a10: PatchEmbed conv
+# ------------------------------------------------------------------------------------------
+def patch_embed(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """Conv3d(k=2, s=2) NCDHW -> channel-last (B, D/2, H/2, W/2, Cout)."""
+    _check(x, "x")
+    _check(weight, "weight")
+    B, Cin, D2, H2, W2 = x.shape
+    Cout = weight.shape[0]
+    if tuple(weight.shape) != (Cout, Cin, 2, 2, 2):
+        raise ValueError(f"patch_embed: weight {tuple(weight.shape)} is not ({Cout},{Cin},2,2,2)")
+    if D2 % 2 or H2 % 2 or W2 % 2:
+        raise ValueError("patch_embed: spatial sizes must be even (PatchEmbed pads otherwise)")
+    if bias is not None:
+        _check(bias, "bias")
+    out = torch.empty((B, D2 // 2, H2 // 2, W2 // 2, Cout), dtype=torch.float32, device=x.device)
+    _lib.call("wf_patch_embed_fwd", x.data_ptr(), weight.data_ptr(), _ptr(bias), out.data_ptr(),
+              B, Cin, Cout, D2 // 2, H2 // 2, W2 // 2, _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# a1: Haar analysis
+# ------------------------------------------------------------------------------------------
+def dwt3d_haar(x_cl: torch.Tensor, ln: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None
+               ) -> torch.Tensor:
+    """1-level Haar DWT of a channel-last (B,D,H,W,C) volume -> bands (8,B,D/2,H/2,W/2,C)."""
+    _check(x_cl, "x")
+    B, D, H, W, C = x_cl.shape
+    bands = torch.empty((8, B, D // 2, H // 2, W // 2, C), dtype=torch.float32, device=x_cl.device)
+    lw = lb = None
+    eps = 0.0
+    if ln is not None:
+        lw, lb, eps = ln
+        _check(lw, "ln_w")
+        _check(lb, "ln_b")
+    _lib.call("wf_dwt3d_haar_fwd", x_cl.data_ptr(), _ptr(lw), _ptr(lb), float(eps),
+              bands.data_ptr(), B, C, D, H, W, _stream())
+    return bands
+
+
+def bands_to_coeffs(bands: torch.Tensor) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+    """(8,B,d,h,w,C) bands -> (LL, detail dict) as NCDHW-shaped (channel-last strided) views,
+    the structure ptwt.wavedec3(level=1) returns (wave_helper.py:350-353)."""
+    ll = bands[0].permute(0, 4, 1, 2, 3)
+    det = {k: bands[i + 1].permute(0, 4, 1, 2, 3) for i, k in enumerate(DETAIL_KEYS)}
+    return ll, det
+
+
+# ------------------------------------------------------------------------------------------
+# a11: Haar synthesis
+# ------------------------------------------------------------------------------------------
+def idwt3d_haar(ll: torch.Tensor, details: Sequence[Dict[str, torch.Tensor]],
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ptwt.waverec3((ll,) + tuple(details), 'db1') for NCDHW-shaped tensors of any strides
+    inside each (B, C, ...) batch with contiguous spatial (y, x) rows or channel-last layout.
+
+    `details` is coarse -> fine.  If `out` is given (B, >=C, 2^L d, 2^L h, 2^L w) with a
+    contiguous (C, D, H, W) block per batch, the result is written into its first C channels
+    (this is how the decoder fuses torch.cat((out, skip), 1), idwt_upsample.py:163)."""
+    if ll.device.type != "cuda":
+        raise RuntimeError("idwt3d_haar: GPU tensors only")
+    if ll.dtype != torch.float32:
+        raise TypeError("idwt3d_haar: float32 only")
+    B, C, d, h, w = ll.shape
+    if ll.stride()[1:] != (d * h * w, h * w, w, 1):
+        ll = ll.contiguous()
+    L = len(details)
+    if not 1 <= L <= 4:
+        raise ValueError("idwt3d_haar: 1..4 detail levels supported")
+    ptrs: List[int] = []
+    strides: List[int] = []
+    keep = []
+    for l, dct in enumerate(details):
+        s = 2 ** l
+        exp = (B, C, d * s, h * s, w * s)
+        ts = []
+        for k in DETAIL_KEYS:
+            t = dct[k]
+            if tuple(t.shape) != exp:
+                raise ValueError(f"idwt3d_haar: level {l} key {k} has shape {tuple(t.shape)}, expected {exp}")
+            if t.device != ll.device or t.dtype != torch.float32:
+                raise TypeError("idwt3d_haar: detail tensors must be float32 on the same GPU")
+            ts.append(t)
+
+        def pattern(t):  # element (b,c,z,y,x) at b*s0 + c*s1 + z*s2 + (y*W_l + x)*s3
+            st = t.stride()
+            return (st[0], st[1], st[2], st[4]) if st[3] == exp[4] * st[4] else None
+
+        pats = [pattern(t) for t in ts]
+        if any(p is None for p in pats) or len(set(pats)) != 1:
+            ts = [t.contiguous() for t in ts]
+            pats = [pattern(t) for t in ts]
+        keep.extend(ts)
+        ptrs.extend(t.data_ptr() for t in ts)
+        strides.extend(pats[0])
+    Do, Ho, Wo = d * 2 ** L, h * 2 ** L, w * 2 ** L
+    if out is None:
+        out = torch.empty((B, C, Do, Ho, Wo), dtype=torch.float32, device=ll.device)
+    else:
+        if out.shape[0] != B or out.shape[1] < C or tuple(out.shape[2:]) != (Do, Ho, Wo):
+            raise ValueError(f"idwt3d_haar: out {tuple(out.shape)} does not fit ({B},{C},{Do},{Ho},{Wo})")
+        if out.stride()[1:] != (Do * Ho * Wo, Ho * Wo, Wo, 1):
+            raise ValueError("idwt3d_haar: out must be contiguous inside each batch")
+    arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+    sarr = (ctypes.c_int64 * len(strides))(*strides)
+    _lib.call("wf_idwt3d_haar", ll.data_ptr(), ll.stride(0), arr, sarr, L, out.data_ptr(),
+              out.stride(0), B, C, d, h, w, _stream())
+    del keep
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# a2/a3: attention
+# ------------------------------------------------------------------------------------------
+def rel_pos_bias(table: torch.Tensor, index: torch.Tensor) -> torch.Tensor:
+    """Dense (heads, N, N) relative-position bias: table[index.view(-1)] (attention.py:94-97)."""
+    _check(table, "relative_position_bias_table")
+    _check(index, "relative_position_index", dtype=torch.int64)
+    T, heads = table.shape
+    N = index.shape[0]
+    out = torch.empty((heads, N, N), dtype=torch.float32, device=table.device)
+    _lib.call("wf_rel_pos_bias", table.data_ptr(), index.data_ptr(), out.data_ptr(), N, heads, T,
+              _stream())
+    return out
+
+
+def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torch.Tensor],
+                     bias: torch.Tensor, wproj: torch.Tensor, bproj: Optional[torch.Tensor],
+                     ws: int, heads: int, scale: float,
+                     ln: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None) -> torch.Tensor:
+    """window_partition + Attention.forward + reshape-reverse (Q1) over a channel-last raster.
+    Returns (B, D1, H1, W1, C) whose rows are the window-major attention outputs."""
+    _check(x_cl, "x")
+    B, D1, H1, W1, C = x_cl.shape
+    wq = bf16_weight(wqkv)
+    wp = bf16_weight(wproj)
+    if bqkv is not None:
+        _check(bqkv, "qkv.bias")
+    if bproj is not None:
+        _check(bproj, "proj.bias")
+    _check(bias, "bias")
+    N = ws ** 3
+    if tuple(bias.shape) != (heads, N, N):
+        raise ValueError(f"window_attention: bias {tuple(bias.shape)} != ({heads},{N},{N})")
+    lw = lb = None
+    eps = 0.0
+    if ln is not None:
+        lw, lb, eps = ln
+    out = torch.empty_like(x_cl)
+    wsb = _lib.query("wf_window_attention_workspace_bytes", B, C, D1, H1, W1)
+    work = torch.empty(wsb, dtype=torch.uint8, device=x_cl.device)
+    _lib.call("wf_window_attention_fwd", x_cl.data_ptr(), _ptr(lw), _ptr(lb), float(eps),
+              wq.data_ptr(), _ptr(bqkv), bias.data_ptr(), wp.data_ptr(), _ptr(bproj),
+              out.data_ptr(), work.data_ptr(), B, C, D1, H1, W1, ws, heads, float(scale),
+              _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# a6: multi-scale fuse
+# ------------------------------------------------------------------------------------------
+def msfuse(srcs: Sequence[torch.Tensor], shortcut: torch.Tensor, ln_eps: Optional[float]
+           ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """shortcut + sum_s trilinear(src_s) (align_corners=False), channel-last; optional stats."""
+    _check(shortcut, "shortcut")
+    B, D, H, W, C = shortcut.shape
+    if len(srcs) > 4:
+        raise ValueError("msfuse: at most 4 sources")
+    dhw: List[int] = []
+    for s in srcs:
+        _check(s, "src")
+        if s.shape[0] != B or s.shape[4] != C:
+            raise ValueError("msfuse: source batch/channels mismatch")
+        dhw.extend(s.shape[1:4])
+    out = torch.empty_like(shortcut)
+    stats = None
+    if ln_eps is not None:
+        stats = torch.empty((B * D * H * W, 2), dtype=torch.float32, device=shortcut.device)
+    arr = (ctypes.c_void_p * max(1, len(srcs)))(*[s.data_ptr() for s in srcs])
+    darr = (ctypes.c_int64 * max(1, len(dhw)))(*dhw)
+    _lib.call("wf_msfuse_fwd", arr, darr, len(srcs), shortcut.data_ptr(), out.data_ptr(),
+              _ptr(stats), float(ln_eps or 0.0), B, C, D, H, W, _stream())
+    return out, stats
+
+
+# ------------------------------------------------------------------------------------------
+# a7/a8: CCF_FFN (+ norm2 / double residual)
+# ------------------------------------------------------------------------------------------
+def ccf_ffn(xh: torch.Tensor, stats: Optional[torch.Tensor], norm2: Optional[torch.nn.Module],
+            mlp: torch.nn.Module) -> torch.Tensor:
+    """Block path (stats given): xh + n2 + ffn(n2), n2 = norm2(xh).  Bare (stats None): xh + ffn(xh)."""
+    _check(xh, "x")
+    B, D, H, W, C = xh.shape
+    hid = mlp.C_hid
+    pw = bf16_weight(mlp.pwconv.weight, (hid, C))
+    fc = bf16_weight(mlp.fc.weight)
+    out = torch.empty_like(xh)
+    wsb = _lib.query("wf_ccf_ffn_workspace_bytes", B, C, hid, D, H, W)
+    work = torch.empty(wsb, dtype=torch.uint8, device=xh.device)
+    n2w = n2b = None
+    if stats is not None:
+        n2w, n2b = norm2.weight, norm2.bias
+    _lib.call("wf_ccf_ffn_fwd", xh.data_ptr(), _ptr(stats), _ptr(n2w), _ptr(n2b),
+              pw.data_ptr(), _ptr(mlp.pwconv.bias), mlp.norm1.weight.data_ptr(),
+              mlp.norm1.bias.data_ptr(), float(mlp.norm1.eps), mlp.dwconv.weight.data_ptr(),
+              mlp.dwconv.bias.data_ptr(), mlp.norm2.weight.data_ptr(), mlp.norm2.bias.data_ptr(),
+              float(mlp.norm2.eps), fc.data_ptr(), _ptr(mlp.fc.bias), out.data_ptr(),
+              work.data_ptr(), B, C, hid, D, H, W, _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# a9: PatchMerging
+# ------------------------------------------------------------------------------------------
+def patch_merging(x_cl: torch.Tensor, norm: torch.nn.LayerNorm, reduction: torch.nn.Linear
+                  ) -> torch.Tensor:
+    _check(x_cl, "x")
+    B, D, H, W, C = x_cl.shape
+    red = bf16_weight(reduction.weight)
+    out = torch.empty((B, D // 2, H // 2, W // 2, 2 * C), dtype=torch.float32, device=x_cl.device)
+    _lib.call("wf_patch_merging_fwd", x_cl.data_ptr(), norm.weight.data_ptr(),
+              norm.bias.data_ptr(), float(norm.eps), red.data_ptr(), out.data_ptr(), B, C, D, H,
+              W, _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# a10: proj_out
+# ------------------------------------------------------------------------------------------
+def proj_out(x_cl: torch.Tensor, normalize: bool, eps: float = 1e-5) -> torch.Tensor:
+    """(B,D,H,W,C) -> NCDHW (B,C,D,H,W), non-affine LayerNorm over C when normalize."""
+    _check(x_cl, "x")
+    B, D, H, W, C = x_cl.shape
+    out = torch.empty((B, C, D, H, W), dtype=torch.float32, device=x_cl.device)
+    _lib.call("wf_proj_out_fwd", x_cl.data_ptr(), out.data_ptr(), int(bool(normalize)),
+              float(eps), B, C, D * H * W, _stream())
+    return out
