@@ -115,10 +115,13 @@ int wf_window_attention_fwd(const float* x, const float* ln_w, const float* ln_b
  * (wave_helper.py:509) needs.
  * src[s]: channel-last (B, sd[s], sh[s], sw[s], C), s < nsrc <= 4; a source whose size equals
  * (D,H,W) is added as-is (level-0 path, wave_helper.py:505).  shortcut, out: (B, D, H, W, C).
- * stats: (B*D*H*W, 2) = {mean, rstd} of out rows with eps ln_eps.                          */
+ * stats: (B*D*H*W, 2) = {mean, rstd} of out rows with eps ln_eps (NULL: not computed).
+ * branch_scale: NULL, or (B) per-sample factors applied to the fused attention branch --
+ * the DropPath (timm, train mode) of wave_helper.py:508 as a per-sample keep/(1-p) mask.   */
 int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, int nsrc,
-                  const float* shortcut, float* out, float* stats, float ln_eps, int64_t B,
-                  int64_t C, int64_t D, int64_t H, int64_t W, void* stream);
+                  const float* shortcut, const float* branch_scale, float* out, float* stats,
+                  float ln_eps, int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                  void* stream);
 
 /* ---- a7/a8: CCF_FFN + the Block's norm2 and double residual (quirk Q4) ---------------- */
 /* Replaces attn_fused + mlp(norm2(attn_fused)) (wave_helper.py:509) with CCF_FFN.forward
@@ -128,23 +131,26 @@ int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, int nsrc,
  * n2 = LN(xh; stats, n2_w, n2_b) and out = xh + n2 + ffn(n2) (Block, Q4);
  * if stats == NULL the input is xh itself and out = xh + ffn(xh) (bare CCF_FFN.forward).
  * pw_bf16 (4C, C), pw_b (4C), ln1_w/b (4C), dw_w (4C, 27) fp32, dw_b (4C), ln2_w/b (4C),
- * fc_bf16 (C, 4C), fc_b (C).  workspace: wf_ccf_ffn_workspace_bytes(...) bytes.          */
+ * fc_bf16 (C, 4C), fc_b (C).  branch_scale: NULL or (B) per-sample DropPath factors on the
+ * FFN branch (wave_helper.py:509).  workspace: wf_ccf_ffn_workspace_bytes(...) bytes.       */
 int64_t wf_ccf_ffn_workspace_bytes(int64_t B, int64_t C, int64_t hidden, int64_t D, int64_t H,
                                    int64_t W);
 int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* n2_w, const float* n2_b,
                    const uint16_t* pw_bf16, const float* pw_b, const float* ln1_w,
                    const float* ln1_b, float eps1, const float* dw_w, const float* dw_b,
                    const float* ln2_w, const float* ln2_b, float eps2,
-                   const uint16_t* fc_bf16, const float* fc_b, float* out, void* workspace,
+                   const uint16_t* fc_bf16, const float* fc_b, const float* branch_scale,
+                   float* out, void* workspace,
                    int64_t B, int64_t C, int64_t hidden, int64_t D, int64_t H, int64_t W,
                    void* stream);
 
 /* ---- a9: PatchMerging (quirk Q3) ------------------------------------------------------ */
 /* Replaces PatchMerging.forward (wave_helper.py:173-194): the 8-way strided gather with its
- * duplicated sub-lattices, LN(8C, eps) and Linear(8C -> 2C, no bias).
+ * duplicated sub-lattices, LN(8C, eps) and Linear(8C -> 2C, no bias).  v2 != 0 selects
+ * PatchMergingV2.forward's itertools.product order instead (wave_helper.py:147-167).
  * x: channel-last (B, D, H, W, C) (D, H, W even); out: channel-last (B, D/2, H/2, W/2, 2C). */
 int wf_patch_merging_fwd(const float* x, const float* ln_w, const float* ln_b, float eps,
-                         const uint16_t* red_bf16, float* out, int64_t B, int64_t C,
+                         const uint16_t* red_bf16, int v2, float* out, int64_t B, int64_t C,
                          int64_t D, int64_t H, int64_t W, void* stream);
 
 /* ---- a10: stage output projection (quirk Q5) ----------------------------------------- */

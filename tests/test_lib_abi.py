@@ -1,0 +1,44 @@
+"""CPU: the C-ABI library loads and exports every entry point include/waveformer_hip.h declares
+(no compute is launched -- there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from waveformer_amd import _lib
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                      "waveformer_hip.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(wf_\w+)\s*\(", src, re.M)))
+
+
+def test_header_and_binding_agree():
+    syms = declared_symbols()
+    assert len(syms) >= 14
+    assert sorted(_lib.SIGNATURES) == syms
+
+
+def test_library_exports_every_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("libwaveformer_hip.so is not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    lib = _lib.load()
+    assert lib.wf_abi_version() == 1
+
+
+def test_shape_errors_are_reported_without_a_gpu():
+    # argument validation runs before any HIP call, so it works on a CPU-only host
+    lib = _lib.load()
+    rc = lib.wf_dwt3d_haar_fwd(None, None, None, 0.0, None, 1, 6, 3, 4, 4, None)
+    assert rc < 0
+    assert b"even" in lib.wf_last_error() or b"multiple of 4" in lib.wf_last_error()
+    with pytest.raises(RuntimeError, match="wf_proj_out_fwd"):
+        _lib.call("wf_proj_out_fwd", None, None, 1, 1e-5, 1, 6, 8, None)
+    assert _lib.query("wf_window_attention_workspace_bytes", 1, 48, 32, 32, 32) >= 32768 * 48 * 8

@@ -33,11 +33,11 @@ SIGNATURES = {
     "wf_window_attention_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64]),
     "wf_window_attention_fwd": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P,
                                      _I64, _I64, _I64, _I64, _I64, _I64, _I64, _F, _P]),
-    "wf_msfuse_fwd": (_I, [_P, _P, _I, _P, _P, _P, _F, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_msfuse_fwd": (_I, [_P, _P, _I, _P, _P, _P, _P, _F, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_ccf_ffn_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I64]),
     "wf_ccf_ffn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _F, _P, _P,
-                            _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
-    "wf_patch_merging_fwd": (_I, [_P, _P, _P, _F, _P, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+                            _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_patch_merging_fwd": (_I, [_P, _P, _P, _F, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_proj_out_fwd": (_I, [_P, _P, _I, _F, _I64, _I64, _I64, _P]),
 }
 

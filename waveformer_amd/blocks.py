@@ -1,0 +1,161 @@
+"""Decoder building blocks with the module names / state_dict keys of the MONAI blocks the
+reference uses (vendored MONAI, monai/networks/blocks/{dynunet_block,unetr_block}.py).
+
+These are the decoder's full-resolution 3^3 convolutions ("next"): in this
+round they run as PyTorch-ROCm convolutions (MIOpen) on the GPU; only the wavelet synthesis
+between them (UnetrIDWTBlock) is a waveformer_amd kernel.  norm_name is always "instance"
+(InstanceNorm3d, affine=False) and the activation LeakyReLU(0.01), as Waveformer builds them.
+"""
+from __future__ import annotations
+
+from typing import Sequence, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+
+def _norm(norm_name, channels: int) -> nn.Module:
+    name = norm_name[0] if isinstance(norm_name, tuple) else norm_name
+    kw = dict(norm_name[1]) if isinstance(norm_name, tuple) and len(norm_name) > 1 else {}
+    name = str(name).lower()
+    if name == "instance":
+        return nn.InstanceNorm3d(channels, **kw)
+    if name == "batch":
+        return nn.BatchNorm3d(channels, **kw)
+    if name == "group":
+        return nn.GroupNorm(num_channels=channels, **kw)
+    raise ValueError(f"unsupported norm_name {norm_name!r}")
+
+
+class Convolution(nn.Sequential):
+    """monai Convolution with conv_only / act=None / norm=None: a container whose single child
+    is named `conv` (state_dict key `<name>.conv.weight`)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride, padding, bias,
+                 is_transposed=False, output_padding=0):
+        super().__init__()
+        if is_transposed:
+            conv = nn.ConvTranspose3d(in_channels, out_channels, kernel_size, stride, padding,
+                                      output_padding=output_padding, bias=bias)
+        else:
+            conv = nn.Conv3d(in_channels, out_channels, kernel_size, stride, padding, bias=bias)
+        self.add_module("conv", conv)
+
+
+def get_conv_layer(spatial_dims: int, in_channels: int, out_channels: int,
+                   kernel_size: Union[Sequence[int], int] = 3, stride: Union[Sequence[int], int] = 1,
+                   bias: bool = False, conv_only: bool = True, is_transposed: bool = False,
+                   **_unused) -> Convolution:
+    """monai.networks.blocks.dynunet_block.get_conv_layer (dynunet_block.py:270-301) for 3D,
+    act/norm/dropout None: padding (k - s + 1) // 2, output_padding 2p + s - k."""
+    if spatial_dims != 3:
+        raise ValueError("only 3D is supported")
+    k = kernel_size if isinstance(kernel_size, int) else kernel_size[0]
+    s = stride if isinstance(stride, int) else stride[0]
+    pad = (k - s + 1) // 2
+    if pad < 0:
+        raise AssertionError("padding value should not be negative")
+    op = 2 * pad + s - k if is_transposed else 0
+    return Convolution(in_channels, out_channels, kernel_size, stride, pad, bias, is_transposed, op)
+
+
+class UnetResBlock(nn.Module):
+    """conv3-norm-lrelu-conv3-norm (+ 1x1 conv + norm residual when channels change) -> lrelu
+    (monai dynunet_block.py:25-111)."""
+
+    def __init__(self, spatial_dims: int, in_channels: int, out_channels: int,
+                 kernel_size=3, stride=1, norm_name: Union[Tuple, str] = "instance",
+                 act_name=("leakyrelu", {"inplace": True, "negative_slope": 0.01}), dropout=None):
+        super().__init__()
+        self.conv1 = get_conv_layer(spatial_dims, in_channels, out_channels, kernel_size, stride)
+        self.conv2 = get_conv_layer(spatial_dims, out_channels, out_channels, kernel_size, 1)
+        self.lrelu = nn.LeakyReLU(negative_slope=0.01, inplace=True)
+        self.norm1 = _norm(norm_name, out_channels)
+        self.norm2 = _norm(norm_name, out_channels)
+        s = stride if isinstance(stride, int) else max(stride)
+        self.downsample = in_channels != out_channels or s != 1
+        if self.downsample:
+            self.conv3 = get_conv_layer(spatial_dims, in_channels, out_channels, 1, stride)
+            self.norm3 = _norm(norm_name, out_channels)
+
+    def forward(self, inp):
+        out = self.lrelu(self.norm1(self.conv1(inp)))
+        out = self.norm2(self.conv2(out))
+        res = self.norm3(self.conv3(inp)) if self.downsample else inp
+        return self.lrelu(out + res)
+
+
+class UnetBasicBlock(nn.Module):
+    """conv3-norm-lrelu-conv3-norm-lrelu (monai dynunet_block.py:114-185)."""
+
+    def __init__(self, spatial_dims: int, in_channels: int, out_channels: int, kernel_size=3,
+                 stride=1, norm_name: Union[Tuple, str] = "instance", act_name=None, dropout=None):
+        super().__init__()
+        self.conv1 = get_conv_layer(spatial_dims, in_channels, out_channels, kernel_size, stride)
+        self.conv2 = get_conv_layer(spatial_dims, out_channels, out_channels, kernel_size, 1)
+        self.lrelu = nn.LeakyReLU(negative_slope=0.01, inplace=True)
+        self.norm1 = _norm(norm_name, out_channels)
+        self.norm2 = _norm(norm_name, out_channels)
+
+    def forward(self, inp):
+        out = self.lrelu(self.norm1(self.conv1(inp)))
+        return self.lrelu(self.norm2(self.conv2(out)))
+
+
+class UnetOutBlock(nn.Module):
+    """1x1x1 conv with bias (monai dynunet_block.py:188-210)."""
+
+    def __init__(self, spatial_dims: int, in_channels: int, out_channels: int, dropout=None):
+        super().__init__()
+        self.conv = get_conv_layer(spatial_dims, in_channels, out_channels, 1, 1, bias=True)
+
+    def forward(self, inp):
+        return self.conv(inp)
+
+
+class UnetrBasicBlock(nn.Module):
+    """monai unetr_block.py:209-259: `layer` = UnetResBlock or UnetBasicBlock."""
+
+    def __init__(self, spatial_dims: int, in_channels: int, out_channels: int, kernel_size,
+                 stride, norm_name, res_block: bool = False):
+        super().__init__()
+        cls = UnetResBlock if res_block else UnetBasicBlock
+        self.layer = cls(spatial_dims, in_channels, out_channels, kernel_size, stride, norm_name)
+
+    def forward(self, inp):
+        return self.layer(inp)
+
+
+class UnetrUpBlock(nn.Module):
+    """monai unetr_block.py:22-86: transposed conv (no bias), concat skip, conv block."""
+
+    def __init__(self, spatial_dims: int, in_channels: int, out_channels: int, kernel_size,
+                 upsample_kernel_size, norm_name, res_block: bool = False):
+        super().__init__()
+        self.transp_conv = get_conv_layer(spatial_dims, in_channels, out_channels,
+                                          upsample_kernel_size, upsample_kernel_size,
+                                          is_transposed=True)
+        cls = UnetResBlock if res_block else UnetBasicBlock
+        self.conv_block = cls(spatial_dims, 2 * out_channels, out_channels, kernel_size, 1,
+                              norm_name)
+
+    def forward(self, inp, skip):
+        out = self.transp_conv(inp)
+        return self.conv_block(torch.cat((out, skip), dim=1))
+
+
+class PatchEmbed(nn.Module):
+    """monai.networks.blocks.PatchEmbed (patchembedding.py:147-225) as MultiscaleTransformer
+    builds it: `proj` = Conv3d(k = s = patch_size), optional `norm`.  The forward used by the
+    encoder is ops.patch_embed (HIP); this module only owns the parameters."""
+
+    def __init__(self, patch_size=2, in_chans: int = 1, embed_dim: int = 48, norm_layer=None,
+                 spatial_dims: int = 3):
+        super().__init__()
+        if spatial_dims != 3:
+            raise ValueError("only 3D is supported")
+        ps = patch_size if isinstance(patch_size, int) else patch_size[0]
+        self.patch_size = (ps, ps, ps)
+        self.embed_dim = embed_dim
+        self.proj = nn.Conv3d(in_chans, embed_dim, kernel_size=ps, stride=ps)
+        self.norm = norm_layer(embed_dim) if norm_layer is not None else None

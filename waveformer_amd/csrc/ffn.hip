@@ -148,7 +148,8 @@ extern "C" int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* 
                               const float* ln1_w, const float* ln1_b, float eps1,
                               const float* dw_w, const float* dw_b, const float* ln2_w,
                               const float* ln2_b, float eps2, const uint16_t* fc_bf16,
-                              const float* fc_b, float* out, void* workspace, int64_t B,
+                              const float* fc_b, const float* branch_scale, float* out,
+                              void* workspace, int64_t B,
                               int64_t C, int64_t hidden, int64_t D, int64_t H, int64_t W,
                               void* stream) {
   WF_REQUIRE(B >= 1 && D >= 1 && H >= 1 && W >= 1, "empty volume");
@@ -218,6 +219,8 @@ extern "C" int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* 
   f.r_stats = stats;
   f.r_ln_w = n2_w;
   f.r_ln_b = n2_b;
+  f.r_scale = branch_scale;
+  f.rows_per_sample = D * H * W;
   f.out = out;
   f.out_bf16 = 0;
   f.ldo = C;
@@ -225,7 +228,8 @@ extern "C" int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* 
 }
 
 extern "C" int wf_patch_merging_fwd(const float* x, const float* ln_w, const float* ln_b,
-                                    float eps, const uint16_t* red_bf16, float* out, int64_t B,
+                                    float eps, const uint16_t* red_bf16, int v2, float* out,
+                                    int64_t B,
                                     int64_t C, int64_t D, int64_t H, int64_t W, void* stream) {
   WF_REQUIRE(B >= 1 && C % 8 == 0 && C >= 8, "C must be a positive multiple of 8");
   WF_REQUIRE(D % 2 == 0 && H % 2 == 0 && W % 2 == 0 && D >= 2 && H >= 2 && W >= 2,
@@ -241,6 +245,10 @@ extern "C" int wf_patch_merging_fwd(const float* x, const float* ln_w, const flo
   g.a_C = (int)C;
   g.a_nseg = 8;
   g.a_map = MAP_MERGE;
+  // (d,h,w) offsets of the 8 sub-lattices, one nibble each (bit2 d, bit1 h, bit0 w):
+  //   PatchMerging (wave_helper.py:183-190, quirk Q3): 000,100,010,001,101,010,001,111
+  //   PatchMergingV2 (itertools.product, :154-156):     000,001,010,011,100,101,110,111
+  g.merge_code = v2 ? 0x76543210 : 0x71251240;
   g.mB = (int)B;
   g.mD = (int)D;
   g.mH = (int)H;

@@ -69,13 +69,10 @@ struct RowSource {
   }
   __device__ int64_t offset(int k) const {
     if (g.a_map == MAP_MERGE) {
-      // PatchMerging.forward sub-lattice order x0..x7 (wave_helper.py:183-190), quirk Q3:
-      // (d,h,w) offsets 000,100,010,001,101,010,001,111 -- x5/x6 repeat x2/x3.
+      // sub-lattice order from merge_code (see wf_patch_merging_fwd)
       const int seg = k / g.a_C;
       const int c = k - seg * g.a_C;
-      const int code = (0x7 << 28) | (0x1 << 24) | (0x2 << 20) | (0x5 << 16) | (0x1 << 12) |
-                       (0x2 << 8) | (0x4 << 4) | 0x0;
-      const int o = (code >> (4 * seg)) & 0xF;  // bit2: d, bit1: h, bit0: w
+      const int o = (g.merge_code >> (4 * seg)) & 0xF;  // bit2: d, bit1: h, bit0: w
       const int64_t p = pos + (((int64_t)((o >> 2) & 1) * g.mH + ((o >> 1) & 1)) * g.mW) +
                         (o & 1);
       return p * g.a_C + c;
@@ -247,14 +244,15 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
       v.w = gelu_erf(v.w);
     } else if (g.epi == EPI_RESID) {
       const f32x4 xr = reinterpret_cast<const f32x4*>(g.r_x + m * (int64_t)N)[c4];
+      const float bs = g.r_scale ? g.r_scale[m / g.rows_per_sample] : 1.f;
       if (g.r_stats) {
         const float mean = g.r_stats[2 * m], rstd = g.r_stats[2 * m + 1];
         const f32x4 lw = reinterpret_cast<const f32x4*>(g.r_ln_w)[c4];
         const f32x4 lb = reinterpret_cast<const f32x4*>(g.r_ln_b)[c4];
         const f32x4 n2 = (xr - mean) * rstd * lw + lb;
-        v = xr + (n2 + v);  // attn_fused + (n2 + ffn(n2)), quirk Q4
+        v = xr + (n2 + v) * bs;  // attn_fused + drop_path(n2 + ffn(n2)), quirk Q4
       } else {
-        v = xr + v;         // bare CCF_FFN.forward: x + x_out (wave_helper.py:293)
+        v = xr + v * bs;         // bare CCF_FFN.forward: x + x_out (wave_helper.py:293)
       }
     }
     if (g.out_bf16) {
@@ -286,10 +284,16 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
   const size_t lds = gemm_lds_bytes(BM, g.K, g.N);
   if (lds > 160 * 1024) return fail(WF_E_SHAPE, std::string(who) + ": K/N too large for the LDS tile");
   const unsigned blocks = (unsigned)cdiv(g.M, BM);
+  auto go = [&](auto kern) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, g);
+  };
   switch (BM) {
-    case 64: hipLaunchKernelGGL(gemm_ares_kernel<64>, dim3(blocks), dim3(256), lds, s, g); break;
-    case 32: hipLaunchKernelGGL(gemm_ares_kernel<32>, dim3(blocks), dim3(256), lds, s, g); break;
-    default: hipLaunchKernelGGL(gemm_ares_kernel<16>, dim3(blocks), dim3(256), lds, s, g); break;
+    case 64: go(gemm_ares_kernel<64>); break;
+    case 32: go(gemm_ares_kernel<32>); break;
+    default: go(gemm_ares_kernel<16>); break;
   }
   return check_launch(who);
 }

@@ -19,6 +19,7 @@ struct GemmArgs {
   int a_nseg;            // K = a_nseg * a_C
   int a_map;             // RowMap
   int mB, mD, mH, mW, mws;  // geometry of the source raster for MAP_WINDOW / MAP_MERGE
+  int merge_code;        // MAP_MERGE: 8 nibbles, sub-lattice s offset (d<<2|h<<1|w) at bits 4s
   int a_ln;              // LnMode
   const float* a_stats;  // LN_GIVEN: (M, 2) {mean, rstd}
   const float* a_ln_w;
@@ -42,6 +43,8 @@ struct GemmArgs {
   const float* r_stats;  //   if non-NULL also add LN(r_x; r_stats, r_ln_w, r_ln_b)
   const float* r_ln_w;
   const float* r_ln_b;
+  const float* r_scale;  //   per-sample factor on the added branch (DropPath) or NULL
+  int64_t rows_per_sample; // M / B for r_scale
 };
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);

@@ -65,6 +65,7 @@ struct MsfuseArgs {
   int sd[4], sh[4], sw[4];
   int nsrc;
   const float* shortcut;
+  const float* branch_scale;
   float* out;
   float* stats;
   float eps;
@@ -132,6 +133,11 @@ __global__ __launch_bounds__(256) void msfuse_kernel(MsfuseArgs a) {
         const f32x4 t1 = t10 * wy0 + t11 * wy1;
         acc[j] += t0 * wz0 + t1 * wz1;
       }
+    }
+    if (a.branch_scale) {
+      const float bs = a.branch_scale[b];
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] *= bs;
     }
     const f32x4* sc = reinterpret_cast<const f32x4*>(a.shortcut + g * C);
     f32x4* dst = reinterpret_cast<f32x4*>(a.out + g * C);
@@ -225,7 +231,8 @@ extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* b
 }
 
 extern "C" int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, int nsrc,
-                             const float* shortcut, float* out, float* stats, float ln_eps,
+                             const float* shortcut, const float* branch_scale, float* out,
+                             float* stats, float ln_eps,
                              int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
                              void* stream) {
   WF_REQUIRE(nsrc >= 0 && nsrc <= 4, "at most 4 sources");
@@ -243,6 +250,7 @@ extern "C" int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, in
   }
   a.nsrc = nsrc;
   a.shortcut = shortcut;
+  a.branch_scale = branch_scale;
   a.out = out;
   a.stats = stats;
   a.eps = ln_eps;

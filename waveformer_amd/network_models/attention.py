@@ -1,0 +1,90 @@
+"""Window multi-head self-attention with a 3D relative-position bias.
+
+Mirrors network_models/attention.py (class Attention, :15-129): same constructor, parameters,
+buffers and state_dict keys.  The forward runs on the waveformer_amd HIP kernels
+(wf_window_attention_fwd): qkv GEMM -> flash-style QK^T + bias / softmax / PV core -> proj.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+def relative_position_index(ws: int) -> torch.Tensor:
+    """Pairwise index into the (2ws-1)^3-row bias table for the ws^3 tokens of a window
+    (row-major (s, h, w) token order).  Reproduces the reference's depth stride of 3*ws-1
+    (attention.py:51-52; quirk Q2) -- not the collision-free (2ws-1)^2."""
+    ar = torch.arange(ws)
+    s, h, w = torch.meshgrid(ar, ar, ar, indexing="ij")
+    pos = torch.stack([s.reshape(-1), h.reshape(-1), w.reshape(-1)], dim=-1)  # (N, 3)
+    d = pos[:, None, :] - pos[None, :, :] + (ws - 1)                           # (N, N, 3)
+    return d[..., 0] * (3 * ws - 1) + d[..., 1] * (2 * ws - 1) + d[..., 2]
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, num_heads=8, qkv_bias=False, qk_scale=None, attn_drop=0.,
+                 proj_drop=0., window_size=6, img_size=(48, 48, 48)):
+        super().__init__()
+        assert dim % num_heads == 0, f"dim {dim} should be divided by num_heads {num_heads}."
+        self.dim = dim
+        self.num_heads = num_heads
+        self.head_dim = dim // num_heads
+        self.scale = qk_scale or self.head_dim ** -0.5
+        self.window_size = window_size
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+        self.relative_position_bias_table = nn.Parameter(
+            torch.zeros((2 * window_size - 1) ** 3, num_heads))
+        self.register_buffer("relative_position_index", relative_position_index(window_size))
+        nn.init.trunc_normal_(self.relative_position_bias_table, std=.02)
+        self.softmax = nn.Softmax(dim=-1)
+        self._bias_key = None
+        self._bias = None
+
+    # ---- dense (heads, N, N) bias, rebuilt only when the table / index change
+    def dense_bias(self) -> torch.Tensor:
+        t, i = self.relative_position_bias_table, self.relative_position_index
+        key = (t.data_ptr(), t._version, i.data_ptr(), i._version, t.device)
+        if self._bias is None or self._bias_key != key:
+            self._bias = ops.rel_pos_bias(t.detach(), i)
+            self._bias_key = key
+        return self._bias
+
+    def _check_train(self):
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError(
+                "waveformer_amd: the attention backward kernels are not built yet; "
+                "run the module in eval() or under torch.no_grad()")
+        if self.training and (self.attn_drop.p > 0 or self.proj_drop.p > 0):
+            raise NotImplementedError("waveformer_amd: attention dropout > 0 is not supported")
+
+    def forward_raster(self, x_cl: torch.Tensor,
+                       ln: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None) -> torch.Tensor:
+        """Attention over the ws^3 windows of a channel-last raster (B, D, H, W, C): the
+        window_partition + forward + plain-reshape "reverse" of Block (wave_helper.py:491-499,
+        quirk Q1).  Row r of the result (as a (B*D*H*W, C) matrix) is token r % N of window
+        r // N; viewed as (B, D, H, W, C) it is exactly the reference's attn_windows."""
+        self._check_train()
+        return ops.window_attention(
+            x_cl, self.qkv.weight, self.qkv.bias, self.dense_bias(), self.proj.weight,
+            self.proj.bias, self.window_size, self.num_heads, self.scale, ln)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x: (B_, N, C) token batches, N = window_size^3 (attention.py:83-104)."""
+        B_, N, C = x.shape
+        ws = self.window_size
+        if N != ws ** 3:
+            raise ValueError(f"expected N = window_size^3 = {ws ** 3}, got {N}")
+        x = x.contiguous()
+        return self.forward_raster(x.view(B_, ws, ws, ws, C)).view(B_, N, C)
+
+    def flops(self):
+        N = self.window_size ** 3
+        return 2 * N * self.dim * 3 * self.dim + 4 * N * N * self.dim + 2 * N * self.dim * self.dim

@@ -1,0 +1,76 @@
+"""IDWT decoder block.
+
+Mirrors network_models/idwt_upsample.py (HFRefinementRes :12-50, UnetrIDWTBlock :53-166):
+same constructor and state_dict keys.  The wavelet synthesis (ptwt.waverec3, :160) and the
+concatenation with the skip (:163) run as one wf_idwt3d_haar launch that writes straight into
+the first half of the concatenated buffer; the surrounding convolutions are PyTorch/MIOpen.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Sequence, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..blocks import UnetBasicBlock, UnetResBlock, get_conv_layer
+
+
+class HFRefinementRes(nn.Module):
+    """x * sigmoid(conv1(relu(IN(dwconv3(x)))))  -- filters high-frequency coefficients."""
+
+    def __init__(self, in_channels, init_alpha=0.3, network_config=None):
+        super().__init__()
+        self.network_config = network_config or {}
+        hf_config = self.network_config.get('hf_refinement', {})
+        self.conv1 = nn.Conv3d(in_channels, in_channels, kernel_size=3, padding=1,
+                               groups=in_channels, bias=True)
+        self.norm = nn.InstanceNorm3d(in_channels, affine=True)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv3d(in_channels, in_channels, kernel_size=1, bias=True)
+        self.sigmoid = nn.Sigmoid() if hf_config.get('use_sigmoid', True) else None
+
+    def forward(self, x):
+        r = self.conv2(self.relu(self.norm(self.conv1(x))))
+        if self.sigmoid is not None:
+            r = self.sigmoid(r)
+        return x * r
+
+
+class UnetrIDWTBlock(nn.Module):
+    def __init__(self, spatial_dims: int, in_channels: int, out_channels: int, stage: int,
+                 hf_refinement: bool, wavelet: str, kernel_size: Union[Sequence[int], int],
+                 norm_name: Union[Tuple, str], res_block: bool = False,
+                 network_config: Dict[str, Any] = None) -> None:
+        super().__init__()
+        self.network_config = network_config or {}
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.wavelet = wavelet
+        self.hf_refinement = hf_refinement
+        if self.hf_refinement:
+            self.hf_ref = nn.ModuleList([
+                HFRefinementRes(in_channels // pow(2, stage), network_config=self.network_config)
+                for _ in range(stage)])
+        self.conv_lf_block = get_conv_layer(spatial_dims, in_channels, out_channels,
+                                            kernel_size=kernel_size, stride=1, conv_only=True)
+        cls = UnetResBlock if res_block else UnetBasicBlock
+        self.conv_block = cls(spatial_dims, out_channels * 2, out_channels,
+                              kernel_size=kernel_size, stride=1, norm_name=norm_name)
+
+    def forward(self, inp, skip, hf_coeffs):
+        if str(self.wavelet) not in ("db1", "haar"):
+            raise NotImplementedError(f"waveformer_amd: IDWT wavelet {self.wavelet!r} not implemented")
+        inp = self.conv_lf_block(inp)
+        if self.hf_refinement:
+            hf_coeffs = tuple({k: self.hf_ref[i](d[k]) for k in d}
+                              for i, d in enumerate(hf_coeffs))
+        B, C = inp.shape[:2]
+        L = len(hf_coeffs)
+        size = tuple(s * 2 ** L for s in inp.shape[2:])
+        if skip.shape[0] != B or tuple(skip.shape[2:]) != size:
+            raise ValueError(f"skip {tuple(skip.shape)} does not match the IDWT output {(B, C) + size}")
+        buf = torch.empty((B, C + skip.shape[1]) + size, dtype=inp.dtype, device=inp.device)
+        ops.idwt3d_haar(inp, hf_coeffs, out=buf)   # channels [0, C)
+        buf[:, C:].copy_(skip)                      # torch.cat((out, skip), 1)
+        return self.conv_block(buf)

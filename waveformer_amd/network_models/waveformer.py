@@ -1,0 +1,138 @@
+"""MultiscaleTransformer -- the 4-stage WaveFormer encoder.
+
+Mirrors network_models/waveformer.py (class MultiscaleTransformer, :36-340): same constructor,
+submodules and state_dict keys.  forward_features keeps every activation channel-last and runs
+PatchEmbed, the Blocks, PatchMerging and proj_out on the HIP kernels; the only layout change
+is proj_out's transposed write of each stage output to NCDHW (the tensors the decoder uses).
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import List, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.init as init
+
+from .. import ops
+from ..blocks import PatchEmbed as _MonaiPatchEmbed
+from .wave_helper import Block, PatchMerging
+
+
+class MultiscaleTransformer(nn.Module):
+    def __init__(self, img_size=(128, 128, 128), patch_size=2, in_chans=4, num_classes=4,
+                 embed_dims=[48, 96, 192, 384], num_heads=[3, 6, 12, 24], mlp_ratios=[4, 4, 4, 4],
+                 decom_levels=[3, 2, 1, 0], multi_scale_attention=True, qkv_bias=False,
+                 qk_scale=None, drop_rate=0., attn_drop_rate=0., drop_path_rate=0.,
+                 norm_layer=nn.LayerNorm, patch_norm=False, depths=[2, 2, 2, 2],
+                 network_config=None):
+        super().__init__()
+        self.network_config = network_config or {}
+        self.num_classes = num_classes
+        self.depths = depths
+        self.patch_norm = patch_norm
+        self.patch_size = patch_size
+        self.img_size = img_size
+        self.levels = decom_levels
+        self.multi_scale_attention = multi_scale_attention
+        self.patch_embed = _MonaiPatchEmbed(patch_size=patch_size, in_chans=in_chans,
+                                            embed_dim=embed_dims[0],
+                                            norm_layer=norm_layer if patch_norm else None,
+                                            spatial_dims=len(img_size))
+        self.pos_drop = nn.Dropout(p=drop_rate)
+        dpr = [v.item() for v in torch.linspace(0, drop_path_rate, sum(depths))]
+        cur = 0
+        for s in range(4):
+            div = 2 ** (s + 1)
+            blocks = nn.ModuleList([
+                Block(dim=embed_dims[s], num_heads=num_heads[s], mlp_ratio=mlp_ratios[s],
+                      qkv_bias=qkv_bias, qk_scale=qk_scale, drop=drop_rate,
+                      attn_drop=attn_drop_rate, drop_path=dpr[cur + i], norm_layer=norm_layer,
+                      level=self.levels[s], ms_attention=self.multi_scale_attention,
+                      img_size=tuple(d // div for d in img_size),
+                      network_config=self.network_config)
+                for i in range(depths[s])])
+            setattr(self, f"block{s + 1}", blocks)
+            cur += depths[s]
+            if s < 3:
+                setattr(self, f"downsample_{s + 1}",
+                        PatchMerging(dim=embed_dims[s], norm_layer=norm_layer,
+                                     spatial_dims=len(img_size)))
+        self.apply(self._init_weights)
+
+    def _init_weights(self, m: nn.Module):
+        cfg = self.network_config.get('initialization', {})
+        if isinstance(m, nn.Linear):
+            nn.init.trunc_normal_(m.weight, std=cfg.get('weight_std', 0.02))
+            if m.bias is not None:
+                init.constant_(m.bias, cfg.get('bias_constant', 0.0))
+        elif isinstance(m, nn.LayerNorm):
+            init.constant_(m.bias, cfg.get('layer_norm_bias', 0.0))
+            init.constant_(m.weight, cfg.get('layer_norm_weight', 1.0))
+        elif isinstance(m, (nn.Conv2d, nn.Conv3d)):
+            fan_out = math.prod(m.kernel_size) * m.out_channels // m.groups
+            m.weight.data.normal_(0, math.sqrt(2.0 / fan_out))
+            if m.bias is not None:
+                m.bias.data.zero_()
+
+    def proj_out(self, x: torch.Tensor, normalize: bool = False) -> torch.Tensor:
+        """waveformer.py:182-204 on an NCDHW tensor (API form).  forward_features calls the
+        fused channel-last -> NCDHW kernel directly."""
+        if x.dim() != 5:
+            raise NotImplementedError("waveformer_amd: 3D (5-D tensor) proj_out only")
+        return ops.proj_out(x.permute(0, 2, 3, 4, 1).contiguous(), normalize)
+
+    def init_weights(self, pretrained: str):
+        if isinstance(pretrained, str):
+            self.load_dualpath_model(self, pretrained)
+        else:
+            raise TypeError('pretrained must be a str or None')
+
+    def load_dualpath_model(self, model: nn.Module, model_file):
+        t0 = time.time()
+        if isinstance(model_file, str):
+            sd = torch.load(model_file, map_location=torch.device('cpu'), weights_only=True)
+            if 'model' in sd.keys():
+                sd = sd['model']
+        else:
+            sd = model_file
+        model.load_state_dict(sd, strict=False)
+        if hasattr(self, 'logger'):
+            self.logger.info(f"Load model, Time usage: {time.time() - t0}")
+
+    def forward_features(self, x_rgb: torch.Tensor, normalize: bool = True
+                         ) -> Tuple[List[torch.Tensor], List]:
+        """waveformer.py:260-322: PatchEmbed -> 4 stages (Blocks, PatchMerging) -> proj_out.
+        Returns (outs: 4 NCDHW tensors, outs_hf: the last block's detail dicts of stages 1-3)."""
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError(
+                "waveformer_amd: backward kernels are not built yet; use eval() / no_grad()")
+        if self.patch_norm:
+            raise NotImplementedError("waveformer_amd: patch_norm=True is not implemented")
+        if x_rgb.dtype != torch.float32:
+            raise TypeError("waveformer_amd: float32 input expected")
+        x = ops.patch_embed(x_rgb.contiguous(), self.patch_embed.proj.weight,
+                            self.patch_embed.proj.bias)
+        outs, outs_hf = [], []
+        for s in range(4):
+            if s > 0:
+                x = getattr(self, f"downsample_{s}")(x)
+            x_h = None
+            for blk in getattr(self, f"block{s + 1}"):
+                r = blk(x)
+                if isinstance(r, tuple):
+                    x, x_h = r
+                else:
+                    x = r
+            B, D, H, W, C = x.shape
+            outs.append(ops.proj_out(x, normalize))
+            if s < 3:
+                outs_hf.append(x_h if x_h is not None else ())
+        return outs, outs_hf
+
+    def forward(self, x_rgb: torch.Tensor):
+        return self.forward_features(x_rgb)
+
+    def flops(self) -> int:
+        return 0

@@ -10,7 +10,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -44,15 +43,11 @@ def _check(t: torch.Tensor, name: str, dtype=torch.float32, contiguous=True) -> 
         raise ValueError(f"{name}: expected a contiguous tensor")
 
 
-_bf16_cache: "weakref.WeakKeyDictionary[torch.Tensor, Tuple[int, int, torch.Tensor]]" = \
-    weakref.WeakKeyDictionary()
-
-
 def bf16_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None) -> torch.Tensor:
-    """bf16 copy of an fp32 weight (made by the wf_cast kernel), cached until p changes."""
-    key = p
-    ent = _bf16_cache.get(key)
+    """bf16 copy of an fp32 weight (made by the wf_cast kernel), cached on the parameter
+    until it changes (in-place optimizer steps / load_state_dict bump its _version)."""
     ver = p._version
+    ent = getattr(p, "_wf_bf16", None)
     if ent is not None and ent[0] == ver and ent[1] == p.data_ptr():
         return ent[2]
     src = p.detach()
@@ -60,7 +55,7 @@ def bf16_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None) -> tor
     out = torch.empty(src.shape if shape is None else shape, dtype=torch.bfloat16,
                       device=src.device)
     _lib.call("wf_cast_f32_to_bf16", src.data_ptr(), out.data_ptr(), src.numel(), _stream())
-    _bf16_cache[key] = (ver, p.data_ptr(), out)
+    p._wf_bf16 = (ver, p.data_ptr(), out)
     return out
 
 
@@ -226,7 +221,8 @@ def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torc
 # ------------------------------------------------------------------------------------------
 # a6: multi-scale fuse
 # ------------------------------------------------------------------------------------------
-def msfuse(srcs: Sequence[torch.Tensor], shortcut: torch.Tensor, ln_eps: Optional[float]
+def msfuse(srcs: Sequence[torch.Tensor], shortcut: torch.Tensor, ln_eps: Optional[float],
+           branch_scale: Optional[torch.Tensor] = None
            ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """shortcut + sum_s trilinear(src_s) (align_corners=False), channel-last; optional stats."""
     _check(shortcut, "shortcut")
@@ -245,7 +241,10 @@ def msfuse(srcs: Sequence[torch.Tensor], shortcut: torch.Tensor, ln_eps: Optiona
         stats = torch.empty((B * D * H * W, 2), dtype=torch.float32, device=shortcut.device)
     arr = (ctypes.c_void_p * max(1, len(srcs)))(*[s.data_ptr() for s in srcs])
     darr = (ctypes.c_int64 * max(1, len(dhw)))(*dhw)
-    _lib.call("wf_msfuse_fwd", arr, darr, len(srcs), shortcut.data_ptr(), out.data_ptr(),
+    if branch_scale is not None:
+        _check(branch_scale, "branch_scale")
+    _lib.call("wf_msfuse_fwd", arr, darr, len(srcs), shortcut.data_ptr(), _ptr(branch_scale),
+              out.data_ptr(),
               _ptr(stats), float(ln_eps or 0.0), B, C, D, H, W, _stream())
     return out, stats
 
@@ -254,7 +253,7 @@ def msfuse(srcs: Sequence[torch.Tensor], shortcut: torch.Tensor, ln_eps: Optiona
 # a7/a8: CCF_FFN (+ norm2 / double residual)
 # ------------------------------------------------------------------------------------------
 def ccf_ffn(xh: torch.Tensor, stats: Optional[torch.Tensor], norm2: Optional[torch.nn.Module],
-            mlp: torch.nn.Module) -> torch.Tensor:
+            mlp: torch.nn.Module, branch_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Block path (stats given): xh + n2 + ffn(n2), n2 = norm2(xh).  Bare (stats None): xh + ffn(xh)."""
     _check(xh, "x")
     B, D, H, W, C = xh.shape
@@ -271,7 +270,8 @@ def ccf_ffn(xh: torch.Tensor, stats: Optional[torch.Tensor], norm2: Optional[tor
               pw.data_ptr(), _ptr(mlp.pwconv.bias), mlp.norm1.weight.data_ptr(),
               mlp.norm1.bias.data_ptr(), float(mlp.norm1.eps), mlp.dwconv.weight.data_ptr(),
               mlp.dwconv.bias.data_ptr(), mlp.norm2.weight.data_ptr(), mlp.norm2.bias.data_ptr(),
-              float(mlp.norm2.eps), fc.data_ptr(), _ptr(mlp.fc.bias), out.data_ptr(),
+              float(mlp.norm2.eps), fc.data_ptr(), _ptr(mlp.fc.bias), _ptr(branch_scale),
+              out.data_ptr(),
               work.data_ptr(), B, C, hid, D, H, W, _stream())
     return out
 
@@ -279,15 +279,15 @@ def ccf_ffn(xh: torch.Tensor, stats: Optional[torch.Tensor], norm2: Optional[tor
 # ------------------------------------------------------------------------------------------
 # a9: PatchMerging
 # ------------------------------------------------------------------------------------------
-def patch_merging(x_cl: torch.Tensor, norm: torch.nn.LayerNorm, reduction: torch.nn.Linear
-                  ) -> torch.Tensor:
+def patch_merging(x_cl: torch.Tensor, norm: torch.nn.LayerNorm, reduction: torch.nn.Linear,
+                  v2: bool = False) -> torch.Tensor:
     _check(x_cl, "x")
     B, D, H, W, C = x_cl.shape
     red = bf16_weight(reduction.weight)
     out = torch.empty((B, D // 2, H // 2, W // 2, 2 * C), dtype=torch.float32, device=x_cl.device)
     _lib.call("wf_patch_merging_fwd", x_cl.data_ptr(), norm.weight.data_ptr(),
-              norm.bias.data_ptr(), float(norm.eps), red.data_ptr(), out.data_ptr(), B, C, D, H,
-              W, _stream())
+              norm.bias.data_ptr(), float(norm.eps), red.data_ptr(), int(bool(v2)), out.data_ptr(),
+              B, C, D, H, W, _stream())
     return out
 
 
