@@ -1,0 +1,289 @@
+#!/usr/bin/env python3
+"""bench.py -- WaveFormer encoder forward on MI355X (BASELINE.json configs[1]).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --precision bf16x3|bf16]
+
+One step = one MultiscaleTransformer forward (PatchEmbed -> 4 stages of DWT / window
+attention / multi-scale fuse / CCF_FFN / PatchMerging -> proj_out; network_models/waveformer.py
+:260-322) over a batch of B synthetic 128^3 x 4 crops already resident in HBM, on the
+waveformer_amd HIP kernels.  N > 1 (launched by torch.distributed.run, one process per GPU)
+runs N independent replicas -- 128^3 crops do not shard -- and reports the
+whole-job rate: B * K * N volumes / the slowest rank's wall time.
+
+Rank 0 prints ONE JSON line.  Besides the driver contract it carries:
+  roofline     : the dominant HBM-bound kernel's algorithmic bytes per launch / its average
+                 launch duration, timed with HIP events on the launch stream inside the timed
+                 region, against the 8 TB/s HBM3E peak (traffic: PMC bytes from
+                 profiles/*pmc*.json when present, else null)
+  cpu_baseline : the oracle (CPU restatement of the reference, fp32 PyTorch) timed on this
+                 host on one volume (rank 0, N = 1 only)
+  parity       : Dice (TC/WT/ET) of the full Waveformer's labels at 128^3 x 4 against the
+                 reference's own labels (tests/golden), run outside the timed region
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "128³×4 volumes/sec fwd (1/2/4/8 MI355X) + Dice Δ vs reference"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4, help="volumes per GPU per step")
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"])
+    ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
+    ap.add_argument("--roofline-op", default="auto")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--parity", type=int, default=1)
+    ap.add_argument("--img", type=int, default=128)
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------------------------------
+# per-launch timing of one op with HIP events on its stream
+# ------------------------------------------------------------------------------------------
+class OpTimer:
+    """Wraps waveformer_amd.ops.<name>; records (algorithmic bytes, start, end) per launch."""
+
+    BYTES = {
+        # 1-level Haar: read the (B,D,H,W,C) input once, write 8 bands of 1/8 size
+        "dwt3d_haar": lambda a, kw, out: 2 * a[0].numel() * 4,
+        # out = shortcut + sum trilinear(src): read shortcut + sources, write out + 8 B stats/row
+        "msfuse": lambda a, kw, out: (2 * a[1].numel() + sum(s.numel() for s in a[0])) * 4
+        + (0 if out[1] is None else out[1].numel() * 4),
+        # LN + transpose: read + write
+        "proj_out": lambda a, kw, out: 2 * a[0].numel() * 4,
+    }
+
+    def __init__(self, name):
+        from waveformer_amd import ops
+        self.ops, self.name = ops, name
+        self.orig = getattr(ops, name)
+        self.rec = []
+        self.active = False
+
+        def wrapped(*a, **kw):
+            if not self.active:
+                return self.orig(*a, **kw)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = self.orig(*a, **kw)
+            e.record()
+            self.rec.append((self.BYTES[name](a, kw, out), s, e))
+            return out
+
+        setattr(ops, name, wrapped)
+        # the network_models modules import `ops` as a module, so the patch is visible to them
+
+    def summary(self):
+        torch.cuda.synchronize()
+        if not self.rec:
+            return None
+        big = max(b for b, _, _ in self.rec)
+        sel = [(b, s.elapsed_time(e)) for b, s, e in self.rec if b == big]
+        avg_ms = sum(t for _, t in sel) / len(sel)
+        return {"bytes_per_launch": big, "avg_ms": avg_ms, "launches": len(sel),
+                "achieved_gbs": big / (avg_ms * 1e-3) / 1e9}
+
+
+def pmc_traffic(kernel_substr):
+    """HBM bytes per launch from the newest profiles/*pmc*.json written by tools/pmc_traffic.py."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        for k, v in d.get("kernels", {}).items():
+            if kernel_substr in k:
+                return v.get("hbm_bytes_per_launch_largest")
+    except Exception:
+        return None
+    return None
+
+
+def build_encoder(img, device):
+    from functools import partial
+    import torch.nn as nn
+    import waveformer_amd.network_models as NM
+    torch.manual_seed(0)  # the reference's own init (trunc_normal / fan-out normal), seeded
+    m = NM.MultiscaleTransformer(img_size=(img,) * 3, in_chans=4, embed_dims=[48, 96, 192, 384],
+                                 num_heads=[3, 6, 12, 24], depths=[2, 2, 2, 2], qkv_bias=True,
+                                 norm_layer=partial(nn.LayerNorm, eps=1e-6))
+    return m.eval().to(device)
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """The oracle encoder (fp32 PyTorch on the host CPU) on one 128^3 x 4 volume."""
+    from oracle import ref_waveformer as R
+    m = build_encoder(128, "cpu")
+    sd = m.state_dict()
+    x = torch.randn(1, 4, 128, 128, 128, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        R.encoder(sd, x, heads=[3, 6, 12, 24], depths=[2] * 4)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            R.encoder(sd, x, heads=[3, 6, 12, 24], depths=[2] * 4)
+            n += 1
+            if time.perf_counter() - t0 > seconds_budget / 2 or n >= 5:
+                break
+        dt = (time.perf_counter() - t0) / n
+    return {"value": 1.0 / dt, "unit": "volumes/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{n} timed encoder forwards (+1 warm-up) of one 128^3x4 volume, B=1, fp32, "
+                      f"oracle/ref_waveformer.py (CPU restatement of the reference), "
+                      f"{dt:.2f} s/volume"}
+
+
+def parity_dice(device):
+    """Full Waveformer at 128^3 x 4 with the golden rule weights vs the reference's labels."""
+    from tests import cases as C
+    case = C.cases()["full128"]
+    m, _ = C.build(case, device)
+    with torch.no_grad():
+        lab = m(C.case_input(case).to(device)).argmax(1).cpu()
+    ref = C.g("full128_labels").long()
+    d = [C.dice(a, b) for a, b in zip(C.brats_regions(lab), C.brats_regions(ref))]
+    del m
+    torch.cuda.empty_cache()
+    return {"dice_tc_wt_et": [round(v, 6) for v in d], "dice_delta_max": round(1 - min(d), 6),
+            "vs": "reference Waveformer labels at 128^3x4 (tests/golden/ref_fixtures.npz)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from waveformer_amd import _lib, ops
+    _lib.load()  # fail loudly without the HIP library
+    ops.set_precision(args.precision)
+
+    model = build_encoder(args.img, dev)
+    x = torch.randn(args.batch, 4, args.img, args.img, args.img, device=dev,
+                    generator=torch.Generator(device=dev).manual_seed(1234 + rank))
+
+    roof_op = args.roofline_op if args.roofline_op != "auto" else "dwt3d_haar"
+    timer = OpTimer(roof_op)
+
+    def step():
+        with torch.no_grad():
+            return model(x)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+
+    graph = None
+    if args.graph:
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            graph.replay()
+            torch.cuda.synchronize()
+        except Exception as e:  # capture unsupported -> eager, said in the output
+            graph = None
+            print(f"[bench] graph capture failed ({e}); timing eager launches", file=sys.stderr)
+
+    def run_steps(k):
+        for _ in range(k):
+            if graph is not None:
+                graph.replay()
+            else:
+                step()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_steps(args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+
+    # per-launch roofline timing of the dominant streaming kernel (eager launches, so the HIP
+    # events sit on the launch stream around each launch)
+    timer.active = True
+    with torch.no_grad():
+        for _ in range(max(2, min(args.steps, 10))):
+            model(x)
+    timer.active = False
+    roof = timer.summary()
+
+    if rank == 0:
+        vols = args.batch * args.steps * world
+        out = {
+            "metric": METRIC,
+            "value": vols / dt,
+            "unit": "volumes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * dt / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic: randn 128^3x4 crops resident in HBM, reference-init random weights",
+            "config": {"workload": f"MultiscaleTransformer (WaveFormer encoder) forward, "
+                                   f"{args.img}^3x4 crops",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "precision": args.precision,
+                       "parallelism": f"replicas x{world} (no data-path collective)",
+                       "hip_graph": graph is not None},
+        }
+        if roof:
+            traffic = pmc_traffic("dwt3d_haar_fwd") if roof_op == "dwt3d_haar" else None
+            out["roofline"] = {"bound": "hbm", "kernel": roof_op,
+                               "achieved": round(roof["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s",
+                               "frac": round(roof["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                               "traffic": traffic,
+                               "algorithmic_bytes_per_launch": roof["bytes_per_launch"],
+                               "avg_launch_us": round(roof["avg_ms"] * 1e3, 2),
+                               "launches_timed": roof["launches"]}
+        if args.parity:
+            try:
+                out["parity"] = parity_dice(dev)
+            except Exception as e:
+                out["parity"] = {"error": str(e)[:200]}
+        if args.cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

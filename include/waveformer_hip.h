@@ -18,10 +18,16 @@
  *                                         keys 'aad','ada','add','daa','dad','dda','ddd'
  *                                         (key char i <-> axis (D,H,W)[i]; 'a' low, 'd' high)
  *   "NCDHW"         (B, C, D, H, W)    -- PyTorch / MONAI convolution layout
- * Activations are fp32 except the GEMM operands, which the kernels round to bf16
- * (fp32 accumulation; LayerNorm, softmax and residual adds stay fp32).
- * Weights passed as `*_bf16` are nn.Linear / 1x1x1-Conv3d weights [N][K] rounded to bf16
- * (wf_cast_f32_to_bf16); every other parameter is the fp32 module tensor as-is.
+ * Activations are fp32.  MFMA operands follow `precision`:
+ *   WF_PREC_BF16  (0): operands rounded to bf16, fp32 accumulation, GEMM-to-GEMM intermediates
+ *                      (qkv, attention output, FFN hidden) stored as bf16;
+ *   WF_PREC_BF16X3 (1): fp32-faithful -- every operand x is split into hi = bf16(x) and
+ *                      lo = bf16(x - hi) and products take hi*hi + lo*hi + hi*lo on the bf16
+ *                      MFMA pipes (relative error ~2^-17); intermediates stored fp32.
+ * LayerNorm, softmax, GELU, wavelets, interpolation and residual adds are fp32 in both.
+ * Weights passed as `*_bf16x2` are nn.Linear / 1x1x1-Conv3d weights [N][K] as two bf16 planes
+ * [2][N][K] = {hi, lo} (wf_split_f32_to_bf16x2); WF_PREC_BF16 reads the hi plane only.  Every
+ * other parameter is the fp32 module tensor as-is.
  */
 #ifndef WAVEFORMER_HIP_H
 #define WAVEFORMER_HIP_H
@@ -32,7 +38,9 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 1
+#define WF_ABI_VERSION 2
+
+enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1 };
 
 enum {
   WF_OK = 0,
@@ -48,6 +56,9 @@ const char* wf_last_error(void);
 
 /* out[i] = bf16(in[i]) (round-to-nearest-even). Weight preparation; no reference analogue. */
 int wf_cast_f32_to_bf16(const float* in, uint16_t* out, int64_t n, void* stream);
+
+/* out[i] = hi = bf16(in[i]), out[n + i] = bf16(in[i] - hi): the [2][...] weight planes. */
+int wf_split_f32_to_bf16x2(const float* in, uint16_t* out, int64_t n, void* stream);
 
 /* ---- a10: PatchEmbed -------------------------------------------------------------- */
 /* Replaces monai PatchEmbed.proj = Conv3d(Cin, Cout, k=2, s=2) as called at
@@ -97,17 +108,18 @@ int wf_rel_pos_bias(const float* table, const int64_t* index, float* bias, int64
  * out: (B*nW*N, C) fp32 in window-major order, which IS the (B, D1, H1, W1, C) raster that
  * the reference's reshape produces (Q1).  raster_rows: x is (B*D1*H1*W1, C); when
  * D1=H1=W1=ws=N^(1/3) and x is a plain (B_, N, C) token batch this is Attention.forward.
- * wqkv_bf16 (3C, C), bqkv (3C) or NULL, bias (heads, N, N) from wf_rel_pos_bias,
- * wproj_bf16 (C, C), bproj (C).  scale = qk_scale or head_dim^-0.5.
+ * wqkv_bf16x2 [2](3C, C), bqkv (3C) or NULL, bias (heads, N, N) from wf_rel_pos_bias,
+ * wproj_bf16x2 [2](C, C), bproj (C).  scale = qk_scale or head_dim^-0.5.
+ * head_dim in {16, 32, 48, 64, 96, 128, 192, 384}.
  * workspace: wf_window_attention_workspace_bytes(...) bytes, 256-B aligned.               */
 int64_t wf_window_attention_workspace_bytes(int64_t B, int64_t C, int64_t D1, int64_t H1,
-                                            int64_t W1);
+                                            int64_t W1, int precision);
 int wf_window_attention_fwd(const float* x, const float* ln_w, const float* ln_b, float ln_eps,
-                            const uint16_t* wqkv_bf16, const float* bqkv,
-                            const float* bias, const uint16_t* wproj_bf16, const float* bproj,
+                            const uint16_t* wqkv_bf16x2, const float* bqkv,
+                            const float* bias, const uint16_t* wproj_bf16x2, const float* bproj,
                             float* out, void* workspace, int64_t B, int64_t C, int64_t D1,
                             int64_t H1, int64_t W1, int64_t ws, int64_t heads, float scale,
-                            void* stream);
+                            int precision, void* stream);
 
 /* ---- a6: multi-scale fuse ------------------------------------------------------------- */
 /* Replaces the F.interpolate(trilinear, align_corners=False) + sum + shortcut of
@@ -130,28 +142,30 @@ int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, int nsrc,
  * xh: channel-last (B, D, H, W, C).  If stats != NULL the FFN input is
  * n2 = LN(xh; stats, n2_w, n2_b) and out = xh + n2 + ffn(n2) (Block, Q4);
  * if stats == NULL the input is xh itself and out = xh + ffn(xh) (bare CCF_FFN.forward).
- * pw_bf16 (4C, C), pw_b (4C), ln1_w/b (4C), dw_w (4C, 27) fp32, dw_b (4C), ln2_w/b (4C),
- * fc_bf16 (C, 4C), fc_b (C).  branch_scale: NULL or (B) per-sample DropPath factors on the
- * FFN branch (wave_helper.py:509).  workspace: wf_ccf_ffn_workspace_bytes(...) bytes.       */
+ * pw_bf16x2 [2](4C, C), pw_b (4C), ln1_w/b (4C), dw_w (4C, 27) fp32, dw_b (4C),
+ * ln2_w/b (4C), fc_bf16x2 [2](C, 4C), fc_b (C).  branch_scale: NULL or (B) per-sample
+ * DropPath factors on the FFN branch (wave_helper.py:509).
+ * workspace: wf_ccf_ffn_workspace_bytes(...) bytes.                                        */
 int64_t wf_ccf_ffn_workspace_bytes(int64_t B, int64_t C, int64_t hidden, int64_t D, int64_t H,
-                                   int64_t W);
+                                   int64_t W, int precision);
 int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* n2_w, const float* n2_b,
-                   const uint16_t* pw_bf16, const float* pw_b, const float* ln1_w,
+                   const uint16_t* pw_bf16x2, const float* pw_b, const float* ln1_w,
                    const float* ln1_b, float eps1, const float* dw_w, const float* dw_b,
                    const float* ln2_w, const float* ln2_b, float eps2,
-                   const uint16_t* fc_bf16, const float* fc_b, const float* branch_scale,
+                   const uint16_t* fc_bf16x2, const float* fc_b, const float* branch_scale,
                    float* out, void* workspace,
                    int64_t B, int64_t C, int64_t hidden, int64_t D, int64_t H, int64_t W,
-                   void* stream);
+                   int precision, void* stream);
 
 /* ---- a9: PatchMerging (quirk Q3) ------------------------------------------------------ */
 /* Replaces PatchMerging.forward (wave_helper.py:173-194): the 8-way strided gather with its
  * duplicated sub-lattices, LN(8C, eps) and Linear(8C -> 2C, no bias).  v2 != 0 selects
  * PatchMergingV2.forward's itertools.product order instead (wave_helper.py:147-167).
- * x: channel-last (B, D, H, W, C) (D, H, W even); out: channel-last (B, D/2, H/2, W/2, 2C). */
+ * x: channel-last (B, D, H, W, C) (D, H, W even); out: channel-last (B, D/2, H/2, W/2, 2C).
+ * red_bf16x2: [2](2C, 8C).                                                                 */
 int wf_patch_merging_fwd(const float* x, const float* ln_w, const float* ln_b, float eps,
-                         const uint16_t* red_bf16, int v2, float* out, int64_t B, int64_t C,
-                         int64_t D, int64_t H, int64_t W, void* stream);
+                         const uint16_t* red_bf16x2, int v2, float* out, int64_t B, int64_t C,
+                         int64_t D, int64_t H, int64_t W, int precision, void* stream);
 
 /* ---- a10: stage output projection (quirk Q5) ----------------------------------------- */
 /* Replaces MultiscaleTransformer.proj_out (waveformer.py:182-204) together with the

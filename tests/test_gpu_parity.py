@@ -4,10 +4,12 @@ and against the reference's own outputs (tests/golden/ref_fixtures.npz).
 Tolerances (stated per check):
   * fp32-only kernels (DWT, IDWT, multi-scale fuse, proj_out LayerNorm, PatchEmbed):
     rel-L2 <= 1e-5 against the oracle in fp32 -- they do the reference's arithmetic in fp32.
-  * kernels with bf16 GEMM operands (qkv / proj / QK^T / PV / pwconv / fc / PatchMerging
-    reduction; fp32 accumulation, fp32 LayerNorm / softmax / residual): rel-L2 <= 1e-2 for a
-    single op, <= 2e-2 through a Block, <= 3e-2 through the encoder (bf16 has an 8-bit
-    mantissa: 2^-9 = 2e-3 relative rounding per operand).
+  * kernels with MFMA operands (qkv / proj / QK^T / PV / pwconv / fc / PatchMerging
+    reduction; fp32 accumulation, fp32 LayerNorm / softmax / residual):
+      - default precision "bf16x3" (split hi/lo bf16 operands, fp32-faithful): rel-L2 <= 5e-5
+        per op and per Block, <= 1e-4 through the encoder and the full model;
+      - fast precision "bf16": rel-L2 <= 1e-2 for a single op, <= 2e-2 through a Block,
+        <= 3e-2 through the encoder (bf16 rounds to 2^-9 = 2e-3 relative per operand).
   * end-to-end metric (BASELINE.json north_star): Dice of TC / WT / ET of the full model's
     argmax labels at 128^3 x 4 >= 1 - 1e-3 against the reference's labels.
 """
@@ -147,11 +149,13 @@ def test_attention_vs_oracle(ws, heads, dim, B_):
     sd = rule_state_dict(m.state_dict())
     m.load_state_dict(sd)
     m = m.eval().to(DEV)
+    from waveformer_amd import ops
     x = seeded_randn((B_, ws ** 3, dim), 12)
-    with torch.no_grad():
-        out = m(cuda(x))
     ref = R.attention(sd, "", x, heads, ws)
-    assert C.rel_l2(out, ref) <= 1e-2
+    for prec, tol in (("bf16x3", 5e-5), ("bf16", 1e-2)):
+        with torch.no_grad(), ops.precision(prec):
+            out = m(cuda(x))
+        assert C.rel_l2(out, ref) <= tol, prec
 
 
 def test_window_attention_q1_layout_on_raster():
@@ -167,36 +171,41 @@ def test_window_attention_q1_layout_on_raster():
         out = m.forward_raster(cuda(x))
     win = R.window_partition(x, 4).view(-1, 64, 48)
     ref = R.attention(sd, "", win, 3, 4).reshape(2, 8, 12, 16, 48)
-    assert C.rel_l2(out, ref) <= 1e-2
+    assert C.rel_l2(out, ref) <= 5e-5
 
 
 # ------------------------------------------------------------------------------ module level
-TOL = {"tensor": 1e-2, "block": 2e-2, "encoder": 3e-2, "full": 3e-2}
+# rel-L2 bounds per precision (measured: bf16x3 2.5e-6..2.6e-5, bf16 1.5e-3..1e-2)
+TOL = {"bf16x3": {"tensor": 5e-5, "block": 5e-5, "encoder": 1e-4, "full": 1e-4},
+       "bf16": {"tensor": 1e-2, "block": 2e-2, "encoder": 3e-2, "full": 3e-2}}
 
 
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
 @pytest.mark.parametrize("name", ["attn_ws8", "attn_ws2_h1", "attn_ws4_h2", "merge", "ccf_ffn",
                                   "block_l3", "block_l1", "block_l0", "block_ss_l2", "enc32",
                                   "full32"])
-def test_module_vs_reference_golden_and_oracle(name):
+def test_module_vs_reference_golden_and_oracle(name, prec):
+    from waveformer_amd import ops
     case = C.cases()[name]
     m, sd = C.build(case, DEV)
     x = C.case_input(case)
-    with torch.no_grad():
+    with torch.no_grad(), ops.precision(prec):
         out = m(cuda(x))
+    with torch.no_grad():
         ora = case.oracle(sd, x)
     got = C.flatten_output(case, out)
     want_oracle = C.flatten_output(case, ora)
     keys = [k for k in C.golden().files if (k == name or k.startswith(name + "_")) and "__" not in k]
     assert set(got) == set(keys)
-    tol = TOL[case.kind]
+    tol = TOL[prec][case.kind]
     for k in keys:
         ref = C.g(k)
         assert tuple(got[k].shape) == tuple(ref.shape), k
         e_ref = C.rel_l2(got[k], ref)
         e_ora = C.rel_l2(got[k], want_oracle[k])
-        # detail bands of deep encoder stages are cancellation-prone: compare them at the
-        # scale of the band they are computed from
-        t = tol * (3 if "_hf" in k and case.kind == "encoder" else 1)
+        # high-pass bands of deep encoder stages are differences of neighbouring voxels
+        # (cancellation): the same absolute error is ~10x larger relative to them
+        t = tol * (10 if "_hf" in k and case.kind == "encoder" else 1)
         assert e_ref <= t, (k, e_ref)
         assert e_ora <= t, (k, e_ora)
 
@@ -211,18 +220,25 @@ def test_encoder128_vs_reference_summaries():
         assert tuple(t.shape) == tuple(C.golden()[k + "__shape"]), k
         sums, sample = C.summary(t)
         ref = C.golden()[k + "__sum"]
-        assert abs(math.sqrt(sums[1]) / math.sqrt(ref[1]) - 1) <= 2e-2, k
-        tol = 1e-1 if "_hf" in k else 3e-2
+        tol = 2e-3 if "_hf" in k else 2e-4  # bf16x3 (default precision)
+        assert abs(math.sqrt(sums[1]) / math.sqrt(ref[1]) - 1) <= tol, k
+        assert abs(sums[2] - ref[2]) <= 10 * tol * math.sqrt(ref[1]), k
         assert C.rel_l2(sample, C.g(k + "__sample")) <= tol, (k, C.rel_l2(sample, C.g(k + "__sample")))
 
 
-def test_full_model_128_dice_vs_reference():
-    """BASELINE north_star: Dice within 1e-3 of the reference (TC / WT / ET of argmax labels)."""
+@pytest.mark.parametrize("prec,bound", [("bf16x3", 1e-3), ("bf16", 5e-2)])
+def test_full_model_128_dice_vs_reference(prec, bound):
+    """BASELINE north_star: Dice within 1e-3 of the reference (TC / WT / ET of the argmax
+    labels of the full model at 128^3 x 4).  The fp32-faithful default (bf16x3) meets it;
+    plain bf16 operands cannot with these weights (every logit margin is uniformly spread near
+    zero, so a 1e-2 logit error flips ~1% of voxels -- measured Dice ~0.98; CPU bf16 autocast of
+    the reference encoder gives 0.97), hence its looser bound."""
+    from waveformer_amd import ops
     case = C.cases()["full128"]
     m, _ = C.build(case, DEV)
-    with torch.no_grad():
+    with torch.no_grad(), ops.precision(prec):
         logits = m(cuda(C.case_input(case)))
     lab = logits.argmax(1).cpu()
     ref = C.g("full128_labels").long()
     d = [C.dice(a, b) for a, b in zip(C.brats_regions(lab), C.brats_regions(ref))]
-    assert min(d) >= 1 - 1e-3, d
+    assert min(d) >= 1 - bound, d

@@ -30,7 +30,7 @@ def test_library_exports_every_symbol():
     for s in declared_symbols():
         assert hasattr(lib, s), s
     lib = _lib.load()
-    assert lib.wf_abi_version() == 1
+    assert lib.wf_abi_version() == _lib.ABI_VERSION
 
 
 def test_shape_errors_are_reported_without_a_gpu():
@@ -41,4 +41,4 @@ def test_shape_errors_are_reported_without_a_gpu():
     assert b"even" in lib.wf_last_error() or b"multiple of 4" in lib.wf_last_error()
     with pytest.raises(RuntimeError, match="wf_proj_out_fwd"):
         _lib.call("wf_proj_out_fwd", None, None, 1, 1e-5, 1, 6, 8, None)
-    assert _lib.query("wf_window_attention_workspace_bytes", 1, 48, 32, 32, 32) >= 32768 * 48 * 8
+    assert _lib.query("wf_window_attention_workspace_bytes", 1, 48, 32, 32, 32, 0) >= 32768 * 48 * 8

@@ -26,21 +26,24 @@ SIGNATURES = {
     "wf_abi_version": (_I, []),
     "wf_last_error": (ctypes.c_char_p, []),
     "wf_cast_f32_to_bf16": (_I, [_P, _P, _I64, _P]),
+    "wf_split_f32_to_bf16x2": (_I, [_P, _P, _I64, _P]),
     "wf_patch_embed_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwt3d_haar_fwd": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_rel_pos_bias": (_I, [_P, _P, _P, _I64, _I64, _I64, _P]),
-    "wf_window_attention_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64]),
+    "wf_window_attention_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I]),
     "wf_window_attention_fwd": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P,
-                                     _I64, _I64, _I64, _I64, _I64, _I64, _I64, _F, _P]),
+                                     _I64, _I64, _I64, _I64, _I64, _I64, _I64, _F, _I, _P]),
     "wf_msfuse_fwd": (_I, [_P, _P, _I, _P, _P, _P, _P, _F, _I64, _I64, _I64, _I64, _I64, _P]),
-    "wf_ccf_ffn_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I64]),
+    "wf_ccf_ffn_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I64, _I]),
     "wf_ccf_ffn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _F, _P, _P,
-                            _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
-    "wf_patch_merging_fwd": (_I, [_P, _P, _P, _F, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+                            _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
+    "wf_patch_merging_fwd": (_I, [_P, _P, _P, _F, _P, _I, _P, _I64, _I64, _I64, _I64, _I64,
+                                  _I, _P]),
     "wf_proj_out_fwd": (_I, [_P, _P, _I, _F, _I64, _I64, _I64, _P]),
 }
 
+ABI_VERSION = 2
 _lock = threading.Lock()
 _lib = None
 _err = None
@@ -66,8 +69,8 @@ def load(path: str | None = None):
             fn.restype = res
             fn.argtypes = args
         ver = lib.wf_abi_version()
-        if ver != 1:
-            raise LibraryMissing(f"{p}: ABI version {ver}, expected 1")
+        if ver != ABI_VERSION:
+            raise LibraryMissing(f"{p}: ABI version {ver}, expected {ABI_VERSION} (rebuild)")
         _lib = lib
         return _lib
 

@@ -5,12 +5,13 @@
 // q@k^T + relative_position_bias -> softmax -> @v -> proj, then the window "reverse" that is
 // a plain reshape (quirk Q1).  Here:
 //   qkv  : gemm_ares with the window gather (and norm1 for level-0 blocks) in its loader
-//   core : one workgroup = (window b_, head h, 64 queries); flash-style loop over 64-key
-//          tiles staged in LDS.  S^T = K.Q^T is computed "swapped" (keys on the MFMA rows,
-//          queries on the lanes) so the fp32 accumulator of S^T is, register for register,
-//          the B operand of O^T = V^T.P^T after bf16 rounding -- P never leaves registers and
-//          the softmax column reductions are 2 lane shuffles.  v_mfma_f32_16x16x16_bf16
-//          covers head_dim in 16-wide steps (head_dim is 16 at the default widths).
+//   core : one workgroup = (window b_, head h, 64 queries); flash-style loop over key tiles
+//          staged in LDS.  S^T = K.Q^T is computed "swapped" (keys on the MFMA rows, queries
+//          on the lanes) so the fp32 accumulator of S^T is, register for register, the B
+//          operand of O^T = V^T.P^T after bf16 rounding -- P never leaves registers and the
+//          softmax column reductions are 2 lane shuffles.  v_mfma_f32_16x16x16_bf16 covers
+//          head_dim in 16-wide steps (head_dim is 16 at the default widths).  PREC_SPLIT
+//          carries Q, K, V and P as bf16 hi + lo pairs (3 MFMAs per product).
 //   proj : gemm_ares; rows stay in window-major order, which is exactly the reference's
 //          reshaped raster (Q1).
 #include "kernels.hpp"
@@ -18,17 +19,36 @@
 namespace wf {
 
 constexpr int kQB = 64;  // queries per workgroup (16 per wave)
-constexpr int kKT = 64;  // keys per LDS tile
 
-template <int HD>
-__global__ __launch_bounds__(256) void attn_core_kernel(const uint16_t* __restrict__ qkv,
+template <bool SPLIT>
+__device__ __forceinline__ void load8_split(const void* base, int64_t off, bf16x8& hi,
+                                            bf16x8& lo) {
+  if (SPLIT) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(base) + off);
+    const f32x4 a = p[0], b = p[1];
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint16_t h = f2bf(v[j]);
+      hi[j] = (short)h;
+      lo[j] = (short)f2bf(v[j] - bf2f(h));
+    }
+  } else {
+    hi = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(base) + off);
+  }
+}
+
+template <int HD, int KT, bool SPLIT>
+__global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__ qkv,
                                                         const float* __restrict__ bias,
-                                                        uint16_t* __restrict__ out, int N,
+                                                        void* __restrict__ out, int N,
                                                         int heads, float scale_log2) {
   constexpr int NC = HD / 16;  // 16-wide head_dim chunks
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[kKT * (HD + 4)];  // [key][hd]
-  __shared__ __attribute__((aligned(16))) uint16_t Vt[HD * (kKT + 4)];  // [hd][key]
-  constexpr int KS = HD + 4, VS = kKT + 4;
+  constexpr int NKT = KT / 16; // 16-key sub-tiles per tile
+  constexpr int KS = HD + 4, VS = KT + 4;
+  constexpr int NB = SPLIT ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[NB][KT * KS];  // [key][hd]
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[NB][HD * VS];  // [hd][key]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int qb = blockIdx.x, h = blockIdx.y;
@@ -41,13 +61,24 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const uint16_t* __restri
   const int g4 = 4 * (lane >> 4);
 
   // Q^T fragments (B operand): lane holds Q[q][c*16 + g4 + j], j < 4
-  bf16x4 qf[NC];
+  bf16x4 qf[NC], qfl[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    if (qv)
-      qf[c] = *reinterpret_cast<const bf16x4*>(qkv + (row0 + q) * ld + h * HD + c * 16 + g4);
-    else
-      qf[c] = bf16x4{0, 0, 0, 0};
+    qf[c] = bf16x4{0, 0, 0, 0};
+    qfl[c] = bf16x4{0, 0, 0, 0};
+    if (!qv) continue;
+    const int64_t off = (row0 + q) * ld + h * HD + c * 16 + g4;
+    if (SPLIT) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(qkv) + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint16_t hh = f2bf(v[j]);
+        qf[c][j] = (short)hh;
+        qfl[c][j] = (short)f2bf(v[j] - bf2f(hh));
+      }
+    } else {
+      qf[c] = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const uint16_t*>(qkv) + off);
+    }
   }
   f32x4 o[NC];
 #pragma unroll
@@ -55,40 +86,49 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const uint16_t* __restri
   float mrun = -INFINITY, lrun = 0.f;
   const float* brow = bias + ((int64_t)h * N + (qv ? q : 0)) * N;
 
-  for (int k0 = 0; k0 < N; k0 += kKT) {
+  for (int k0 = 0; k0 < N; k0 += KT) {
     __syncthreads();
-    // stage K rows and V^T for keys k0..k0+63 (16-B chunks of 8 head_dim values)
-    for (int it = tid; it < kKT * (HD / 8); it += 256) {
+    // stage K rows and V^T for keys k0..k0+KT-1 (chunks of 8 head_dim values)
+    for (int it = tid; it < KT * (HD / 8); it += 256) {
       const int kr = it / (HD / 8), ch = it % (HD / 8);
       const int key = k0 + kr;
-      bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+      bf16x8 kh = {0, 0, 0, 0, 0, 0, 0, 0}, kl = kh, vh = kh, vl = kh;
       if (key < N) {
-        const uint16_t* src = qkv + (row0 + key) * ld + h * HD + ch * 8;
-        kv = *reinterpret_cast<const bf16x8*>(src + C);
-        vv = *reinterpret_cast<const bf16x8*>(src + 2 * C);
+        const int64_t off = (row0 + key) * ld + h * HD + ch * 8;
+        load8_split<SPLIT>(qkv, off + C, kh, kl);
+        load8_split<SPLIT>(qkv, off + 2 * C, vh, vl);
       }
-      *reinterpret_cast<bf16x8*>(Ks + kr * KS + ch * 8) = kv;
+      *reinterpret_cast<bf16x8*>(&Ks[0][kr * KS + ch * 8]) = kh;
+      if (SPLIT) *reinterpret_cast<bf16x8*>(&Ks[NB - 1][kr * KS + ch * 8]) = kl;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * VS + kr] = (uint16_t)vv[j];
+      for (int j = 0; j < 8; ++j) {
+        Vt[0][(ch * 8 + j) * VS + kr] = (uint16_t)vh[j];
+        if (SPLIT) Vt[NB - 1][(ch * 8 + j) * VS + kr] = (uint16_t)vl[j];
+      }
     }
     __syncthreads();
 
-    // S^T for 4 sub-tiles of 16 keys: rows key = k0 + kt*16 + g4 + i, column = query
-    f32x4 s[4];
+    // S^T for NKT sub-tiles of 16 keys: rows key = k0 + kt*16 + g4 + i, column = query
+    f32x4 s[NKT];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
       s[kt] = f32x4{0, 0, 0, 0};
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const bf16x4 a =
-            *reinterpret_cast<const bf16x4*>(Ks + (kt * 16 + (lane & 15)) * KS + c * 16 + g4);
+        const int ko = (kt * 16 + (lane & 15)) * KS + c * 16 + g4;
+        const bf16x4 a = *reinterpret_cast<const bf16x4*>(&Ks[0][ko]);
+        if (SPLIT) {
+          const bf16x4 al = *reinterpret_cast<const bf16x4*>(&Ks[NB - 1][ko]);
+          s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, qf[c], s[kt], 0, 0, 0);
+          s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, qfl[c], s[kt], 0, 0, 0);
+        }
         s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, qf[c], s[kt], 0, 0, 0);
       }
     }
     // scale + relative-position bias (log2 domain), key mask
     float tmax = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
       const int kb = k0 + kt * 16 + g4;
       f32x4 bv;
       if (kb + 3 < N) {
@@ -113,14 +153,16 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const uint16_t* __restri
     const float alpha = exp2f(mrun - mnew);  // mrun = -inf on the first tile -> 0
     mrun = mnew;
     float psum = 0.f;
-    bf16x4 pf[4];
+    bf16x4 pf[NKT], pfl[NKT];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float p = exp2f(s[kt][i] - mnew);
         psum += p;
-        pf[kt][i] = (short)f2bf(p);
+        const uint16_t ph = f2bf(p);
+        pf[kt][i] = (short)ph;
+        pfl[kt][i] = SPLIT ? (short)f2bf(p - bf2f(ph)) : (short)0;
       }
     }
     lrun = lrun * alpha + psum;
@@ -128,9 +170,14 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const uint16_t* __restri
     for (int c = 0; c < NC; ++c) {
       o[c] *= alpha;
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const bf16x4 a =
-            *reinterpret_cast<const bf16x4*>(Vt + (c * 16 + (lane & 15)) * VS + kt * 16 + g4);
+      for (int kt = 0; kt < NKT; ++kt) {
+        const int vo = (c * 16 + (lane & 15)) * VS + kt * 16 + g4;
+        const bf16x4 a = *reinterpret_cast<const bf16x4*>(&Vt[0][vo]);
+        if (SPLIT) {
+          const bf16x4 al = *reinterpret_cast<const bf16x4*>(&Vt[NB - 1][vo]);
+          o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, pf[kt], o[c], 0, 0, 0);
+          o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pfl[kt], o[c], 0, 0, 0);
+        }
         o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pf[kt], o[c], 0, 0, 0);
       }
     }
@@ -140,27 +187,36 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const uint16_t* __restri
   lrun += __shfl_xor(lrun, 32, 64);
   if (qv) {
     const float inv = 1.f / lrun;
-    uint16_t* dst = out + (row0 + q) * C + h * HD + g4;
+    const int64_t off = (row0 + q) * C + h * HD + g4;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      bf16x4 r;
+      if (SPLIT) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off + c * 16) = o[c] * inv;
+      } else {
+        bf16x4 r;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) r[i] = (short)f2bf(o[c][i] * inv);
-      *reinterpret_cast<bf16x4*>(dst + c * 16) = r;
+        for (int i = 0; i < 4; ++i) r[i] = (short)f2bf(o[c][i] * inv);
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(out) + off + c * 16) = r;
+      }
     }
   }
 }
 
-int launch_attn_core(const uint16_t* qkv, const float* bias, uint16_t* out, int64_t Bw, int N,
-                     int heads, int hd, float scale, hipStream_t s) {
+int launch_attn_core(const void* qkv, const float* bias, void* out, int64_t Bw, int N,
+                     int heads, int hd, float scale, int prec, hipStream_t s) {
   if (Bw <= 0) return WF_OK;
   if (Bw > 65535) return fail(WF_E_SHAPE, "attention: more than 65535 windows per call");
   dim3 grid((unsigned)cdiv(N, kQB), (unsigned)heads, (unsigned)Bw);
   const float sl2 = scale * 1.4426950408889634f;
-#define WF_ATTN_CASE(HDV)                                                                 \
-  case HDV:                                                                               \
-    hipLaunchKernelGGL(attn_core_kernel<HDV>, grid, dim3(256), 0, s, qkv, bias, out, N,   \
-                       heads, sl2);                                                       \
+  const bool split = prec == PREC_SPLIT;
+#define WF_ATTN_CASE(HDV)                                                                  \
+  case HDV:                                                                                \
+    if (split)                                                                             \
+      hipLaunchKernelGGL((attn_core_kernel<HDV, (HDV >= 192 ? 32 : 64), true>), grid,      \
+                         dim3(256), 0, s, qkv, bias, out, N, heads, sl2);                  \
+    else                                                                                   \
+      hipLaunchKernelGGL((attn_core_kernel<HDV, 64, false>), grid, dim3(256), 0, s, qkv,   \
+                         bias, out, N, heads, sl2);                                        \
     break;
   switch (hd) {
     WF_ATTN_CASE(16)
@@ -186,6 +242,8 @@ __global__ void rel_pos_bias_kernel(const float* __restrict__ table, const int64
   for (int h = 0; h < heads; ++h) bias[h * NN + i] = table[r * heads + h];
 }
 
+static int64_t act_bytes(int prec) { return prec == PREC_SPLIT ? 4 : 2; }
+
 }  // namespace wf
 
 using namespace wf;
@@ -203,40 +261,44 @@ extern "C" int wf_rel_pos_bias(const float* table, const int64_t* index, float* 
 }
 
 extern "C" int64_t wf_window_attention_workspace_bytes(int64_t B, int64_t C, int64_t D1,
-                                                       int64_t H1, int64_t W1) {
+                                                       int64_t H1, int64_t W1, int precision) {
   const int64_t rows = B * D1 * H1 * W1;
-  const int64_t qkv = ((rows * 3 * C * 2) + 255) & ~(int64_t)255;
-  const int64_t ao = ((rows * C * 2) + 255) & ~(int64_t)255;
+  const int64_t e = act_bytes(precision);
+  const int64_t qkv = ((rows * 3 * C * e) + 255) & ~(int64_t)255;
+  const int64_t ao = ((rows * C * e) + 255) & ~(int64_t)255;
   return qkv + ao;
 }
 
 extern "C" int wf_window_attention_fwd(const float* x, const float* ln_w, const float* ln_b,
-                                       float ln_eps, const uint16_t* wqkv_bf16,
+                                       float ln_eps, const uint16_t* wqkv_bf16x2,
                                        const float* bqkv, const float* bias,
-                                       const uint16_t* wproj_bf16, const float* bproj, float* out,
-                                       void* workspace, int64_t B, int64_t C, int64_t D1,
-                                       int64_t H1, int64_t W1, int64_t ws, int64_t heads,
-                                       float scale, void* stream) {
+                                       const uint16_t* wproj_bf16x2, const float* bproj,
+                                       float* out, void* workspace, int64_t B, int64_t C,
+                                       int64_t D1, int64_t H1, int64_t W1, int64_t ws,
+                                       int64_t heads, float scale, int precision, void* stream) {
   WF_REQUIRE(B >= 1 && C >= 8 && C % 8 == 0, "C must be a positive multiple of 8");
   WF_REQUIRE(ws >= 1 && D1 % ws == 0 && H1 % ws == 0 && W1 % ws == 0,
              "the raster must tile into ws^3 windows (window_partition, wave_helper.py:459)");
   WF_REQUIRE(heads >= 1 && C % heads == 0, "dim must be divisible by num_heads");
+  WF_REQUIRE(precision == PREC_BF16 || precision == PREC_SPLIT, "unknown precision");
   WF_REQUIRE_PTR(x);
-  WF_REQUIRE_PTR(wqkv_bf16);
+  WF_REQUIRE_PTR(wqkv_bf16x2);
   WF_REQUIRE_PTR(bias);
-  WF_REQUIRE_PTR(wproj_bf16);
+  WF_REQUIRE_PTR(wproj_bf16x2);
   WF_REQUIRE_PTR(out);
   WF_REQUIRE_PTR(workspace);
   if (ln_w) WF_REQUIRE_PTR(ln_b);
   const int64_t N = ws * ws * ws;
   const int64_t rows = B * D1 * H1 * W1;
   const int64_t Bw = rows / N;
+  const int64_t e = act_bytes(precision);
   hipStream_t s = (hipStream_t)stream;
-  uint16_t* qkv = reinterpret_cast<uint16_t*>(workspace);
-  uint16_t* ao = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(workspace) +
-                                             (((rows * 3 * C * 2) + 255) & ~(int64_t)255));
+  void* qkv = workspace;
+  void* ao = reinterpret_cast<char*>(workspace) + (((rows * 3 * C * e) + 255) & ~(int64_t)255);
+  const int obf = precision == PREC_BF16;
   // 1. qkv = Linear(window_partition(norm1?(x)))
   GemmArgs g{};
+  g.prec = precision;
   g.a_src = x;
   g.a_bf16 = 0;
   g.a_C = (int)C;
@@ -251,29 +313,31 @@ extern "C" int wf_window_attention_fwd(const float* x, const float* ln_w, const 
   g.a_ln_w = ln_w;
   g.a_ln_b = ln_b;
   g.a_eps = ln_eps;
-  g.w = wqkv_bf16;
+  g.w = wqkv_bf16x2;
   g.M = rows;
   g.N = (int)(3 * C);
   g.K = (int)C;
   g.epi = EPI_STORE;
   g.bias = bqkv;
   g.out = qkv;
-  g.out_bf16 = 1;
+  g.out_bf16 = obf;
   g.ldo = 3 * C;
   int rc = launch_gemm(g, s, "wf_window_attention_fwd(qkv)");
   if (rc) return rc;
   // 2. softmax(q k^T * scale + bias) v
-  rc = launch_attn_core(qkv, bias, ao, Bw, (int)N, (int)heads, (int)(C / heads), scale, s);
+  rc = launch_attn_core(qkv, bias, ao, Bw, (int)N, (int)heads, (int)(C / heads), scale,
+                        precision, s);
   if (rc) return rc;
   // 3. proj; window-major rows == the reshaped raster (Q1)
   GemmArgs p{};
+  p.prec = precision;
   p.a_src = ao;
-  p.a_bf16 = 1;
+  p.a_bf16 = obf;
   p.a_C = (int)C;
   p.a_nseg = 1;
   p.a_map = MAP_IDENTITY;
   p.a_ln = LN_NONE;
-  p.w = wproj_bf16;
+  p.w = wproj_bf16x2;
   p.M = rows;
   p.N = (int)C;
   p.K = (int)C;

@@ -8,10 +8,12 @@
 //
 // Structure (one 256-thread workgroup = BM rows x all N columns):
 //   1. loader: the BM source rows (gathered, optionally LayerNorm'ed in fp32) are rounded to
-//      bf16 into an LDS tile A[BM][KP] -- A is read from HBM exactly once.
+//      bf16 into an LDS tile A[BM][KP] (plus the residual tile A_lo for PREC_SPLIT) -- A is
+//      read from HBM exactly once.
 //   2. MFMA: each wave owns 16 columns of a 64-column chunk; per 32-deep k step it loads its
-//      Wt[n][k..k+8] fragment straight from L2 (the weights are at most 1.2 MB) and issues
-//      BM/16 v_mfma_f32_16x16x32_bf16 against A fragments read by ds_read_b128.
+//      Wt[n][k..k+8] fragment(s) straight from L2 (the weights are at most 1.2 MB) and issues
+//      BM/16 v_mfma_f32_16x16x32_bf16 (x3 for PREC_SPLIT: hi*hi + lo*hi + hi*lo) against A
+//      fragments read by ds_read_b128.
 //   3. the fp32 accumulators land in an LDS row buffer R[BM][N]; the epilogue then walks rows
 //      (bias, LayerNorm+GELU or residual) and writes whole rows with 16-B stores.
 // Roofline: for every call site K, N <= 1536 and the arithmetic intensity is far below the
@@ -88,7 +90,7 @@ __device__ __forceinline__ float tpr_sum(float v) {
   return v;
 }
 
-template <int BM>
+template <int BM, bool SPLIT>
 __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPR = 256 / BM;  // threads per row in row-assigned phases
@@ -97,8 +99,10 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
   const int K32 = (K + 31) & ~31;
   const int KP = K32 + 8;        // bf16 row stride of A (16 B pad vs bank conflicts)
   const int NP = N + 4;          // fp32 row stride of R
+  const size_t abytes = ((size_t)BM * KP * 2 + 15) & ~(size_t)15;
   uint16_t* A = reinterpret_cast<uint16_t*>(smem);
-  float* R = reinterpret_cast<float*>(smem + (((size_t)BM * KP * 2 + 15) & ~(size_t)15));
+  uint16_t* Alo = reinterpret_cast<uint16_t*>(smem + abytes);  // PREC_SPLIT only
+  float* R = reinterpret_cast<float*>(smem + (SPLIT ? 2 : 1) * abytes);
   float* st = R + (size_t)BM * NP;  // [BM][2]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
     for (int item = tid; item < BM * KC; item += 256) {
       const int r = item / KC, ch = item - r * KC;
       const int64_t m = m0 + r;
-      bf16x8 o = {0, 0, 0, 0, 0, 0, 0, 0};
+      bf16x8 o = {0, 0, 0, 0, 0, 0, 0, 0}, olo = {0, 0, 0, 0, 0, 0, 0, 0};
       if (m < g.M && ch * 8 < K) {
         RowSource rs(g, m);
         float v[8];
@@ -164,9 +168,14 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
           for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * wv[j] + bv[j];
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(v[j]);
+        for (int j = 0; j < 8; ++j) {
+          const uint16_t hi = f2bf(v[j]);
+          o[j] = (short)hi;
+          if (SPLIT) olo[j] = (short)f2bf(v[j] - bf2f(hi));
+        }
       }
       *reinterpret_cast<bf16x8*>(A + (size_t)r * KP + ch * 8) = o;
+      if (SPLIT) *reinterpret_cast<bf16x8*>(Alo + (size_t)r * KP + ch * 8) = olo;
     }
   }
   __syncthreads();
@@ -177,19 +186,33 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
     const int n = n0 + wid * 16 + (lane & 15);
     const bool nv = n < N;
     const uint16_t* wrow = g.w + (int64_t)(nv ? n : 0) * K;
+    const uint16_t* wlo = wrow + (int64_t)N * K;  // lo plane (PREC_SPLIT)
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0, 0, 0, 0};
-    bf16x8 bnext = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (nv && kq < K) bnext = *reinterpret_cast<const bf16x8*>(wrow + kq);
+    const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    bf16x8 bnext = z8, blnext = z8;
+    if (nv && kq < K) {
+      bnext = *reinterpret_cast<const bf16x8*>(wrow + kq);
+      if (SPLIT) blnext = *reinterpret_cast<const bf16x8*>(wlo + kq);
+    }
     for (int k0 = 0; k0 < K32; k0 += 32) {
-      const bf16x8 b = bnext;
-      bnext = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (nv && k0 + 32 + kq < K) bnext = *reinterpret_cast<const bf16x8*>(wrow + k0 + 32 + kq);
+      const bf16x8 b = bnext, bl = blnext;
+      bnext = z8;
+      blnext = z8;
+      if (nv && k0 + 32 + kq < K) {
+        bnext = *reinterpret_cast<const bf16x8*>(wrow + k0 + 32 + kq);
+        if (SPLIT) blnext = *reinterpret_cast<const bf16x8*>(wlo + k0 + 32 + kq);
+      }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const bf16x8 a =
-            *reinterpret_cast<const bf16x8*>(A + (size_t)(mt * 16 + (lane & 15)) * KP + k0 + kq);
+        const size_t aoff = (size_t)(mt * 16 + (lane & 15)) * KP + k0 + kq;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + aoff);
+        if (SPLIT) {
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(Alo + aoff);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[mt], 0, 0, 0);
+        }
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[mt], 0, 0, 0);
       }
     }
@@ -268,10 +291,10 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
   }
 }
 
-static size_t gemm_lds_bytes(int BM, int K, int N) {
+static size_t gemm_lds_bytes(int BM, int K, int N, bool split) {
   const size_t K32 = (size_t)((K + 31) & ~31);
   const size_t a = ((size_t)BM * (K32 + 8) * 2 + 15) & ~(size_t)15;
-  return a + (size_t)BM * (N + 4) * 4 + (size_t)BM * 2 * 4;
+  return (split ? 2 : 1) * a + (size_t)BM * (N + 4) * 4 + (size_t)BM * 2 * 4;
 }
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
@@ -279,9 +302,10 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
   if (g.N <= 0 || g.N % 4 != 0) return fail(WF_E_SHAPE, std::string(who) + ": N must be a positive multiple of 4");
   if (g.a_C % 8 != 0) return fail(WF_E_SHAPE, std::string(who) + ": channels must be a multiple of 8");
   if (g.M <= 0) return WF_OK;
+  const bool split = g.prec == PREC_SPLIT;
   int BM = 64;
-  while (BM > 16 && gemm_lds_bytes(BM, g.K, g.N) > 80 * 1024) BM >>= 1;
-  const size_t lds = gemm_lds_bytes(BM, g.K, g.N);
+  while (BM > 16 && gemm_lds_bytes(BM, g.K, g.N, split) > 80 * 1024) BM >>= 1;
+  const size_t lds = gemm_lds_bytes(BM, g.K, g.N, split);
   if (lds > 160 * 1024) return fail(WF_E_SHAPE, std::string(who) + ": K/N too large for the LDS tile");
   const unsigned blocks = (unsigned)cdiv(g.M, BM);
   auto go = [&](auto kern) {
@@ -290,10 +314,18 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, g);
   };
-  switch (BM) {
-    case 64: go(gemm_ares_kernel<64>); break;
-    case 32: go(gemm_ares_kernel<32>); break;
-    default: go(gemm_ares_kernel<16>); break;
+  if (split) {
+    switch (BM) {
+      case 64: go(gemm_ares_kernel<64, true>); break;
+      case 32: go(gemm_ares_kernel<32, true>); break;
+      default: go(gemm_ares_kernel<16, true>); break;
+    }
+  } else {
+    switch (BM) {
+      case 64: go(gemm_ares_kernel<64, false>); break;
+      case 32: go(gemm_ares_kernel<32, false>); break;
+      default: go(gemm_ares_kernel<16, false>); break;
+    }
   }
   return check_launch(who);
 }

@@ -4,14 +4,23 @@
 
 namespace wf {
 
+// Arithmetic of the MFMA operands (see include/waveformer_hip.h, WF_PREC_*):
+//   PREC_BF16  -- operands rounded to bf16, fp32 accumulation; intermediates stored bf16.
+//   PREC_SPLIT -- "bf16x3": every fp32 operand x is carried as hi = bf16(x) plus
+//                 lo = bf16(x - hi); products use hi*hi + lo*hi + hi*lo (the lo*lo term is
+//                 below 2^-17 relative), i.e. fp32-faithful results on the bf16 MFMA pipes;
+//                 intermediates stay fp32.
+enum Prec { PREC_BF16 = 0, PREC_SPLIT = 1 };
+
 // ---- A-resident MFMA GEMM:  out[m, n] = epilogue( sum_k A[m, k] * Wt[n, k] ) -------------
 // A rows are produced by a loader (gather + optional LayerNorm + bf16 rounding) into LDS once
-// per workgroup; the weight Wt [N][K] (bf16) streams from L2.
+// per workgroup; the weight Wt [2][N][K] (bf16 hi plane, then lo plane) streams from L2.
 enum RowMap { MAP_IDENTITY = 0, MAP_WINDOW = 1, MAP_MERGE = 2 };
 enum LnMode { LN_NONE = 0, LN_GIVEN = 1, LN_COMPUTE = 2 };
 enum EpiMode { EPI_STORE = 0, EPI_LN_GELU = 1, EPI_RESID = 2 };
 
 struct GemmArgs {
+  int prec;              // Prec
   // ---- A loader
   const void* a_src;     // fp32 or bf16 rows
   int a_bf16;            // 1: a_src is bf16
@@ -26,7 +35,7 @@ struct GemmArgs {
   const float* a_ln_b;
   float a_eps;
   // ---- B
-  const uint16_t* w;     // [N][K] bf16
+  const uint16_t* w;     // [2][N][K] bf16 (hi plane; lo plane read only for PREC_SPLIT)
   // ---- problem
   int64_t M;
   int N, K;
@@ -49,13 +58,14 @@ struct GemmArgs {
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);
 
-// ---- windowed attention core over a (B_, N, 3C) bf16 qkv buffer -------------------------
-int launch_attn_core(const uint16_t* qkv, const float* bias, uint16_t* out, int64_t Bw, int N,
-                     int heads, int hd, float scale, hipStream_t s);
+// ---- windowed attention core over a (B_, N, 3C) qkv buffer (bf16, or fp32 when SPLIT) ----
+int launch_attn_core(const void* qkv, const float* bias, void* out, int64_t Bw, int N,
+                     int heads, int hd, float scale, int prec, hipStream_t s);
 
-// ---- depthwise 3^3 conv + bias + LayerNorm + GELU over a channel-last bf16 volume -------
-int launch_dwconv_ln_gelu(const uint16_t* in, const float* w, const float* b,
-                          const float* ln_w, const float* ln_b, float eps, uint16_t* out,
-                          int B, int Hd, int D, int H, int W, hipStream_t s);
+// ---- depthwise 3^3 conv + bias + LayerNorm + GELU over a channel-last volume ------------
+// (bf16 storage for PREC_BF16, fp32 for PREC_SPLIT)
+int launch_dwconv_ln_gelu(const void* in, const float* w, const float* b, const float* ln_w,
+                          const float* ln_b, float eps, void* out, int B, int Hd, int D, int H,
+                          int W, int prec, hipStream_t s);
 
 }  // namespace wf

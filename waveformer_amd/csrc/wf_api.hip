@@ -28,6 +28,18 @@ __global__ void cast_f32_bf16_kernel(const float* __restrict__ in, uint16_t* __r
   for (; i < n; i += stride) out[i] = f2bf(in[i]);
 }
 
+__global__ void split_f32_bf16x2_kernel(const float* __restrict__ in, uint16_t* __restrict__ out,
+                                        int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    const float v = in[i];
+    const uint16_t hi = f2bf(v);
+    out[i] = hi;
+    out[n + i] = f2bf(v - bf2f(hi));
+  }
+}
+
 }  // namespace wf
 
 extern "C" int wf_abi_version(void) { return WF_ABI_VERSION; }
@@ -44,4 +56,16 @@ extern "C" int wf_cast_f32_to_bf16(const float* in, uint16_t* out, int64_t n, vo
   hipLaunchKernelGGL(wf::cast_f32_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0,
                      (hipStream_t)stream, in, out, n);
   return wf::check_launch("wf_cast_f32_to_bf16");
+}
+
+extern "C" int wf_split_f32_to_bf16x2(const float* in, uint16_t* out, int64_t n, void* stream) {
+  WF_REQUIRE(n >= 0, "n < 0");
+  if (n == 0) return WF_OK;
+  WF_REQUIRE_PTR(in);
+  WF_REQUIRE_PTR(out);
+  int64_t blocks = wf::cdiv(n, 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wf::split_f32_bf16x2_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     (hipStream_t)stream, in, out, n);
+  return wf::check_launch("wf_split_f32_to_bf16x2");
 }

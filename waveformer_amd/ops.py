@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -43,19 +44,59 @@ def _check(t: torch.Tensor, name: str, dtype=torch.float32, contiguous=True) -> 
         raise ValueError(f"{name}: expected a contiguous tensor")
 
 
-def bf16_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None) -> torch.Tensor:
-    """bf16 copy of an fp32 weight (made by the wf_cast kernel), cached on the parameter
-    until it changes (in-place optimizer steps / load_state_dict bump its _version)."""
+# ------------------------------------------------------------------------------------------
+# precision of the MFMA operands (include/waveformer_hip.h, WF_PREC_*)
+# ------------------------------------------------------------------------------------------
+PRECISIONS = {"bf16": 0, "bf16x3": 1}
+_precision = os.environ.get("WAVEFORMER_PRECISION", "bf16x3")
+if _precision not in PRECISIONS:
+    raise ValueError(f"WAVEFORMER_PRECISION={_precision!r}: expected one of {sorted(PRECISIONS)}")
+
+
+def set_precision(p: str) -> None:
+    """'bf16x3' (default): fp32-faithful split-bf16 MFMA operands, fp32 intermediates.
+    'bf16': plain bf16 operands and bf16 GEMM-to-GEMM intermediates (fastest)."""
+    global _precision
+    if p not in PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {p!r}")
+    _precision = p
+
+
+def get_precision() -> str:
+    return _precision
+
+
+class precision:
+    """Context manager: `with ops.precision("bf16"): model(x)`."""
+
+    def __init__(self, p: str):
+        self.p = p
+
+    def __enter__(self):
+        self.prev = get_precision()
+        set_precision(self.p)
+
+    def __exit__(self, *exc):
+        set_precision(self.prev)
+
+
+def _prec() -> int:
+    return PRECISIONS[_precision]
+
+
+def split_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None) -> torch.Tensor:
+    """[2][N][K] bf16 {hi, lo} planes of an fp32 weight (wf_split_f32_to_bf16x2), cached on the
+    parameter until it changes (in-place optimizer steps / load_state_dict bump _version)."""
     ver = p._version
-    ent = getattr(p, "_wf_bf16", None)
+    ent = getattr(p, "_wf_bf16x2", None)
     if ent is not None and ent[0] == ver and ent[1] == p.data_ptr():
         return ent[2]
     src = p.detach()
     _check(src, "weight")
-    out = torch.empty(src.shape if shape is None else shape, dtype=torch.bfloat16,
+    out = torch.empty((2,) + tuple(src.shape if shape is None else shape), dtype=torch.bfloat16,
                       device=src.device)
-    _lib.call("wf_cast_f32_to_bf16", src.data_ptr(), out.data_ptr(), src.numel(), _stream())
-    p._wf_bf16 = (ver, p.data_ptr(), out)
+    _lib.call("wf_split_f32_to_bf16x2", src.data_ptr(), out.data_ptr(), src.numel(), _stream())
+    p._wf_bf16x2 = (ver, p.data_ptr(), out)
     return out
 
 
@@ -194,8 +235,8 @@ def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torc
     Returns (B, D1, H1, W1, C) whose rows are the window-major attention outputs."""
     _check(x_cl, "x")
     B, D1, H1, W1, C = x_cl.shape
-    wq = bf16_weight(wqkv)
-    wp = bf16_weight(wproj)
+    wq = split_weight(wqkv)
+    wp = split_weight(wproj)
     if bqkv is not None:
         _check(bqkv, "qkv.bias")
     if bproj is not None:
@@ -209,12 +250,13 @@ def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torc
     if ln is not None:
         lw, lb, eps = ln
     out = torch.empty_like(x_cl)
-    wsb = _lib.query("wf_window_attention_workspace_bytes", B, C, D1, H1, W1)
+    prec = _prec()
+    wsb = _lib.query("wf_window_attention_workspace_bytes", B, C, D1, H1, W1, prec)
     work = torch.empty(wsb, dtype=torch.uint8, device=x_cl.device)
     _lib.call("wf_window_attention_fwd", x_cl.data_ptr(), _ptr(lw), _ptr(lb), float(eps),
               wq.data_ptr(), _ptr(bqkv), bias.data_ptr(), wp.data_ptr(), _ptr(bproj),
               out.data_ptr(), work.data_ptr(), B, C, D1, H1, W1, ws, heads, float(scale),
-              _stream())
+              prec, _stream())
     return out
 
 
@@ -258,10 +300,11 @@ def ccf_ffn(xh: torch.Tensor, stats: Optional[torch.Tensor], norm2: Optional[tor
     _check(xh, "x")
     B, D, H, W, C = xh.shape
     hid = mlp.C_hid
-    pw = bf16_weight(mlp.pwconv.weight, (hid, C))
-    fc = bf16_weight(mlp.fc.weight)
+    pw = split_weight(mlp.pwconv.weight, (hid, C))
+    fc = split_weight(mlp.fc.weight)
+    prec = _prec()
     out = torch.empty_like(xh)
-    wsb = _lib.query("wf_ccf_ffn_workspace_bytes", B, C, hid, D, H, W)
+    wsb = _lib.query("wf_ccf_ffn_workspace_bytes", B, C, hid, D, H, W, prec)
     work = torch.empty(wsb, dtype=torch.uint8, device=xh.device)
     n2w = n2b = None
     if stats is not None:
@@ -272,7 +315,7 @@ def ccf_ffn(xh: torch.Tensor, stats: Optional[torch.Tensor], norm2: Optional[tor
               mlp.dwconv.bias.data_ptr(), mlp.norm2.weight.data_ptr(), mlp.norm2.bias.data_ptr(),
               float(mlp.norm2.eps), fc.data_ptr(), _ptr(mlp.fc.bias), _ptr(branch_scale),
               out.data_ptr(),
-              work.data_ptr(), B, C, hid, D, H, W, _stream())
+              work.data_ptr(), B, C, hid, D, H, W, prec, _stream())
     return out
 
 
@@ -283,11 +326,11 @@ def patch_merging(x_cl: torch.Tensor, norm: torch.nn.LayerNorm, reduction: torch
                   v2: bool = False) -> torch.Tensor:
     _check(x_cl, "x")
     B, D, H, W, C = x_cl.shape
-    red = bf16_weight(reduction.weight)
+    red = split_weight(reduction.weight)
     out = torch.empty((B, D // 2, H // 2, W // 2, 2 * C), dtype=torch.float32, device=x_cl.device)
     _lib.call("wf_patch_merging_fwd", x_cl.data_ptr(), norm.weight.data_ptr(),
               norm.bias.data_ptr(), float(norm.eps), red.data_ptr(), int(bool(v2)), out.data_ptr(),
-              B, C, D, H, W, _stream())
+              B, C, D, H, W, _prec(), _stream())
     return out
 
 
