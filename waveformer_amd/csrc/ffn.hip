@@ -71,22 +71,36 @@ __global__ __launch_bounds__(512) void dwconv_ln_gelu_kernel(
       wt[k].w = w[(4 * chunk + 3) * 27 + k];
     }
     const f32x4 bv = reinterpret_cast<const f32x4*>(bias)[chunk];
-    auto ld = [&](int zz, int yy, int xx) -> vec {
-      if (zz < 0 || zz >= D || yy < 0 || yy >= H || xx < 0 || xx >= W) return S::zero();
-      return *reinterpret_cast<const vec*>(in + ((((int64_t)b * D + zz) * H + yy) * W + xx) * Hd +
-                                           4 * chunk);
+    // The 9 (dz, dy) input rows: clamped base pointers + a validity mask.  Loads are always
+    // issued (clamped in-bounds addresses) and zeroed by a select afterwards: a branch around
+    // each load would make hipcc wait vmcnt(0) per load and serialise the 9-load batch.
+    const T* rowp[9];
+    unsigned rvalid = 0;
+#pragma unroll
+    for (int r9 = 0; r9 < 9; ++r9) {
+      const int zz = z + r9 / 3 - 1, yy = y + r9 % 3 - 1;
+      const bool ok = zz >= 0 && zz < D && yy >= 0 && yy < H;
+      rvalid |= (ok ? 1u : 0u) << r9;
+      const int zc = min(max(zz, 0), D - 1), yc = min(max(yy, 0), H - 1);
+      rowp[r9] = in + (((int64_t)b * D + zc) * H + yc) * (int64_t)W * Hd + 4 * chunk;
+    }
+    auto ld = [&](int r9, int xx) -> vec {
+      const int xc = min(max(xx, 0), W - 1);
+      const vec v = *reinterpret_cast<const vec*>(rowp[r9] + (int64_t)xc * Hd);
+      const bool ok = ((rvalid >> r9) & 1u) && xx >= 0 && xx < W;
+      return ok ? v : S::zero();
     };
     vec win[9][3];
 #pragma unroll
     for (int r9 = 0; r9 < 9; ++r9) {
-      win[r9][0] = ld(z + r9 / 3 - 1, y + r9 % 3 - 1, xb - 1);
-      win[r9][1] = ld(z + r9 / 3 - 1, y + r9 % 3 - 1, xb);
+      win[r9][0] = ld(r9, xb - 1);
+      win[r9][1] = ld(r9, xb);
     }
 #pragma unroll 1
     for (int xi = 0; xi < TW; ++xi) {
       const int x = xb + xi;
 #pragma unroll
-      for (int r9 = 0; r9 < 9; ++r9) win[r9][2] = ld(z + r9 / 3 - 1, y + r9 % 3 - 1, x + 1);
+      for (int r9 = 0; r9 < 9; ++r9) win[r9][2] = ld(r9, x + 1);
       f32x4 acc = bv;
 #pragma unroll
       for (int r9 = 0; r9 < 9; ++r9)

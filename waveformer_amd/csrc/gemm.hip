@@ -302,6 +302,8 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
   if (g.N <= 0 || g.N % 4 != 0) return fail(WF_E_SHAPE, std::string(who) + ": N must be a positive multiple of 4");
   if (g.a_C % 8 != 0) return fail(WF_E_SHAPE, std::string(who) + ": channels must be a multiple of 8");
   if (g.M <= 0) return WF_OK;
+  static const bool ares_only = getenv("WF_GEMM_ARES_ONLY") != nullptr;  // A/B switch
+  if (!ares_only && try_launch_gemm_rows(g, s)) return check_launch(who);
   const bool split = g.prec == PREC_SPLIT;
   int BM = 64;
   while (BM > 16 && gemm_lds_bytes(BM, g.K, g.N, split) > 80 * 1024) BM >>= 1;

@@ -57,6 +57,8 @@ struct GemmArgs {
 };
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);
+// streaming variant (gemm_rows.hip); returns 1 if it took the shape, 0 to fall back
+int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s);
 
 // ---- windowed attention core over a (B_, N, 3C) qkv buffer (bf16, or fp32 when SPLIT) ----
 int launch_attn_core(const void* qkv, const float* bias, void* out, int64_t Bw, int N,
