@@ -11,10 +11,13 @@ runs N independent replicas -- 128^3 crops do not shard -- and repor
 whole-job rate: B * K * N volumes / the slowest rank's wall time.
 
 Rank 0 prints ONE JSON line.  Besides the driver contract it carries:
-  roofline     : the dominant HBM-bound kernel's algorithmic bytes per launch / its average
-                 launch duration, timed with HIP events on the launch stream inside the timed
-                 region, against the 8 TB/s HBM3E peak (traffic: PMC bytes from
-                 profiles/*pmc*.json when present, else null)
+  roofline     : the dominant kernel of the step (the CCF_FFN depthwise conv): its algorithmic
+                 bytes per launch / its average launch duration, timed with HIP events on the
+                 launch stream (eager repeats of the step after the timed region), against the
+                 8 TB/s HBM3E peak (traffic: PMC bytes per launch from profiles/*pmc*.json when
+                 present, else null)
+  rooflines    : the same for the DWT (north-star HBM target), the multi-scale fuse, and the
+                 window attention op (MFMA-bound: algorithmic FLOPs vs the dense bf16 peak)
   cpu_baseline : the oracle (CPU restatement of the reference, fp32 PyTorch) timed on this
                  host on one volume (rank 0, N = 1 only)
   parity       : Dice (TC/WT/ET) of the full Waveformer's labels at 128^3 x 4 against the
@@ -38,6 +41,10 @@ sys.path.insert(0, REPO)
 
 METRIC = "128³×4 volumes/sec fwd (1/2/4/8 MI355X) + Dice Δ vs reference"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
+# bench op name -> kernel-name substring in the PMC summary (profiles/*pmc*.json)
+PMC_KERNEL = {"ccf_ffn_dwconv": "dwconv3d_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
+              "msfuse": "msfuse", "proj_out": "proj_out"}
 
 
 def parse():
@@ -58,10 +65,30 @@ def parse():
 # ------------------------------------------------------------------------------------------
 # per-launch timing of one op with HIP events on its stream
 # ------------------------------------------------------------------------------------------
-class OpTimer:
-    """Wraps waveformer_amd.ops.<name>; records (algorithmic bytes, start, end) per launch."""
+def _dw_bytes(a, kw, out):
+    """CCF_FFN depthwise conv: read h1 + write h2 (positions x hidden, fp32 for bf16x3, bf16
+    for bf16) + the (mean, M2) partial per 32 channels of every position."""
+    from waveformer_amd import ops
+    P, Hd = a[1], a[2]
+    e = 4 if ops.get_precision() == "bf16x3" else 2
+    return 2 * P * Hd * e + P * (Hd // 32) * 8
 
-    BYTES = {
+
+def _attn_flops(a, kw, out):
+    """window attention: qkv (2*T*C*3C) + QK^T and PV (2 * 2*T*N*C) + proj (2*T*C*C)."""
+    x = a[0]
+    T, C = x.numel() // x.shape[-1], x.shape[-1]
+    N = a[6] ** 3
+    return 2 * T * C * 3 * C + 4 * T * N * C + 2 * T * C * C
+
+
+class OpTimer:
+    """Wraps waveformer_amd.ops.<name>; records (algorithmic bytes or flops, start, end) per
+    launch with HIP events on the current (= launch) stream."""
+
+    WORK = {
+        # CCF_FFN depthwise 3^3 conv (the step's dominant kernel)
+        "ccf_ffn_dwconv": _dw_bytes,
         # 1-level Haar: read the (B,D,H,W,C) input once, write 8 bands of 1/8 size
         "dwt3d_haar": lambda a, kw, out: 2 * a[0].numel() * 4,
         # out = shortcut + sum trilinear(src): read shortcut + sources, write out + 8 B stats/row
@@ -69,6 +96,8 @@ class OpTimer:
         + (0 if out[1] is None else out[1].numel() * 4),
         # LN + transpose: read + write
         "proj_out": lambda a, kw, out: 2 * a[0].numel() * 4,
+        # windowed attention (qkv GEMM + core + proj GEMM), FLOPs
+        "window_attention": _attn_flops,
     }
 
     def __init__(self, name):
@@ -85,21 +114,22 @@ class OpTimer:
             s.record()
             out = self.orig(*a, **kw)
             e.record()
-            self.rec.append((self.BYTES[name](a, kw, out), s, e))
+            self.rec.append((self.WORK[name](a, kw, out), s, e))
             return out
 
         setattr(ops, name, wrapped)
         # the network_models modules import `ops` as a module, so the patch is visible to them
 
     def summary(self):
+        """The largest launch class (max work per launch): its work, mean duration and rate."""
         torch.cuda.synchronize()
         if not self.rec:
             return None
         big = max(b for b, _, _ in self.rec)
         sel = [(b, s.elapsed_time(e)) for b, s, e in self.rec if b == big]
         avg_ms = sum(t for _, t in sel) / len(sel)
-        return {"bytes_per_launch": big, "avg_ms": avg_ms, "launches": len(sel),
-                "achieved_gbs": big / (avg_ms * 1e-3) / 1e9}
+        return {"work_per_launch": big, "avg_ms": avg_ms, "launches": len(sel),
+                "rate": big / (avg_ms * 1e-3)}
 
 
 def pmc_traffic(kernel_substr):
@@ -182,8 +212,9 @@ def main():
     x = torch.randn(args.batch, 4, args.img, args.img, args.img, device=dev,
                     generator=torch.Generator(device=dev).manual_seed(1234 + rank))
 
-    roof_op = args.roofline_op if args.roofline_op != "auto" else "dwt3d_haar"
-    timer = OpTimer(roof_op)
+    roof_op = args.roofline_op if args.roofline_op != "auto" else "ccf_ffn_dwconv"
+    timers = {n: OpTimer(n) for n in dict.fromkeys([roof_op, "dwt3d_haar", "msfuse",
+                                                    "window_attention"])}
 
     def step():
         with torch.no_grad():
@@ -233,12 +264,14 @@ def main():
 
     # per-launch roofline timing of the dominant streaming kernel (eager launches, so the HIP
     # events sit on the launch stream around each launch)
-    timer.active = True
+    for t in timers.values():
+        t.active = True
     with torch.no_grad():
         for _ in range(max(2, min(args.steps, 10))):
             model(x)
-    timer.active = False
-    roof = timer.summary()
+    for t in timers.values():
+        t.active = False
+    roofs = {n: t.summary() for n, t in timers.items()}
 
     if rank == 0:
         vols = args.batch * args.steps * world
@@ -262,16 +295,25 @@ def main():
                        "parallelism": f"replicas x{world} (no data-path collective)",
                        "hip_graph": graph is not None},
         }
-        if roof:
-            traffic = pmc_traffic("dwt3d_haar_fwd") if roof_op == "dwt3d_haar" else None
-            out["roofline"] = {"bound": "hbm", "kernel": roof_op,
-                               "achieved": round(roof["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
-                               "unit": "GB/s",
-                               "frac": round(roof["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                               "traffic": traffic,
-                               "algorithmic_bytes_per_launch": roof["bytes_per_launch"],
-                               "avg_launch_us": round(roof["avg_ms"] * 1e3, 2),
-                               "launches_timed": roof["launches"]}
+        def roofline(name, r):
+            if name == "window_attention":  # MFMA-bound: algorithmic FLOPs vs dense bf16 peak
+                ach = r["rate"] / 1e12
+                return {"bound": "mfma", "kernel": name, "achieved": round(ach, 2),
+                        "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                        "algorithmic_flops_per_launch": r["work_per_launch"],
+                        "avg_launch_us": round(r["avg_ms"] * 1e3, 2),
+                        "launches_timed": r["launches"]}
+            ach = r["rate"] / 1e9
+            return {"bound": "hbm", "kernel": name, "achieved": round(ach, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                    "traffic": pmc_traffic(PMC_KERNEL.get(name, name)),
+                    "algorithmic_bytes_per_launch": r["work_per_launch"],
+                    "avg_launch_us": round(r["avg_ms"] * 1e3, 2), "launches_timed": r["launches"]}
+
+        if roofs.get(roof_op):
+            out["roofline"] = roofline(roof_op, roofs[roof_op])
+        out["rooflines"] = {n: roofline(n, r) for n, r in roofs.items() if r and n != roof_op}
         if args.parity:
             try:
                 out["parity"] = parity_dice(dev)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 2
+#define WF_ABI_VERSION 3
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1 };
 
@@ -156,6 +156,17 @@ int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* n2_w, const
                    float* out, void* workspace,
                    int64_t B, int64_t C, int64_t hidden, int64_t D, int64_t H, int64_t W,
                    int precision, void* stream);
+/* The same three launches one at a time (stage 1: pwconv GEMM -> workspace h1; 2: depthwise
+ * conv h1 -> h2 + per-32-channel LayerNorm partials; 3: LN2 + GELU + fc GEMM + residuals ->
+ * out), with the same arguments; stage 0 runs all three (== wf_ccf_ffn_fwd).  Lets a caller
+ * time or interleave the stages.                                                           */
+int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats, const float* n2_w,
+                     const float* n2_b, const uint16_t* pw_bf16x2, const float* pw_b,
+                     const float* ln1_w, const float* ln1_b, float eps1, const float* dw_w,
+                     const float* dw_b, const float* ln2_w, const float* ln2_b, float eps2,
+                     const uint16_t* fc_bf16x2, const float* fc_b, const float* branch_scale,
+                     float* out, void* workspace, int64_t B, int64_t C, int64_t hidden,
+                     int64_t D, int64_t H, int64_t W, int precision, void* stream);
 
 /* ---- a9: PatchMerging (quirk Q3) ------------------------------------------------------ */
 /* Replaces PatchMerging.forward (wave_helper.py:173-194): the 8-way strided gather with its

@@ -121,6 +121,13 @@ def cases() -> Dict[str, Case]:
                        (1, 4, 32, 32, 32), 22,
                        lambda sd, x: R.waveformer(sd, x, heads=[3, 6, 12, 24], depths=[2] * 4),
                        "full")
+    c["full32hf"] = Case("full32hf", partial(NM.Waveformer, img_size=(32,) * 3, in_chans=4,
+                                             out_chans=4,
+                                             network_config={"transformer": {"hf_refinement": True}}),
+                         (1, 4, 32, 32, 32), 23,
+                         lambda sd, x: R.waveformer(sd, x, heads=[3, 6, 12, 24], depths=[2] * 4,
+                                                    hf_refine=True),
+                         "full")
     c["enc128"] = Case("enc128", partial(NM.MultiscaleTransformer, img_size=(128,) * 3,
                                          in_chans=4, qkv_bias=True, norm_layer=_ln6()),
                        (1, 4, 128, 128, 128), 0,
@@ -133,6 +140,19 @@ def cases() -> Dict[str, Case]:
                         (1, 4, 128, 128, 128), 0,
                         lambda sd, x: R.waveformer(sd, x, heads=[3, 6, 12, 24], depths=[2] * 4),
                         "labels")
+    # config 5: 192^3 x 4 crops, window 12 (N = 1728), HF refinement branch on
+    c["enc192"] = Case("enc192", partial(NM.MultiscaleTransformer, img_size=(192,) * 3,
+                                         in_chans=4, qkv_bias=True, norm_layer=_ln6()),
+                       (1, 4, 192, 192, 192), 5,
+                       lambda sd, x: R.encoder(sd, x, heads=[3, 6, 12, 24], depths=[2] * 4),
+                       "summary_encoder")
+    c["full192hf"] = Case("full192hf", partial(NM.Waveformer, img_size=(192,) * 3, in_chans=4,
+                                               out_chans=4,
+                                               network_config={"transformer": {"hf_refinement": True}}),
+                          (1, 4, 192, 192, 192), 5,
+                          lambda sd, x: R.waveformer(sd, x, heads=[3, 6, 12, 24], depths=[2] * 4,
+                                                     hf_refine=True),
+                          "labels")
     return c
 
 

@@ -99,7 +99,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
     ap.add_argument("--skip-128", action="store_true")
+    ap.add_argument("--groups", default="small,128",
+                    help="comma list of: small, 128, hf32, 192.  Arrays of groups not listed "
+                         "are kept from the existing ref_fixtures.npz")
     args = ap.parse_args()
+    groups = set(args.groups.split(","))
+    if args.skip_128:
+        groups.discard("128")
     sys.dont_write_bytecode = True
     _install_standins()
     sys.path.insert(0, args.reference)
@@ -108,7 +114,44 @@ def main():
     torch.set_num_threads(8)
     torch.set_grad_enabled(False)
     ln6 = partial(nn.LayerNorm, eps=1e-6)
-    out = {}
+    dst = os.path.join(HERE, "ref_fixtures.npz")
+    out = dict(np.load(dst)) if os.path.exists(dst) else {}
+    t0 = time.time()
+    if "small" in groups:
+        _small(out, ln6, Attention, Block, CCF_FFN, MultiscaleTransformer, PatchMerging,
+               Waveformer)
+    if "hf32" in groups:
+        # full model with the high-frequency refinement branch (idwt_upsample.py:39-50, 96-105)
+        net = apply_rule(Waveformer(img_size=(32,) * 3, in_chans=4, out_chans=4,
+                                    network_config={"transformer": {"hf_refinement": True}})).eval()
+        _full("full32hf", net(seeded_randn((1, 4, 32, 32, 32), 23)), out)
+    if "128" in groups:
+        _big128(out, ln6, MultiscaleTransformer, Waveformer)
+    if "192" in groups:
+        # config 5: 192^3 x 4 (window 12, N = 1728) encoder summaries and the full model with
+        # the HF refinement branch -> labels for the Dice check
+        x192 = seeded_randn((1, 4, 192, 192, 192), 5)
+        enc = apply_rule(MultiscaleTransformer(img_size=(192,) * 3, in_chans=4, qkv_bias=True,
+                                               norm_layer=ln6)).eval()
+        t1 = time.time()
+        outs, hfs = enc(x192)
+        print(f"enc192 {time.time() - t1:.1f}s")
+        for i, o in enumerate(outs):
+            _summary(f"enc192_out{i}", o, out)
+        del enc, outs, hfs
+        net = apply_rule(Waveformer(img_size=(192,) * 3, in_chans=4, out_chans=4,
+                                    network_config={"transformer": {"hf_refinement": True}})).eval()
+        t1 = time.time()
+        logits = net(x192)
+        print(f"full192hf {time.time() - t1:.1f}s")
+        _summary("full192hf", logits, out)
+        out["full192hf_labels"] = logits.argmax(1).to(torch.uint8).numpy()
+
+    np.savez_compressed(dst, **out)
+    print("wrote", len(out), "arrays in", f"{time.time() - t0:.1f}s")
+
+
+def _small(out, ln6, Attention, Block, CCF_FFN, MultiscaleTransformer, PatchMerging, Waveformer):
     t0 = time.time()
 
     # ---- Attention (attention.py:83-104)
@@ -165,7 +208,10 @@ def main():
         spec = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()]
         out[tag + "__keys"] = np.frombuffer(json.dumps(spec).encode(), dtype=np.uint8)
 
-    if not args.skip_128:
+
+
+def _big128(out, ln6, MultiscaleTransformer, Waveformer):
+    if True:
         # ---- config 2: encoder at 128^3 x 4 (summaries), full model labels
         x128 = seeded_randn((1, 4, 128, 128, 128), 0)
         enc = apply_rule(MultiscaleTransformer(img_size=(128,) * 3, in_chans=4, qkv_bias=True,
@@ -185,9 +231,6 @@ def main():
         print(f"full128 {time.time() - t1:.1f}s")
         _summary("full128", logits, out)
         out["full128_labels"] = logits.argmax(1).to(torch.uint8).numpy()
-
-    np.savez_compressed(os.path.join(HERE, "ref_fixtures.npz"), **out)
-    print("wrote", len(out), "arrays in", f"{time.time() - t0:.1f}s")
 
 
 if __name__ == "__main__":

@@ -183,7 +183,7 @@ TOL = {"bf16x3": {"tensor": 5e-5, "block": 5e-5, "encoder": 1e-4, "full": 1e-4},
 @pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
 @pytest.mark.parametrize("name", ["attn_ws8", "attn_ws2_h1", "attn_ws4_h2", "merge", "ccf_ffn",
                                   "block_l3", "block_l1", "block_l0", "block_ss_l2", "enc32",
-                                  "full32"])
+                                  "full32", "full32hf"])
 def test_module_vs_reference_golden_and_oracle(name, prec):
     from waveformer_amd import ops
     case = C.cases()[name]
@@ -224,6 +224,34 @@ def test_encoder128_vs_reference_summaries():
         assert abs(math.sqrt(sums[1]) / math.sqrt(ref[1]) - 1) <= tol, k
         assert abs(sums[2] - ref[2]) <= 10 * tol * math.sqrt(ref[1]), k
         assert C.rel_l2(sample, C.g(k + "__sample")) <= tol, (k, C.rel_l2(sample, C.g(k + "__sample")))
+
+
+def test_encoder192_vs_reference_summaries():
+    """config 5 widths at 192^3 x 4: window 12 (N = 1728 tokens, 23^3-row bias table)."""
+    case = C.cases()["enc192"]
+    m, _ = C.build(case, DEV)
+    with torch.no_grad():
+        outs, _ = m(cuda(C.case_input(case)))
+    for i, t in enumerate(outs):
+        k = f"enc192_out{i}"
+        assert tuple(t.shape) == tuple(C.golden()[k + "__shape"]), k
+        sums, sample = C.summary(t)
+        ref = C.golden()[k + "__sum"]
+        assert abs(math.sqrt(sums[1]) / math.sqrt(ref[1]) - 1) <= 2e-4, k
+        assert C.rel_l2(sample, C.g(k + "__sample")) <= 2e-4, (k, C.rel_l2(sample, C.g(k + "__sample")))
+
+
+def test_full_model_192_hf_refinement_dice_vs_reference():
+    """config 5: full model with the HF refinement branch at 192^3 x 4 (bf16x3): Dice of the
+    argmax labels (TC / WT / ET) against the reference's own labels."""
+    case = C.cases()["full192hf"]
+    m, _ = C.build(case, DEV)
+    with torch.no_grad():
+        logits = m(cuda(C.case_input(case)))
+    lab = logits.argmax(1).cpu()
+    ref = C.g("full192hf_labels").long()
+    d = [C.dice(a, b) for a, b in zip(C.brats_regions(lab), C.brats_regions(ref))]
+    assert min(d) >= 1 - 1e-3, d
 
 
 @pytest.mark.parametrize("prec,bound", [("bf16x3", 1e-3), ("bf16", 5e-2)])

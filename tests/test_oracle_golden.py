@@ -64,7 +64,7 @@ def test_window_reverse_quirk_q1_is_not_identity():
 
 
 SMALL = ["attn_ws8", "attn_ws2_h1", "attn_ws4_h2", "block_l3", "block_l1", "block_l0",
-         "block_ss_l2", "merge", "ccf_ffn", "enc32", "full32"]
+         "block_ss_l2", "merge", "ccf_ffn", "enc32", "full32", "full32hf"]
 
 
 @pytest.mark.parametrize("name", SMALL)
@@ -100,6 +100,21 @@ def test_oracle_matches_reference_encoder128():
         # voxels (cancellation), so the same absolute fp32 noise is up to ~1e-4 relative there
         tol = 2e-4 if "_hf" in k else 2e-6
         assert C.rel_l2(sample, C.g(k + "__sample")) <= tol, k
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["enc192"])
+def test_oracle_matches_reference_encoder192_summaries(name):
+    case = C.cases()[name]
+    _, sd = C.build(case)
+    with torch.no_grad():
+        outs, _ = case.oracle(sd, C.case_input(case))
+    for i, t in enumerate(outs):
+        k = f"{name}_out{i}"
+        sums, sample = C.summary(t)
+        assert tuple(t.shape) == tuple(C.golden()[k + "__shape"])
+        np.testing.assert_allclose(sums[1], C.golden()[k + "__sum"][1], rtol=1e-5)
+        assert C.rel_l2(sample, C.g(k + "__sample")) <= 2e-6, k
 
 
 def test_oracle_matches_reference_full128_dice():

@@ -1,0 +1,55 @@
+"""HBM traffic per launch from two separate rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of
+the same command, written to a JSON summary that bench.py reads (roofline.traffic).
+
+    python tools/pmc_traffic.py gpurun_out/TAG_pmc_fetch gpurun_out/TAG_pmc_write OUT.json
+
+Per MI355X_MICROARCH.md (HBM [CDNA4]): FETCH_SIZE and WRITE_SIZE are kilobytes at the L2's
+memory side (Infinity-Cache hits included); on gfx950 FETCH_SIZE reports half the bytes of a
+16 B/lane streaming read, so it is doubled here; WRITE_SIZE is exact for 16 B/lane stores.
+For each kernel the largest launch (max fetch) is reported."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def load(root, counter):
+    out = collections.defaultdict(list)
+    for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0]
+            out[(name, r.get("Dispatch_Id", ""))].append(float(r["Counter_Value"]))
+    per = collections.defaultdict(list)
+    for (name, _), v in out.items():
+        per[name].append(sum(v))  # sum over XCD/instance rows of one dispatch
+    return per
+
+
+def main():
+    fetch_root, write_root, dst = sys.argv[1], sys.argv[2], sys.argv[3]
+    fetch, write = load(fetch_root, "FETCH_SIZE"), load(write_root, "WRITE_SIZE")
+    kernels = {}
+    for name, fv in fetch.items():
+        if "rocclr" in name or "at::native" in name:
+            continue
+        wv = write.get(name, [0.0])
+        f_kb, w_kb = max(fv), max(wv)
+        kernels[name] = {
+            "launches": len(fv),
+            "fetch_size_kb_largest": f_kb,
+            "write_size_kb_largest": w_kb,
+            "hbm_bytes_per_launch_largest": int(2 * f_kb * 1024 + w_kb * 1024),
+        }
+    json.dump({"source": [fetch_root, write_root],
+               "correction": "bytes = 2 * FETCH_SIZE[KB] * 1024 + WRITE_SIZE[KB] * 1024 (gfx950 "
+                             "FETCH_SIZE halving, MI355X_MICROARCH.md)",
+               "kernels": kernels}, open(dst, "w"), indent=1)
+    for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch_largest"])[:12]:
+        print(f"{v['hbm_bytes_per_launch_largest'] / 1e6:10.1f} MB  {k}")
+
+
+if __name__ == "__main__":
+    main()

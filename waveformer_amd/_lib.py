@@ -38,12 +38,14 @@ SIGNATURES = {
     "wf_ccf_ffn_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I64, _I]),
     "wf_ccf_ffn_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _F, _P, _P,
                             _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
+    "wf_ccf_ffn_stage": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _F, _P,
+                              _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
     "wf_patch_merging_fwd": (_I, [_P, _P, _P, _F, _P, _I, _P, _I64, _I64, _I64, _I64, _I64,
                                   _I, _P]),
     "wf_proj_out_fwd": (_I, [_P, _P, _I, _F, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lock = threading.Lock()
 _lib = None
 _err = None

@@ -24,6 +24,14 @@ struct Store4<uint16_t> {  // bf16 storage
   }
   static __device__ __forceinline__ uint16_t down(float v) { return f2bf(v); }
   static __device__ __forceinline__ vec zero() { return vec{0, 0, 0, 0}; }
+  static __device__ __forceinline__ void store4(uint16_t* p, f32x4 v) {
+    bf16x4 o;
+    o[0] = (short)f2bf(v.x);
+    o[1] = (short)f2bf(v.y);
+    o[2] = (short)f2bf(v.z);
+    o[3] = (short)f2bf(v.w);
+    *reinterpret_cast<bf16x4*>(p) = o;
+  }
 };
 template <>
 struct Store4<float> {  // fp32 storage
@@ -31,6 +39,9 @@ struct Store4<float> {  // fp32 storage
   static __device__ __forceinline__ f32x4 up(vec u) { return u; }
   static __device__ __forceinline__ float down(float v) { return v; }
   static __device__ __forceinline__ vec zero() { return vec{0, 0, 0, 0}; }
+  static __device__ __forceinline__ void store4(float* p, f32x4 v) {
+    *reinterpret_cast<f32x4*>(p) = v;
+  }
 };
 
 // Depthwise 3x3x3 conv + bias, then LayerNorm over the Hd channels of each position and
@@ -44,11 +55,16 @@ __global__ __launch_bounds__(512) void dwconv_ln_gelu_kernel(
     T* __restrict__ out, int B, int Hd, int D, int H, int W, int R) {
   typedef Store4<T> S;
   typedef typename S::vec vec;
-  extern __shared__ __attribute__((aligned(16))) float rb[];  // [R*TW][Hd+4]
+  extern __shared__ __attribute__((aligned(16))) float rb[];  // [R*TW][Hd+4], then stats
   const int HP = Hd + 4;
   const int nchunk = Hd >> 2;
   const int ntx = (W + TW - 1) / TW, nty = (H + R - 1) / R;
-  int t = blockIdx.x;
+  // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin dispatch), so give each
+  // XCD a contiguous run of (z, y, x) tiles -- neighbouring tiles re-read the same input rows
+  // and now find them in that XCD's L2 (bijective for any grid size; T1 of the HIP guide).
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
   const int xt = t % ntx;
   t /= ntx;
   const int yt = t % nty;
@@ -115,25 +131,230 @@ __global__ __launch_bounds__(512) void dwconv_ln_gelu_kernel(
     }
   }
   __syncthreads();
-  // LayerNorm + GELU per position: one wave per position, lanes over channels
-  const int lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
-  for (int p = wv; p < R * TW; p += nw) {
+  // LayerNorm statistics: one lane per position walks its row in LDS (no cross-lane traffic)
+  const int P = R * TW;
+  float* st = rb + (size_t)P * HP;  // [P][2]
+  for (int p = tid; p < P; p += blockDim.x) {
+    const f32x4* row = reinterpret_cast<const f32x4*>(rb + (size_t)p * HP);
+    f32x4 s4 = {0, 0, 0, 0};
+    for (int c = 0; c < nchunk; ++c) s4 += row[c];
+    const float mean = ((s4.x + s4.y) + (s4.z + s4.w)) / (float)Hd;
+    f32x4 q4 = {0, 0, 0, 0};
+    for (int c = 0; c < nchunk; ++c) {
+      const f32x4 d = row[c] - mean;
+      q4 += d * d;
+    }
+    st[2 * p] = mean;
+    st[2 * p + 1] = rsqrtf(((q4.x + q4.y) + (q4.z + q4.w)) / (float)Hd + eps);
+  }
+  __syncthreads();
+  // normalise + GELU + store: consecutive threads own consecutive 4-channel chunks of a row,
+  // so every store instruction writes whole contiguous rows
+  for (int it = tid; it < P * nchunk; it += blockDim.x) {
+    const int p = it / nchunk, c = it - p * nchunk;
     const int yy = yt * R + p / TW, xx = xb + p % TW;
     if (yy >= H || xx >= W) continue;
-    const float* row = rb + (size_t)p * HP;
-    float s = 0.f;
-    for (int e = lane; e < Hd; e += 64) s += row[e];
-    const float mean = group_sum<64>(s) / (float)Hd;
-    float q = 0.f;
-    for (int e = lane; e < Hd; e += 64) {
-      const float d = row[e] - mean;
-      q += d * d;
-    }
-    const float rstd = rsqrtf(group_sum<64>(q) / (float)Hd + eps);
-    T* dst = out + ((((int64_t)b * D + z) * H + yy) * W + xx) * Hd;
-    for (int e = lane; e < Hd; e += 64)
-      dst[e] = S::down(gelu_erf((row[e] - mean) * rstd * ln_w[e] + ln_b[e]));
+    const f32x4 lw = reinterpret_cast<const f32x4*>(ln_w)[c];
+    const f32x4 lb = reinterpret_cast<const f32x4*>(ln_b)[c];
+    f32x4 v = (reinterpret_cast<const f32x4*>(rb + (size_t)p * HP)[c] - st[2 * p]) * st[2 * p + 1] *
+                  lw + lb;
+    T* dst = out + ((((int64_t)b * D + z) * H + yy) * W + xx) * Hd + 4 * c;
+    v.x = gelu_erf(v.x);
+    v.y = gelu_erf(v.y);
+    v.z = gelu_erf(v.z);
+    v.w = gelu_erf(v.w);
+    S::store4(dst, v);
   }
+}
+
+// Depthwise 3x3x3 conv + bias, no normalisation (CCF_FFN's LN2 + GELU run in the fc GEMM's
+// A loader).  Workgroup = (b, z segment of ZS output planes, TY x TX tile of (y, x), CH = 32
+// channels); 256 threads = TX columns x CH channels, each thread owning the TY outputs of its
+// (x, channel) column.  The workgroup marches z through the input planes z0-1 .. z0+ZS: each
+// plane's (TY+2) x (TX+2) x CH halo tile is staged once into LDS (double buffered; the next
+// plane's loads are issued before the current plane's arithmetic), and every input value is
+// read from LDS once per thread row and scattered into the three output planes it feeds
+// (rolling accumulators accA/accB/accC = planes p-1, p, p+1): 3.75 LDS reads and 27 FMAs per
+// output.  Global traffic is one read of the input (+ the halo, shared through L2 by the
+// neighbouring tiles that the XCD-contiguous order runs on the same XCD) and one write.
+template <typename T>
+struct Vec16;  // one 16-byte global vector of T, widened to fp32
+template <>
+struct Vec16<float> {
+  typedef f32x4 raw;
+  static constexpr int N = 4;
+  static __device__ __forceinline__ raw zero() { return raw{0, 0, 0, 0}; }
+  static __device__ __forceinline__ void put(float* d, raw u) {
+    *reinterpret_cast<f32x4*>(d) = u;
+  }
+};
+template <>
+struct Vec16<uint16_t> {
+  typedef bf16x8 raw;
+  static constexpr int N = 8;
+  static __device__ __forceinline__ raw zero() { return raw{0, 0, 0, 0, 0, 0, 0, 0}; }
+  static __device__ __forceinline__ void put(float* d, raw u) {
+    reinterpret_cast<f32x4*>(d)[0] = f32x4{bf2f((uint16_t)u[0]), bf2f((uint16_t)u[1]),
+                                           bf2f((uint16_t)u[2]), bf2f((uint16_t)u[3])};
+    reinterpret_cast<f32x4*>(d)[1] = f32x4{bf2f((uint16_t)u[4]), bf2f((uint16_t)u[5]),
+                                           bf2f((uint16_t)u[6]), bf2f((uint16_t)u[7])};
+  }
+};
+
+constexpr int DW_CH = 32, DW_TX = 8, DW_TY = 8;
+
+template <typename T>
+__global__ __launch_bounds__(256) void dwconv3d_kernel(
+    const T* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias,
+    T* __restrict__ out, float* __restrict__ pstats, int B, int Hd, int D, int H, int W, int ZS) {
+  constexpr int CH = DW_CH, TX = DW_TX, TY = DW_TY;
+  static_assert(CH == DW_STAT_GROUP, "one statistics group per workgroup channel chunk");
+  constexpr int PY = TY + 2, PX = TX + 2;
+  typedef Vec16<T> V;
+  constexpr int NV = CH / V::N;                  // 16-byte vectors per tile position
+  constexpr int NLD = (PY * PX * NV + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float pl[2][PY * PX * CH];
+
+  const int ncc = Hd / CH, ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY;
+  const int nzs = (D + ZS - 1) / ZS;
+  // XCD-contiguous tile order, channel chunk fastest, then x: the ncc workgroups that split
+  // one spatial tile's Hd-wide rows run together (whole rows leave DRAM together), and
+  // neighbouring tiles, which share halo rows, run on the same XCD and meet in its L2
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int cc = t % ncc;
+  t /= ncc;
+  const int xt = t % ntx;
+  t /= ntx;
+  const int yt = t % nty;
+  t /= nty;
+  const int zt = t % nzs;
+  const int b = t / nzs;
+  const int x0 = xt * TX, y0 = yt * TY, z0 = zt * ZS, z1 = min(z0 + ZS, D);
+  const int c0 = cc * CH;
+  const int tid = threadIdx.x;
+  const int ch = tid % CH, xi = tid / CH;
+
+  float wt[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) wt[k] = w[(c0 + ch) * 27 + k];
+  const float bv = bias[c0 + ch];
+
+  // staging of one input plane: item i -> (tile position i / NV, vector i % NV)
+  typename V::raw stg[NLD];
+  const T* src = in + (int64_t)b * D * H * W * Hd + c0;
+  auto fetch = [&](int p) {
+    const bool pz = p >= 0 && p < D;
+    const int pc = min(max(p, 0), D - 1);
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) {
+      const int i = min(j * 256 + tid, PY * PX * NV - 1);
+      const int pos = i / NV, v = i - pos * NV;
+      const int yy = y0 - 1 + pos / PX, xx = x0 - 1 + pos % PX;
+      const bool ok = pz && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const int yc = min(max(yy, 0), H - 1), xc = min(max(xx, 0), W - 1);
+      const typename V::raw u = *reinterpret_cast<const typename V::raw*>(
+          src + (((int64_t)pc * H + yc) * W + xc) * Hd + V::N * v);
+      stg[j] = ok ? u : V::zero();
+    }
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) {
+      const int i = j * 256 + tid;
+      if (i < PY * PX * NV) V::put(pl[buf] + (size_t)i * V::N, stg[j]);
+    }
+  };
+
+  float accA[TY], accB[TY], accC[TY];
+#pragma unroll
+  for (int o = 0; o < TY; ++o) accA[o] = accB[o] = accC[o] = 0.f;
+  const int xo = x0 + xi;
+  fetch(z0 - 1);
+  commit(0);
+  __syncthreads();
+  int buf = 0;
+  for (int p = z0 - 1; p <= z1; ++p) {
+    fetch(p + 1);  // next plane in flight during this plane's arithmetic (past z1: unused)
+    const float* P = pl[buf] + xi * CH + ch;
+    // plane p feeds output p+1 (kz = 0), p (kz = 1) and p-1 (kz = 2)
+#pragma unroll
+    for (int r = 0; r < PY; ++r) {
+      const float v0 = P[(r * PX + 0) * CH], v1 = P[(r * PX + 1) * CH], v2 = P[(r * PX + 2) * CH];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int o = r - ky;  // output row fed by input row r through tap ky
+        if (o < 0 || o >= TY) continue;
+        const float* w0 = wt + ky * 3;
+        accC[o] += w0[0] * v0 + w0[1] * v1 + w0[2] * v2;
+        accB[o] += w0[9] * v0 + w0[10] * v1 + w0[11] * v2;
+        accA[o] += w0[18] * v0 + w0[19] * v1 + w0[20] * v2;
+      }
+    }
+    // output plane p-1 is complete
+    const int zo = p - 1;
+    if (zo >= z0) {
+      float r1[TY], mu[TY], m2[TY];
+#pragma unroll
+      for (int o = 0; o < TY; ++o) {
+        r1[o] = accA[o] + bv;
+        if (sizeof(T) == 2) r1[o] = bf2f(f2bf(r1[o]));  // statistics of the stored values
+      }
+      if (pstats) {  // {mean, M2} of this 32-channel group (32 consecutive lanes) per position
+#pragma unroll
+        for (int o = 0; o < TY; ++o) mu[o] = group_sum<32>(r1[o]) * (1.f / 32.f);
+#pragma unroll
+        for (int o = 0; o < TY; ++o) {
+          const float d = r1[o] - mu[o];
+          m2[o] = group_sum<32>(d * d);
+        }
+      }
+      if (xo < W) {
+#pragma unroll
+        for (int o = 0; o < TY; ++o) {
+          const int yo = y0 + o;
+          if (yo < H) {
+            const int64_t pos = (((int64_t)b * D + zo) * H + yo) * W + xo;
+            T* dst = out + pos * Hd + c0 + ch;
+            if (sizeof(T) == 4) *reinterpret_cast<float*>(dst) = r1[o];
+            else *reinterpret_cast<uint16_t*>(dst) = f2bf(r1[o]);
+            if (pstats && ch == 0)
+              *reinterpret_cast<float2*>(pstats + (pos * ncc + cc) * 2) = float2{mu[o], m2[o]};
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < TY; ++o) {
+      accA[o] = accB[o];
+      accB[o] = accC[o];
+      accC[o] = 0.f;
+    }
+    commit(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+}
+
+int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, float* pstats,
+                    int B, int Hd, int D, int H, int W, int prec, hipStream_t s) {
+  if (Hd % DW_CH != 0) return fail(WF_E_SHAPE, "dwconv3d: hidden width must be a multiple of 32");
+  // z segment: enough workgroups to fill 256 CUs ~8 deep, but long enough that the two halo
+  // planes per segment stay a small overhead
+  const int64_t base = (int64_t)B * (Hd / DW_CH) * cdiv(H, DW_TY) * cdiv(W, DW_TX);
+  int ZS = D;
+  while (ZS > 8 && base * cdiv(D, ZS) < 2048) ZS = (ZS + 1) / 2;
+  const int64_t blocks = base * cdiv(D, ZS);
+  if (prec == PREC_SPLIT)
+    hipLaunchKernelGGL((dwconv3d_kernel<float>), dim3((unsigned)blocks), dim3(256), 0, s,
+                       reinterpret_cast<const float*>(in), w, b, reinterpret_cast<float*>(out),
+                       pstats, B, Hd, D, H, W, ZS);
+  else
+    hipLaunchKernelGGL((dwconv3d_kernel<uint16_t>), dim3((unsigned)blocks), dim3(256), 0, s,
+                       reinterpret_cast<const uint16_t*>(in), w, b,
+                       reinterpret_cast<uint16_t*>(out), pstats, B, Hd, D, H, W, ZS);
+  return check_launch("dwconv3d");
 }
 
 template <typename T>
@@ -169,7 +390,7 @@ int launch_dwconv_ln_gelu(const void* in, const float* w, const float* b, const 
   if (tw_eff <= 2) tw_t = 2;
   else if (tw_eff <= 4) tw_t = 4;
   else if (tw_eff <= 8) tw_t = 8;
-  const size_t lds = (size_t)R * tw_t * (Hd + 4) * 4;
+  const size_t lds = ((size_t)R * tw_t * (Hd + 4) + 2 * (size_t)R * tw_t) * 4;
   const int64_t blocks = (int64_t)B * D * cdiv(H, R) * cdiv(W, tw_t);
   if (prec == PREC_SPLIT)
     launch_dw<float>(tw_t, dim3((unsigned)blocks), dim3(threads), lds, s, in, w, b, ln_w, ln_b,
@@ -189,17 +410,21 @@ extern "C" int64_t wf_ccf_ffn_workspace_bytes(int64_t B, int64_t C, int64_t hidd
   (void)C;
   const int64_t e = precision == PREC_SPLIT ? 4 : 2;
   const int64_t one = ((B * D * H * W * hidden * e) + 255) & ~(int64_t)255;
-  return 2 * one;
+  // + the dwconv's per-32-channel-group {mean, M2} of every position (LN2 in the fc loader)
+  const int64_t st = B * D * H * W * (hidden / DW_STAT_GROUP) * 2 * 4;
+  return 2 * one + ((st + 255) & ~(int64_t)255);
 }
 
-extern "C" int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* n2_w,
-                              const float* n2_b, const uint16_t* pw_bf16x2, const float* pw_b,
-                              const float* ln1_w, const float* ln1_b, float eps1,
-                              const float* dw_w, const float* dw_b, const float* ln2_w,
-                              const float* ln2_b, float eps2, const uint16_t* fc_bf16x2,
-                              const float* fc_b, const float* branch_scale, float* out,
-                              void* workspace, int64_t B, int64_t C, int64_t hidden, int64_t D,
-                              int64_t H, int64_t W, int precision, void* stream) {
+extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
+                                const float* n2_w, const float* n2_b,
+                                const uint16_t* pw_bf16x2, const float* pw_b,
+                                const float* ln1_w, const float* ln1_b, float eps1,
+                                const float* dw_w, const float* dw_b, const float* ln2_w,
+                                const float* ln2_b, float eps2, const uint16_t* fc_bf16x2,
+                                const float* fc_b, const float* branch_scale, float* out,
+                                void* workspace, int64_t B, int64_t C, int64_t hidden,
+                                int64_t D, int64_t H, int64_t W, int precision, void* stream) {
+  WF_REQUIRE(stage >= 0 && stage <= 3, "stage must be 0 (all), 1 (pwconv), 2 (dwconv) or 3 (fc)");
   WF_REQUIRE(B >= 1 && D >= 1 && H >= 1 && W >= 1, "empty volume");
   WF_REQUIRE(C % 8 == 0 && hidden % 8 == 0, "C and hidden must be multiples of 8");
   WF_REQUIRE(precision == PREC_BF16 || precision == PREC_SPLIT, "unknown precision");
@@ -249,11 +474,23 @@ extern "C" int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* 
   g.out = h1;
   g.out_bf16 = hbf;
   g.ldo = hidden;
-  int rc = launch_gemm(g, s, "wf_ccf_ffn_fwd(pwconv)");
+  int rc = 0;
+  if (stage == 0 || stage == 1) rc = launch_gemm(g, s, "wf_ccf_ffn_fwd(pwconv)");
   if (rc) return rc;
-  rc = launch_dwconv_ln_gelu(h1, dw_w, dw_b, ln2_w, ln2_b, eps2, h2, (int)B, (int)hidden,
-                             (int)D, (int)H, (int)W, precision, s);
-  if (rc) return rc;
+  // dwconv + LN2 + GELU: either fused in one kernel (LN over the full 4C row per position in
+  // LDS), or the z-marching depthwise conv with LN2 + GELU moved into the fc loader
+  static const bool fused_dw = getenv("WF_FFN_FUSED_DW") != nullptr;
+  const bool split_ln = !fused_dw && hidden % 32 == 0;
+  float* pst = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 2 * one);
+  if (stage == 0 || stage == 2) {
+    if (split_ln)
+      rc = launch_dwconv3d(h1, dw_w, dw_b, h2, pst, (int)B, (int)hidden, (int)D, (int)H,
+                           (int)W, precision, s);
+    else
+      rc = launch_dwconv_ln_gelu(h1, dw_w, dw_b, ln2_w, ln2_b, eps2, h2, (int)B, (int)hidden,
+                                 (int)D, (int)H, (int)W, precision, s);
+  }
+  if (rc || stage == 1 || stage == 2) return rc;
   GemmArgs f{};
   f.prec = precision;
   f.a_src = h2;
@@ -261,7 +498,17 @@ extern "C" int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* 
   f.a_C = (int)hidden;
   f.a_nseg = 1;
   f.a_map = MAP_IDENTITY;
-  f.a_ln = LN_NONE;
+  if (split_ln) {
+    f.a_ln = LN_PARTIAL;
+    f.a_stats = pst;
+    f.a_np = (int)(hidden / DW_STAT_GROUP);
+    f.a_ln_w = ln2_w;
+    f.a_ln_b = ln2_b;
+    f.a_eps = eps2;
+    f.a_gelu = 1;
+  } else {
+    f.a_ln = LN_NONE;
+  }
   f.w = fc_bf16x2;
   f.M = M;
   f.N = (int)C;
@@ -278,6 +525,19 @@ extern "C" int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* 
   f.out_bf16 = 0;
   f.ldo = C;
   return launch_gemm(f, s, "wf_ccf_ffn_fwd(fc)");
+}
+
+extern "C" int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* n2_w,
+                              const float* n2_b, const uint16_t* pw_bf16x2, const float* pw_b,
+                              const float* ln1_w, const float* ln1_b, float eps1,
+                              const float* dw_w, const float* dw_b, const float* ln2_w,
+                              const float* ln2_b, float eps2, const uint16_t* fc_bf16x2,
+                              const float* fc_b, const float* branch_scale, float* out,
+                              void* workspace, int64_t B, int64_t C, int64_t hidden, int64_t D,
+                              int64_t H, int64_t W, int precision, void* stream) {
+  return wf_ccf_ffn_stage(0, xh, stats, n2_w, n2_b, pw_bf16x2, pw_b, ln1_w, ln1_b, eps1, dw_w,
+                          dw_b, ln2_w, ln2_b, eps2, fc_bf16x2, fc_b, branch_scale, out,
+                          workspace, B, C, hidden, D, H, W, precision, stream);
 }
 
 extern "C" int wf_patch_merging_fwd(const float* x, const float* ln_w, const float* ln_b,

@@ -140,6 +140,19 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
         }
       }
       rstd = rsqrtf(tpr_sum<TPR>(sq) / (float)K + g.a_eps);
+    } else if (g.a_ln == LN_PARTIAL) {  // combine the producer's per-group {mean, M2}
+      const int np = g.a_np;
+      const float* ps = g.a_stats + (mv ? m : 0) * np * 2;
+      float s = 0.f;
+      for (int c = q; c < np; c += TPR) s += ps[2 * c];
+      mean = tpr_sum<TPR>(s) / (float)np;
+      const float ng = (float)(K / np);
+      float sq = 0.f;
+      for (int c = q; c < np; c += TPR) {
+        const float d = ps[2 * c] - mean;
+        sq += ps[2 * c + 1] + ng * d * d;
+      }
+      rstd = rsqrtf(tpr_sum<TPR>(sq) / (float)K + g.a_eps);
     }
     if (q == 0) {
       st[2 * r] = mean;
@@ -166,6 +179,10 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
           const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * wv[j] + bv[j];
+          if (g.a_gelu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+          }
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -302,8 +319,15 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
   if (g.N <= 0 || g.N % 4 != 0) return fail(WF_E_SHAPE, std::string(who) + ": N must be a positive multiple of 4");
   if (g.a_C % 8 != 0) return fail(WF_E_SHAPE, std::string(who) + ": channels must be a multiple of 8");
   if (g.M <= 0) return WF_OK;
-  static const bool ares_only = getenv("WF_GEMM_ARES_ONLY") != nullptr;  // A/B switch
-  if (!ares_only && try_launch_gemm_rows(g, s)) return check_launch(who);
+  // streaming kernels first: gemm_rows when one LDS-resident weight chunk covers all N,
+  // else the K-chunked gemm_kc (WF_GEMM_NO_KC: gemm_rows over several column chunks); the A-resident
+  // gemm_ares takes the remaining shapes.  (WF_GEMM_ARES_ONLY / WF_GEMM_NO_KC: A/B switches)
+  static const bool ares_only = getenv("WF_GEMM_ARES_ONLY") != nullptr;
+  static const bool no_kc = getenv("WF_GEMM_NO_KC") != nullptr;
+  if (!ares_only) {
+    if (try_launch_gemm_rows(g, s, !no_kc)) return check_launch(who);
+    if (!no_kc && try_launch_gemm_kc(g, s)) return check_launch(who);
+  }
   const bool split = g.prec == PREC_SPLIT;
   int BM = 64;
   while (BM > 16 && gemm_lds_bytes(BM, g.K, g.N, split) > 80 * 1024) BM >>= 1;

@@ -1,0 +1,65 @@
+// gemm_common.hpp -- A-operand helpers shared by the streaming GEMMs (gemm_rows, gemm_kc).
+#pragma once
+#include "kernels.hpp"
+
+namespace wf {
+
+template <bool BF16>
+__device__ __forceinline__ void load8f(const void* src, int64_t off, float (&v)[8]) {
+  if (BF16) {
+    const bf16x8 u = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(src) + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f((uint16_t)u[j]);
+  } else {
+    const f32x4* p = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(src) + off);
+    const f32x4 a = p[0], b = p[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+
+// Source element offset of logical (row m, column k).
+template <int MAP>
+struct RowMapper {
+  int pos;  // source raster row (MAP_MERGE: the (2z, 2y, 2x) corner)
+  __device__ __forceinline__ RowMapper(const GemmArgs& g, int m) {
+    if (MAP == MAP_WINDOW) {
+      const int ws = g.mws;
+      const int N = ws * ws * ws;
+      const int nWh = g.mH / ws, nWw = g.mW / ws, nW = (g.mD / ws) * nWh * nWw;
+      const int bw = m / N;
+      const int t = m - bw * N;
+      const int b = bw / nW;
+      int wi = bw - b * nW;
+      const int wx = wi % nWw;
+      wi /= nWw;
+      const int wy = wi % nWh, wz = wi / nWh;
+      const int tx = t % ws, ty = (t / ws) % ws, tz = t / (ws * ws);
+      pos = ((b * g.mD + wz * ws + tz) * g.mH + wy * ws + ty) * g.mW + wx * ws + tx;
+    } else if (MAP == MAP_MERGE) {
+      const int d = g.mD >> 1, h = g.mH >> 1, w = g.mW >> 1;
+      int r = m;
+      const int x = r % w;
+      r /= w;
+      const int y = r % h;
+      r /= h;
+      const int z = r % d;
+      const int b = r / d;
+      pos = ((b * g.mD + 2 * z) * g.mH + 2 * y) * g.mW + 2 * x;
+    } else {
+      pos = m;
+    }
+  }
+  __device__ __forceinline__ int64_t offset(const GemmArgs& g, int k) const {
+    if (MAP == MAP_MERGE) {
+      const int seg = k / g.a_C;
+      const int c = k - seg * g.a_C;
+      const int o = (g.merge_code >> (4 * seg)) & 0xF;  // bit2: d, bit1: h, bit0: w
+      const int p = pos + (((o >> 2) & 1) * g.mH + ((o >> 1) & 1)) * g.mW + (o & 1);
+      return (int64_t)p * g.a_C + c;
+    }
+    return (int64_t)pos * g.K + k;
+  }
+};
+
+}  // namespace wf

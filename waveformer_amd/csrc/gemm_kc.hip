@@ -1,0 +1,373 @@
+// gemm_kc.hip -- K-chunked MFMA GEMM for the Linear layers whose weight is too large to sit in
+// LDS whole (PatchMerging 8C -> 2C, the CCF_FFN fc of stages 2-4, stage 3/4 qkv/pw).
+//
+// out[m, n] = epilogue( sum_k A[m, k] * Wt[n, k] )
+//   * workgroup = 4 waves x RT row tiles of 16 rows (64 * RT rows) x one column chunk of
+//     NC = NT * 16 output channels (grid.y walks the chunks);
+//   * the weight chunk streams through LDS 32 k at a time, double buffered: the next k step's
+//     [NC][32] bf16 hi (+ lo) slice is loaded into registers while the MFMAs of the current
+//     one run, and written to the other buffer behind them (one barrier per k step);
+//   * A fragments come straight from global memory into registers (lane l: row l&15,
+//     k = 8*(l>>4) .. +7 of the step), one step ahead, through the row gather / LayerNorm /
+//     GELU / bf16 hi-lo split of gemm_common.hpp's RowMapper;
+//   * transposed MFMA (weight fragment = A operand), so each lane ends with 4 consecutive
+//     output channels of one row: 16-byte epilogue loads and stores.
+// LayerNorm of A: LN_GIVEN (stats passed in), LN_COMPUTE (one shifted sum / sum-of-squares
+// pass over the row before the k loop) or LN_PARTIAL (per-group {mean, M2} of the producer
+// combined by Chan's formula).
+#include "gemm_common.hpp"
+
+namespace wf {
+
+constexpr int KC_BK = 32;       // k per step (one 16x16x32 MFMA)
+constexpr int KC_KP = KC_BK + 8;  // LDS row stride in bf16 (16 B pad: conflict-free b128 reads)
+
+template <int NT>
+struct KcCfg {
+  static constexpr int RT = NT >= 24 ? 1 : 2;  // accumulators: RT * NT * 4 <= 96 VGPRs
+  static constexpr int NC = NT * 16;
+  static constexpr int WITEMS = NC * (KC_BK / 8);  // 16-byte pieces per plane per k step
+  static constexpr int WPT = (WITEMS + 255) / 256;  // per thread
+};
+
+template <int NT, bool SPLIT, int MAP, int EPI, bool ABF16>
+__global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
+  typedef KcCfg<NT> C;
+  constexpr int RT = C::RT, NC = C::NC, NPL = SPLIT ? 2 : 1;
+  extern __shared__ __attribute__((aligned(16))) uint16_t Wl[];  // [2][NPL][NC][KC_KP]
+  const int K = g.K, N = g.N;
+  const int M = (int)g.M;
+  const int nks = (K + KC_BK - 1) / KC_BK;
+  const int c0 = blockIdx.y * NC;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const int rbase = blockIdx.x * (64 * RT) + wid * (16 * RT);
+
+  // ---- weight staging: piece i -> (column i / 4, k-octet i % 4) of the step's slice
+  bf16x8 wst[NPL][C::WPT];
+  auto wfetch = [&](int ks) {
+#pragma unroll
+    for (int j = 0; j < C::WPT; ++j) {
+      const int i = min(j * 256 + tid, C::WITEMS - 1);
+      const int n = c0 + (i >> 2), k = ks * KC_BK + 8 * (i & 3);
+      const bool ok = n < N && k < K;
+      const int64_t off = (int64_t)min(n, N - 1) * K + min(k, K - 8);
+      const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      const bf16x8 h = *reinterpret_cast<const bf16x8*>(g.w + off);
+      wst[0][j] = ok ? h : z;
+      if (SPLIT) {
+        const bf16x8 l = *reinterpret_cast<const bf16x8*>(g.w + (int64_t)N * K + off);
+        wst[NPL - 1][j] = ok ? l : z;
+      }
+    }
+  };
+  auto wcommit = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < C::WPT; ++j) {
+      const int i = j * 256 + tid;
+      if (i < C::WITEMS) {
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+          *reinterpret_cast<bf16x8*>(Wl + ((size_t)(buf * NPL + pl) * NC + (i >> 2)) * KC_KP +
+                                     8 * (i & 3)) = wst[pl][j];
+      }
+    }
+  };
+
+  // ---- A rows of this lane (row l15 of each of its RT tiles) and their LayerNorm stats
+  int arow[RT];
+  float mean[RT], rstd[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    arow[rt] = min(rbase + rt * 16 + l15, M - 1);
+    mean[rt] = 0.f;
+    rstd[rt] = 1.f;
+  }
+  if (g.a_ln == LN_GIVEN) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      mean[rt] = g.a_stats[2 * arow[rt]];
+      rstd[rt] = g.a_stats[2 * arow[rt] + 1];
+    }
+  } else if (g.a_ln == LN_COMPUTE) {
+    // one pass: sums of x - s and (x - s)^2 with s = the row's first element (keeps the
+    // variance free of cancellation when |mean| >> std); the 4 lanes of a row split the k range
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const RowMapper<MAP> rm(g, arow[rt]);
+      float v0[8];
+      load8f<ABF16>(g.a_src, rm.offset(g, 0), v0);
+      const float sh = v0[0];
+      float s = 0.f, q = 0.f;
+      for (int ch = g4; ch < K / 8; ch += 4) {
+        float v[8];
+        load8f<ABF16>(g.a_src, rm.offset(g, ch * 8), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[j] - sh;
+          s += d;
+          q += d * d;
+        }
+      }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      const float ms = s / (float)K;
+      mean[rt] = sh + ms;
+      rstd[rt] = rsqrtf(fmaxf(q / (float)K - ms * ms, 0.f) + g.a_eps);
+    }
+  } else if (g.a_ln == LN_PARTIAL) {
+    const int np = g.a_np;
+    const float ng = (float)(K / np);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const float* ps = g.a_stats + (int64_t)arow[rt] * np * 2;
+      float s = 0.f;
+      for (int c = g4; c < np; c += 4) s += ps[2 * c];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const float mu = s / (float)np;
+      float q = 0.f;
+      for (int c = g4; c < np; c += 4) {
+        const float d = ps[2 * c] - mu;
+        q += ps[2 * c + 1] + ng * d * d;
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      mean[rt] = mu;
+      rstd[rt] = rsqrtf(q / (float)K + g.a_eps);
+    }
+  }
+
+  f32x4 acc[RT][NT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0, 0, 0, 0};
+
+  float an[RT][8];
+  auto afetch = [&](int ks) {
+    const int k = min(ks * KC_BK + 8 * g4, K - 8);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const RowMapper<MAP> rm(g, arow[rt]);
+      load8f<ABF16>(g.a_src, rm.offset(g, k), an[rt]);
+    }
+  };
+
+  // the loader's LayerNorm gamma/beta in LDS (a global load inside the k loop would queue on
+  // the in-order vmcnt behind the prefetches and drain them every step)
+  float* lnw = reinterpret_cast<float*>(Wl + (size_t)2 * NPL * NC * KC_KP);
+  float* lnb = lnw + nks * KC_BK;
+  if (g.a_ln != LN_NONE) {
+    for (int i = tid; i < nks * KC_BK; i += 256) {
+      lnw[i] = i < K ? g.a_ln_w[i] : 0.f;
+      lnb[i] = i < K ? g.a_ln_b[i] : 0.f;
+    }
+  }
+  wfetch(0);
+  wcommit(0);
+  afetch(0);
+  __syncthreads();
+  int buf = 0;
+#pragma unroll 1
+  for (int ks = 0; ks < nks; ++ks) {
+    const int k = ks * KC_BK + 8 * g4;
+    const bool kv = k < K;
+    float v[RT][8];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[rt][j] = an[rt][j];
+    wfetch(min(ks + 1, nks - 1));  // next step's weight slice (last step: unused re-read)
+    afetch(min(ks + 1, nks - 1));
+    bf16x8 ah[RT], al[RT];
+    {
+      float wv[8], bv[8];
+      if (g.a_ln != LN_NONE) {
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(lnw + k);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(lnw + k + 4);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(lnb + k);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(lnb + k + 4);
+        wv[0] = w0.x; wv[1] = w0.y; wv[2] = w0.z; wv[3] = w0.w;
+        wv[4] = w1.x; wv[5] = w1.y; wv[6] = w1.z; wv[7] = w1.w;
+        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+        bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        if (g.a_ln != LN_NONE) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[rt][j] = (v[rt][j] - mean[rt]) * rstd[rt] * wv[j] + bv[j];
+          if (g.a_gelu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[rt][j] = gelu_erf(v[rt][j]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = kv ? v[rt][j] : 0.f;
+          const uint16_t h = f2bf(x);
+          ah[rt][j] = (short)h;
+          al[rt][j] = SPLIT ? (short)f2bf(x - bf2f(h)) : (short)0;
+        }
+      }
+    }
+    const uint16_t* Wb = Wl + (size_t)buf * NPL * NC * KC_KP;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int wo = (t * 16 + l15) * KC_KP + 8 * g4;
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Wb + wo);
+      if (SPLIT) {
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Wb + NC * KC_KP + wo);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al[rt], acc[rt][t], 0, 0, 0);
+          acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah[rt], acc[rt][t], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah[rt], acc[rt][t], 0, 0, 0);
+      if (t % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    wcommit(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // ---- epilogue: acc[rt][t][i] = out[row rbase + 16 rt + l15][channel c0 + 16 t + 4 g4 + i]
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int row = rbase + rt * 16 + l15;
+    const bool rv = row < M;
+    const int rowc = min(row, M - 1);
+    if (g.bias) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[rt][t] += *reinterpret_cast<const f32x4*>(g.bias + min(c0 + t * 16 + 4 * g4, N - 4));
+    }
+    float rm_ = 0.f, rs_ = 1.f, bs = 1.f;
+    if (EPI == EPI_LN_GELU) {  // NC == N: the 4 lanes of a row hold the full row
+      float s = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) s += (acc[rt][t].x + acc[rt][t].y) + (acc[rt][t].z + acc[rt][t].w);
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      rm_ = s / (float)N;
+      float q = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const f32x4 d = acc[rt][t] - rm_;
+        q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      rs_ = rsqrtf(q / (float)N + g.e_eps);
+    } else if (EPI == EPI_RESID) {
+      if (g.r_stats) {
+        rm_ = g.r_stats[2 * rowc];
+        rs_ = g.r_stats[2 * rowc + 1];
+      }
+      if (g.r_scale) bs = g.r_scale[rowc / (int)g.rows_per_sample];
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = c0 + t * 16 + 4 * g4;
+      const int colc = min(col, N - 4);
+      f32x4 v = acc[rt][t];
+      if (EPI == EPI_LN_GELU) {
+        const f32x4 lw = *reinterpret_cast<const f32x4*>(g.e_ln_w + colc);
+        const f32x4 lb = *reinterpret_cast<const f32x4*>(g.e_ln_b + colc);
+        v = (v - rm_) * rs_ * lw + lb;
+        v.x = gelu_erf(v.x);
+        v.y = gelu_erf(v.y);
+        v.z = gelu_erf(v.z);
+        v.w = gelu_erf(v.w);
+      } else if (EPI == EPI_RESID) {
+        const f32x4 xr = *reinterpret_cast<const f32x4*>(g.r_x + (int64_t)rowc * N + colc);
+        if (g.r_stats) {
+          const f32x4 lw = *reinterpret_cast<const f32x4*>(g.r_ln_w + colc);
+          const f32x4 lb = *reinterpret_cast<const f32x4*>(g.r_ln_b + colc);
+          const f32x4 n2 = (xr - rm_) * rs_ * lw + lb;
+          v = xr + (n2 + v) * bs;  // attn_fused + drop_path(n2 + ffn(n2)), quirk Q4
+        } else {
+          v = xr + v * bs;
+        }
+      }
+      if (rv && col < N) {
+        if (g.out_bf16) {
+          bf16x4 o;
+          o[0] = (short)f2bf(v.x);
+          o[1] = (short)f2bf(v.y);
+          o[2] = (short)f2bf(v.z);
+          o[3] = (short)f2bf(v.w);
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(g.out) + (int64_t)row * g.ldo + col) = o;
+        } else {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(g.out) + (int64_t)row * g.ldo + col) = v;
+        }
+      }
+      if (t % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+template <int NT, int MAP, int EPI>
+static void go_kc(const GemmArgs& g, hipStream_t s) {
+  typedef KcCfg<NT> C;
+  const bool split = g.prec == PREC_SPLIT;
+  void (*kern)(GemmArgs);
+  if (g.a_bf16)
+    kern = split ? gemm_kc_kernel<NT, true, MAP, EPI, true> : gemm_kc_kernel<NT, false, MAP, EPI, true>;
+  else
+    kern = split ? gemm_kc_kernel<NT, true, MAP, EPI, false> : gemm_kc_kernel<NT, false, MAP, EPI, false>;
+  const size_t lds = (size_t)2 * (split ? 2 : 1) * C::NC * KC_KP * 2 +
+                     (g.a_ln != LN_NONE ? (size_t)2 * cdiv(g.K, KC_BK) * KC_BK * 4 : 0);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const dim3 grid((unsigned)cdiv(g.M, 64 * C::RT), (unsigned)(g.N / C::NC));
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g);
+}
+
+template <int MAP, int EPI>
+static void dispatch_kc(int nt, const GemmArgs& g, hipStream_t s) {
+  switch (nt) {
+    case 24: go_kc<24, MAP, EPI>(g, s); break;
+    case 12: go_kc<12, MAP, EPI>(g, s); break;
+    case 8: go_kc<8, MAP, EPI>(g, s); break;
+    case 6: go_kc<6, MAP, EPI>(g, s); break;
+    case 4: go_kc<4, MAP, EPI>(g, s); break;
+    case 3: go_kc<3, MAP, EPI>(g, s); break;
+    default: go_kc<2, MAP, EPI>(g, s); break;
+  }
+}
+
+int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s) {
+  if (g.N % 32 != 0 || g.K < 8 || g.M >= ((int64_t)1 << 31)) return 0;
+  const bool known = (g.a_map == MAP_WINDOW && g.epi == EPI_STORE) ||
+                     (g.a_map == MAP_IDENTITY) || (g.a_map == MAP_MERGE && g.epi == EPI_STORE);
+  if (!known) return 0;
+  const int tiles = g.N / 16;
+  static const int cand[] = {24, 12, 8, 6, 4, 3, 2};
+  // widest column chunk that divides N (fewest re-reads of A); then, for small M, narrower
+  // chunks until the grid has ~2 workgroups per CU (the K loop is a serial chain per workgroup)
+  auto blocks = [&](int c) { return cdiv(g.M, 64 * (c >= 24 ? 1 : 2)) * (tiles / c); };
+  int nt = 0;
+  for (int c : cand) {
+    if (tiles % c != 0) continue;
+    if (g.epi == EPI_LN_GELU && c != tiles) continue;  // LayerNorm needs the full row
+    if (nt == 0 || (g.epi != EPI_LN_GELU && blocks(nt) < 512 && c >= 3)) nt = c;
+    if (blocks(nt) >= 512) break;
+  }
+  if (nt == 0) return 0;
+  if (g.a_map == MAP_WINDOW) dispatch_kc<MAP_WINDOW, EPI_STORE>(nt, g, s);
+  else if (g.a_map == MAP_MERGE) dispatch_kc<MAP_MERGE, EPI_STORE>(nt, g, s);
+  else if (g.epi == EPI_LN_GELU) dispatch_kc<MAP_IDENTITY, EPI_LN_GELU>(nt, g, s);
+  else if (g.epi == EPI_RESID) dispatch_kc<MAP_IDENTITY, EPI_RESID>(nt, g, s);
+  else dispatch_kc<MAP_IDENTITY, EPI_STORE>(nt, g, s);
+  return 1;
+}
+
+}  // namespace wf

@@ -16,67 +16,9 @@
 // around a load makes hipcc wait vmcnt(0) for it and serialises the stream.  The row map
 // (identity / window gather / PatchMerging gather) and the epilogue are template parameters
 // so each call site compiles to straight-line code with 32-bit index math.
-#include "kernels.hpp"
+#include "gemm_common.hpp"
 
 namespace wf {
-
-template <bool BF16>
-__device__ __forceinline__ void load8f(const void* src, int64_t off, float (&v)[8]) {
-  if (BF16) {
-    const bf16x8 u = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(src) + off);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = bf2f((uint16_t)u[j]);
-  } else {
-    const f32x4* p = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(src) + off);
-    const f32x4 a = p[0], b = p[1];
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  }
-}
-
-// Source element offset of logical (row m, column k).
-template <int MAP>
-struct RowMapper {
-  int pos;  // source raster row (MAP_MERGE: the (2z, 2y, 2x) corner)
-  __device__ __forceinline__ RowMapper(const GemmArgs& g, int m) {
-    if (MAP == MAP_WINDOW) {
-      const int ws = g.mws;
-      const int N = ws * ws * ws;
-      const int nWh = g.mH / ws, nWw = g.mW / ws, nW = (g.mD / ws) * nWh * nWw;
-      const int bw = m / N;
-      const int t = m - bw * N;
-      const int b = bw / nW;
-      int wi = bw - b * nW;
-      const int wx = wi % nWw;
-      wi /= nWw;
-      const int wy = wi % nWh, wz = wi / nWh;
-      const int tx = t % ws, ty = (t / ws) % ws, tz = t / (ws * ws);
-      pos = ((b * g.mD + wz * ws + tz) * g.mH + wy * ws + ty) * g.mW + wx * ws + tx;
-    } else if (MAP == MAP_MERGE) {
-      const int d = g.mD >> 1, h = g.mH >> 1, w = g.mW >> 1;
-      int r = m;
-      const int x = r % w;
-      r /= w;
-      const int y = r % h;
-      r /= h;
-      const int z = r % d;
-      const int b = r / d;
-      pos = ((b * g.mD + 2 * z) * g.mH + 2 * y) * g.mW + 2 * x;
-    } else {
-      pos = m;
-    }
-  }
-  __device__ __forceinline__ int64_t offset(const GemmArgs& g, int k) const {
-    if (MAP == MAP_MERGE) {
-      const int seg = k / g.a_C;
-      const int c = k - seg * g.a_C;
-      const int o = (g.merge_code >> (4 * seg)) & 0xF;  // bit2: d, bit1: h, bit0: w
-      const int p = pos + (((o >> 2) & 1) * g.mH + ((o >> 1) & 1)) * g.mW + (o & 1);
-      return (int64_t)p * g.a_C + c;
-    }
-    return (int64_t)pos * g.K + k;
-  }
-};
 
 template <int NT, bool SPLIT, int MAP, int EPI, bool ABF16>
 __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
@@ -107,19 +49,49 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
       }
     }
   }
+  // the loader's LayerNorm gamma/beta [K32] and the epilogue's bias / LN gamma / LN beta
+  // [NCOL] live in LDS: read from global inside the loops they would sit on the in-order
+  // vmcnt behind the A prefetch and drain it at every k step
+  float* lnw = reinterpret_cast<float*>(Wl + (SPLIT ? 2 : 1) * NCOL * KP);
+  float* lnb = lnw + K32;
+  float* ebias = lnb + K32;
+  float* elw = ebias + NCOL;
+  float* elb = elw + NCOL;
+  for (int i = tid; i < K32; i += blockDim.x) {
+    const bool ok = g.a_ln != LN_NONE && i < K;
+    lnw[i] = ok ? g.a_ln_w[i] : 0.f;
+    lnb[i] = ok ? g.a_ln_b[i] : 0.f;
+  }
+  for (int i = tid; i < NCOL; i += blockDim.x) {
+    const int n = c0 + i;
+    ebias[i] = (g.bias && n < N) ? g.bias[n] : 0.f;
+    const bool e = EPI == EPI_LN_GELU && n < N;
+    elw[i] = e ? g.e_ln_w[n] : 0.f;
+    elb[i] = e ? g.e_ln_b[n] : 0.f;
+  }
   __syncthreads();
 
   const int ntiles = (M + 15) >> 4;
   const int nwaves = blockDim.x >> 6;
-  for (int tile = blockIdx.x * nwaves + wid; tile < ntiles; tile += gridDim.x * nwaves) {
-    // ---- A rows of this lane: row l15 of the tile
-    const int arow_c = min(tile * 16 + l15, M - 1);
-    const RowMapper<MAP> rm(g, arow_c);
-    float mean = 0.f, rstd = 1.f;
-    if (g.a_ln == LN_GIVEN) {
-      mean = g.a_stats[2 * arow_c];
-      rstd = g.a_stats[2 * arow_c + 1];
-    } else if (g.a_ln == LN_COMPUTE) {  // lanes l15, l15+16, l15+32, l15+48 share the row
+  const int stride = gridDim.x * nwaves;
+  // the first A fragment (and LN_GIVEN stats) of a wave's NEXT tile are loaded during the
+  // current tile's last k step, so they are in flight through its epilogue
+  int tile = blockIdx.x * nwaves + wid;
+  int arow_c = min(tile * 16 + l15, M - 1);
+  RowMapper<MAP> rm(g, arow_c);
+  float vn[8];
+  load8f<ABF16>(g.a_src, rm.offset(g, min(8 * g4, K - 8)), vn);
+  float gmean = 0.f, grstd = 1.f;
+  if (g.a_ln == LN_GIVEN) {
+    gmean = g.a_stats[2 * arow_c];
+    grstd = g.a_stats[2 * arow_c + 1];
+  }
+  for (; tile < ntiles; tile += stride) {
+    // ---- A rows of this lane: row l15 of the tile (and of the next one)
+    const int arow_n = min((tile + stride) * 16 + l15, M - 1);
+    const RowMapper<MAP> rmn(g, arow_n);
+    float mean = gmean, rstd = grstd;
+    if (g.a_ln == LN_COMPUTE) {  // lanes l15, l15+16, l15+32, l15+48 share the row
       float s = 0.f;
       for (int ch = g4; ch < K / 8; ch += 4) {
         float v[8];
@@ -143,15 +115,30 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
       q += __shfl_xor(q, 16, 64);
       q += __shfl_xor(q, 32, 64);
       rstd = rsqrtf(q / (float)K + g.a_eps);
+    } else if (g.a_ln == LN_PARTIAL) {  // combine the producer's per-group {mean, M2}
+      const int np = g.a_np;
+      const float* ps = g.a_stats + (int64_t)arow_c * np * 2;
+      float s = 0.f;
+      for (int c = g4; c < np; c += 4) s += ps[2 * c];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      mean = s / (float)np;
+      const float ng = (float)(K / np);
+      float q = 0.f;
+      for (int c = g4; c < np; c += 4) {
+        const float d = ps[2 * c] - mean;
+        q += ps[2 * c + 1] + ng * d * d;
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      rstd = rsqrtf(q / (float)K + g.a_eps);
     }
 
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0, 0, 0, 0};
 
-    // k loop with a one-step register prefetch of the A fragment
-    float vn[8];
-    load8f<ABF16>(g.a_src, rm.offset(g, min(8 * g4, K - 8)), vn);
+    // k loop with a one-step register prefetch of the A fragment (last step: the next tile's)
 #pragma unroll 1
     for (int k0 = 0; k0 < K32; k0 += 32) {
       const int k = k0 + 8 * g4;
@@ -159,17 +146,22 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = vn[j];
-      load8f<ABF16>(g.a_src, rm.offset(g, min(k + 32, K - 8)), vn);  // (last: unused)
+      const int64_t noff = k0 + 32 < K32 ? rm.offset(g, min(k + 32, K - 8))
+                                         : rmn.offset(g, min(8 * g4, K - 8));
+      load8f<ABF16>(g.a_src, noff, vn);
       if (g.a_ln != LN_NONE) {
-        const int kk = min(k, K - 8);
-        const f32x4 w0 = *reinterpret_cast<const f32x4*>(g.a_ln_w + kk);
-        const f32x4 w1 = *reinterpret_cast<const f32x4*>(g.a_ln_w + kk + 4);
-        const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.a_ln_b + kk);
-        const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.a_ln_b + kk + 4);
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(lnw + k);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(lnw + k + 4);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(lnb + k);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(lnb + k + 4);
         const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
         const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * wv[j] + bv[j];
+        if (g.a_gelu) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+        }
       }
       bf16x8 ah, al;
 #pragma unroll
@@ -179,73 +171,100 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
         ah[j] = (short)h;
         al[j] = SPLIT ? (short)f2bf(x - bf2f(h)) : (short)0;
       }
+      // transposed product C^T = Wt . A^T: the weight fragment is the A operand (rows =
+      // output channels), the activation fragment the B operand (columns = positions), so
+      // the accumulator gives each lane 4 CONSECUTIVE channels of one position.
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int wo = (t * 16 + l15) * KP + k0 + 8 * g4;
         const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Wl + wo);
         if (SPLIT) {
           const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Wl + NCOL * KP + wo);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc[t], 0, 0, 0);
         }
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc[t], 0, 0, 0);
+        // keep the LDS fragment reads from being hoisted all at once (VGPR pressure ->
+        // occupancy): a scheduling fence every 3 tiles
+        if (t % 3 == 2) __builtin_amdgcn_sched_barrier(0);
       }
     }
 
-    // ---- epilogue on the accumulators: acc[t][i] = C[row 4*g4+i][col c0 + t*16 + l15]
-    if (g.bias) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] += g.bias[min(c0 + t * 16 + l15, N - 1)];
+    if (g.a_ln == LN_GIVEN) {  // next tile's stats, in flight through the epilogue
+      gmean = g.a_stats[2 * arow_n];
+      grstd = g.a_stats[2 * arow_n + 1];
     }
-#pragma unroll 1
-    for (int i = 0; i < 4; ++i) {
-      const int row = tile * 16 + 4 * g4 + i;
-      const bool rv = row < M;
-      const int rowc = min(row, M - 1);
-      float rm_ = 0.f, rs_ = 1.f, bs = 1.f;
-      if (EPI == EPI_LN_GELU) {  // full row in this wave (NCOL == N): 16-lane reductions
-        float s = 0.f;
+
+    // ---- epilogue: acc[t][i] = out[position tile*16 + l15][channel c0 + t*16 + 4*g4 + i]
+    const int row = tile * 16 + l15;
+    const bool rv = row < M;
+    const int rowc = min(row, M - 1);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) s += acc[t][i];
-        rm_ = group_sum<16>(s) / (float)N;
-        float q = 0.f;
+    for (int t = 0; t < NT; ++t) acc[t] += *reinterpret_cast<const f32x4*>(ebias + t * 16 + 4 * g4);
+    float rm_ = 0.f, rs_ = 1.f, bs = 1.f;
+    if (EPI == EPI_LN_GELU) {  // full row in this wave (NCOL == N): the 4 lanes of a position
+      float s = 0.f;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const float d = acc[t][i] - rm_;
-          q += d * d;
-        }
-        rs_ = rsqrtf(group_sum<16>(q) / (float)N + g.e_eps);
-      } else if (EPI == EPI_RESID) {
-        if (g.r_stats) {
-          rm_ = g.r_stats[2 * rowc];
-          rs_ = g.r_stats[2 * rowc + 1];
-        }
-        if (g.r_scale) bs = g.r_scale[rowc / (int)g.rows_per_sample];
-      }
+      for (int t = 0; t < NT; ++t) s += (acc[t].x + acc[t].y) + (acc[t].z + acc[t].w);
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      rm_ = s / (float)N;
+      float q = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const int col = c0 + t * 16 + l15;
-        const int colc = min(col, N - 1);
-        float v = acc[t][i];
-        if (EPI == EPI_LN_GELU) {
-          v = gelu_erf((v - rm_) * rs_ * g.e_ln_w[colc] + g.e_ln_b[colc]);
-        } else if (EPI == EPI_RESID) {
-          const float xr = g.r_x[(int64_t)rowc * N + colc];
-          if (g.r_stats) {
-            const float n2 = (xr - rm_) * rs_ * g.r_ln_w[colc] + g.r_ln_b[colc];
-            v = xr + (n2 + v) * bs;  // attn_fused + drop_path(n2 + ffn(n2)), quirk Q4
-          } else {
-            v = xr + v * bs;         // bare CCF_FFN.forward: x + x_out
-          }
-        }
-        if (rv && col < N) {
-          if (g.out_bf16)
-            reinterpret_cast<uint16_t*>(g.out)[(int64_t)row * g.ldo + col] = f2bf(v);
-          else
-            reinterpret_cast<float*>(g.out)[(int64_t)row * g.ldo + col] = v;
+        const f32x4 d = acc[t] - rm_;
+        q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+      }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      rs_ = rsqrtf(q / (float)N + g.e_eps);
+    } else if (EPI == EPI_RESID) {
+      if (g.r_stats) {
+        rm_ = g.r_stats[2 * rowc];
+        rs_ = g.r_stats[2 * rowc + 1];
+      }
+      if (g.r_scale) bs = g.r_scale[rowc / (int)g.rows_per_sample];
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = c0 + t * 16 + 4 * g4;
+      const int colc = min(col, N - 4);
+      f32x4 v = acc[t];
+      if (EPI == EPI_LN_GELU) {
+        const f32x4 lw = *reinterpret_cast<const f32x4*>(elw + t * 16 + 4 * g4);
+        const f32x4 lb = *reinterpret_cast<const f32x4*>(elb + t * 16 + 4 * g4);
+        v = (v - rm_) * rs_ * lw + lb;
+        v.x = gelu_erf(v.x);
+        v.y = gelu_erf(v.y);
+        v.z = gelu_erf(v.z);
+        v.w = gelu_erf(v.w);
+      } else if (EPI == EPI_RESID) {
+        const f32x4 xr = *reinterpret_cast<const f32x4*>(g.r_x + (int64_t)rowc * N + colc);
+        if (g.r_stats) {
+          const f32x4 lw = *reinterpret_cast<const f32x4*>(g.r_ln_w + colc);
+          const f32x4 lb = *reinterpret_cast<const f32x4*>(g.r_ln_b + colc);
+          const f32x4 n2 = (xr - rm_) * rs_ * lw + lb;
+          v = xr + (n2 + v) * bs;  // attn_fused + drop_path(n2 + ffn(n2)), quirk Q4
+        } else {
+          v = xr + v * bs;         // bare CCF_FFN.forward: x + x_out
         }
       }
+      if (rv && col < N) {
+        if (g.out_bf16) {
+          bf16x4 o;
+          o[0] = (short)f2bf(v.x);
+          o[1] = (short)f2bf(v.y);
+          o[2] = (short)f2bf(v.z);
+          o[3] = (short)f2bf(v.w);
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(g.out) + (int64_t)row * g.ldo + col) = o;
+        } else {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(g.out) + (int64_t)row * g.ldo + col) = v;
+        }
+      }
+      if (t % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // bound load hoisting (VGPRs)
     }
+    arow_c = arow_n;
+    rm = rmn;
   }
 }
 
@@ -277,7 +296,7 @@ static void dispatch_nt(int nt, const GemmArgs& g, dim3 grid, size_t lds, hipStr
   }
 }
 
-int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s) {
+int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_only) {
   if (g.N % 16 != 0 || g.K < 8 || g.M >= ((int64_t)1 << 31)) return 0;
   // call-site shapes (the others fall back to gemm_ares): window qkv, identity store/LN/resid,
   // PatchMerging gather
@@ -299,8 +318,9 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s) {
     }
   }
   if (nt == 0) return 0;
-  const size_t lds = (size_t)nt * 16 * per_col;
+  const size_t lds = (size_t)nt * 16 * per_col + (size_t)(2 * K32 + 3 * nt * 16) * 4;
   const int chunks = tiles / nt;
+  if (single_chunk_only && chunks > 1) return 0;
   const int64_t ntiles = (g.M + 15) / 16;
   int64_t gx = cdiv(ntiles, 8);
   const int64_t cap = (512 + chunks - 1) / chunks;  // ~2 workgroups of 8 waves per CU

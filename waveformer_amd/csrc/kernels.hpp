@@ -16,7 +16,9 @@ enum Prec { PREC_BF16 = 0, PREC_SPLIT = 1 };
 // A rows are produced by a loader (gather + optional LayerNorm + bf16 rounding) into LDS once
 // per workgroup; the weight Wt [2][N][K] (bf16 hi plane, then lo plane) streams from L2.
 enum RowMap { MAP_IDENTITY = 0, MAP_WINDOW = 1, MAP_MERGE = 2 };
-enum LnMode { LN_NONE = 0, LN_GIVEN = 1, LN_COMPUTE = 2 };
+// LN_PARTIAL: a_stats holds a_np (mean, M2) pairs per row, each over K / a_np consecutive
+// columns (written by the producing kernel); the loader combines them (Chan et al.).
+enum LnMode { LN_NONE = 0, LN_GIVEN = 1, LN_COMPUTE = 2, LN_PARTIAL = 3 };
 enum EpiMode { EPI_STORE = 0, EPI_LN_GELU = 1, EPI_RESID = 2 };
 
 struct GemmArgs {
@@ -30,10 +32,12 @@ struct GemmArgs {
   int mB, mD, mH, mW, mws;  // geometry of the source raster for MAP_WINDOW / MAP_MERGE
   int merge_code;        // MAP_MERGE: 8 nibbles, sub-lattice s offset (d<<2|h<<1|w) at bits 4s
   int a_ln;              // LnMode
-  const float* a_stats;  // LN_GIVEN: (M, 2) {mean, rstd}
+  const float* a_stats;  // LN_GIVEN: (M, 2) {mean, rstd};  LN_PARTIAL: (M, a_np, 2) {mean, M2}
+  int a_np;
   const float* a_ln_w;
   const float* a_ln_b;
   float a_eps;
+  int a_gelu;            // 1: GELU(erf) after the loader's LayerNorm (CCF_FFN norm -> act)
   // ---- B
   const uint16_t* w;     // [2][N][K] bf16 (hi plane; lo plane read only for PREC_SPLIT)
   // ---- problem
@@ -58,7 +62,7 @@ struct GemmArgs {
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);
 // streaming variant (gemm_rows.hip); returns 1 if it took the shape, 0 to fall back
-int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s);
+int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_only);
 
 // ---- windowed attention core over a (B_, N, 3C) qkv buffer (bf16, or fp32 when SPLIT) ----
 int launch_attn_core(const void* qkv, const float* bias, void* out, int64_t Bw, int N,
@@ -69,5 +73,14 @@ int launch_attn_core(const void* qkv, const float* bias, void* out, int64_t Bw, 
 int launch_dwconv_ln_gelu(const void* in, const float* w, const float* b, const float* ln_w,
                           const float* ln_b, float eps, void* out, int B, int Hd, int D, int H,
                           int W, int prec, hipStream_t s);
+// ---- depthwise 3^3 conv + bias only (the LayerNorm + GELU run in the next GEMM's loader);
+// returns 0 on success, WF_E_SHAPE if the shape is not covered (Hd % 32 != 0)
+// pstats (optional): (M, Hd / 32, 2) {mean, M2} of each 32-channel group of every output row
+int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, float* pstats,
+                    int B, int Hd, int D, int H, int W, int prec, hipStream_t s);
+constexpr int DW_STAT_GROUP = 32;
+// K-chunked MFMA GEMM (gemm_kc.hip) for the shapes whose weight does not fit gemm_rows' LDS
+// in one column chunk; returns 1 if it took the shape
+int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s);
 
 }  // namespace wf

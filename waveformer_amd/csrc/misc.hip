@@ -12,44 +12,76 @@ namespace wf {
 // Workgroup = one output row (b, z, y): the 2x2 input rows of every input channel are staged
 // in LDS (coalesced along x), the weights next to them; outputs are written channel-last.
 // ---------------------------------------------------------------------------------------
+// Thread = (output channel co, x group xg): the Cin*8 weights of co sit in registers and the
+// thread walks x = xg, xg + XG, ...; the slab reads are wave-wide broadcasts (a wave covers at
+// most two x positions) and the stores are contiguous channel-last rows.
+template <int CIN>
 __global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ bias,
-                                                          float* __restrict__ out, int Cin,
+                                                          float* __restrict__ out, int Cin_rt,
                                                           int Cout, int D, int H, int W) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+  extern __shared__ __attribute__((aligned(16))) float slab[];  // [Cin][dz][dy][2W]
+  const int Cin = CIN > 0 ? CIN : Cin_rt;
   const int W2 = 2 * W, H2 = 2 * H, D2 = 2 * D;
-  float* slab = sm;                       // [Cin][2][2][W2]
-  float* ws = slab + (size_t)Cin * 4 * W2;  // [Cout][Cin*8]
-  float* bs = ws + (size_t)Cout * Cin * 8;
   int r = blockIdx.x;
   const int y = r % H;
   r /= H;
   const int z = r % D;
   const int b = r / D;
   const int tid = threadIdx.x;
-  for (int i = tid; i < Cin * 4 * W2; i += blockDim.x) {
-    const int xx = i % W2;
-    int t = i / W2;
-    const int dy = t & 1, dz = (t >> 1) & 1, ci = t >> 2;
-    slab[i] = x[((((int64_t)b * Cin + ci) * D2 + 2 * z + dz) * H2 + 2 * y + dy) * W2 + xx];
-  }
-  for (int i = tid; i < Cout * Cin * 8; i += blockDim.x) ws[i] = w[i];
-  for (int i = tid; i < Cout; i += blockDim.x) bs[i] = bias ? bias[i] : 0.f;
-  __syncthreads();
-  float* orow = out + (((int64_t)b * D + z) * H + y) * W * (int64_t)Cout;
-  for (int i = tid; i < W * Cout; i += blockDim.x) {
-    const int co = i % Cout, xo = i / Cout;
-    float acc = bs[co];
-    const float* wr = ws + (size_t)co * Cin * 8;
-    for (int ci = 0; ci < Cin; ++ci) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {  // weight index (dz, dy, dx) = (k>>2, k>>1 & 1, k & 1)
-        const int dz = k >> 2, dy = (k >> 1) & 1, dx = k & 1;
-        acc += wr[ci * 8 + k] * slab[((ci * 2 + dz) * 2 + dy) * W2 + 2 * xo + dx];
-      }
+  // stage the 2x2 input rows of every input channel (float4 when the row allows it)
+  if ((W2 & 3) == 0) {
+    const int n4 = Cin * 4 * (W2 >> 2);
+    for (int i = tid; i < n4; i += blockDim.x) {
+      const int x4 = i % (W2 >> 2);
+      const int t = i / (W2 >> 2);
+      const int dy = t & 1, dz = (t >> 1) & 1, ci = t >> 2;
+      reinterpret_cast<f32x4*>(slab)[i] = reinterpret_cast<const f32x4*>(
+          x + ((((int64_t)b * Cin + ci) * D2 + 2 * z + dz) * H2 + 2 * y + dy) * W2)[x4];
     }
-    orow[i] = acc;
+  } else {
+    for (int i = tid; i < Cin * 4 * W2; i += blockDim.x) {
+      const int xx = i % W2;
+      const int t = i / W2;
+      const int dy = t & 1, dz = (t >> 1) & 1, ci = t >> 2;
+      slab[i] = x[((((int64_t)b * Cin + ci) * D2 + 2 * z + dz) * H2 + 2 * y + dy) * W2 + xx];
+    }
+  }
+  const int XG = blockDim.x / Cout;
+  const int co = tid % Cout, xg = tid / Cout;
+  const bool act = xg < XG;
+  const int cw = act ? co : 0;
+  // weight (co, ci, dz, dy, dx) at w[(co * Cin + ci) * 8 + (dz * 4 + dy * 2 + dx)]
+  constexpr int NW = CIN > 0 ? CIN * 8 : 1;
+  float wr[NW];
+  if (CIN > 0) {
+#pragma unroll
+    for (int k = 0; k < NW; ++k) wr[k] = w[(int64_t)cw * NW + k];
+  }
+  const float bv = bias ? bias[cw] : 0.f;
+  __syncthreads();
+  if (!act) return;
+  float* orow = out + (((int64_t)b * D + z) * H + y) * W * (int64_t)Cout;
+  for (int xo = xg; xo < W; xo += XG) {
+    float acc = bv;
+    if (CIN > 0) {
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // q = dz * 2 + dy; the dx pair is adjacent in the slab
+          const float2 v = *reinterpret_cast<const float2*>(slab + (ci * 4 + q) * W2 + 2 * xo);
+          acc += wr[ci * 8 + 2 * q] * v.x + wr[ci * 8 + 2 * q + 1] * v.y;
+        }
+    } else {
+      for (int ci = 0; ci < Cin; ++ci)
+        for (int q = 0; q < 4; ++q) {
+          const float2 v = *reinterpret_cast<const float2*>(slab + (ci * 4 + q) * W2 + 2 * xo);
+          acc += w[((int64_t)co * Cin + ci) * 8 + 2 * q] * v.x +
+                 w[((int64_t)co * Cin + ci) * 8 + 2 * q + 1] * v.y;
+        }
+    }
+    orow[(int64_t)xo * Cout + co] = acc;
   }
 }
 
@@ -158,6 +190,88 @@ __global__ __launch_bounds__(256) void msfuse_kernel(MsfuseArgs a) {
   }
 }
 
+// Row variant: workgroup = one output row (b, z, y).  For each source the depth/height
+// interpolation is done once per source x position -- R_s[xs] = wz0 (wy0 r00 + wy1 r01) +
+// wz1 (wy0 r10 + wy1 r11) over the 4 contributing source rows, staged in LDS -- and each output
+// then needs 2 LDS reads per source (x interpolation last; ATen interpolates x first, so the
+// fp32 rounding differs in the last bits).  Global traffic: the 4 source rows per source (L2)
+// plus one read of the shortcut row and one write of the output row.
+template <int G, int V>
+__global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float R[];  // sum_s sw[s] * C
+  const int C = a.C, C4 = C >> 2;
+  int r = blockIdx.x;
+  const int y = r % a.H;
+  r /= a.H;
+  const int z = r % a.D;
+  const int b = r / a.D;
+  const int tid = threadIdx.x;
+  int roff[4];
+  int ro = 0;
+  for (int s = 0; s < a.nsrc; ++s) {
+    roff[s] = ro;
+    const int sd = a.sd[s], sh = a.sh[s], sw = a.sw[s];
+    int z0, z1, y0, y1;
+    float wz0, wz1, wy0, wy1;
+    lin_index(z, sd, a.D, z0, z1, wz0, wz1);
+    lin_index(y, sh, a.H, y0, y1, wy0, wy1);
+    const f32x4* base = reinterpret_cast<const f32x4*>(a.src[s] + (int64_t)b * sd * sh * sw * C);
+    const f32x4* r00 = base + ((int64_t)z0 * sh + y0) * sw * C4;
+    const f32x4* r01 = base + ((int64_t)z0 * sh + y1) * sw * C4;
+    const f32x4* r10 = base + ((int64_t)z1 * sh + y0) * sw * C4;
+    const f32x4* r11 = base + ((int64_t)z1 * sh + y1) * sw * C4;
+    for (int i = tid; i < sw * C4; i += blockDim.x) {
+      const f32x4 t0 = r00[i] * wy0 + r01[i] * wy1;
+      const f32x4 t1 = r10[i] * wy0 + r11[i] * wy1;
+      reinterpret_cast<f32x4*>(R + ro)[i] = t0 * wz0 + t1 * wz1;
+    }
+    ro += sw * C;
+  }
+  __syncthreads();
+  const int lane = tid & 63, gl = lane & (G - 1);
+  const int gpb = blockDim.x / G;
+  bool live[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) live[j] = gl + j * G < C4;
+  const float bs = a.branch_scale ? a.branch_scale[b] : 1.f;
+  const int64_t rowbase = (((int64_t)b * a.D + z) * a.H + y) * a.W;
+  for (int x = tid / G; x < a.W; x += gpb) {
+    f32x4 acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = f32x4{0, 0, 0, 0};
+    for (int s = 0; s < a.nsrc; ++s) {
+      int x0, x1;
+      float wx0, wx1;
+      lin_index(x, a.sw[s], a.W, x0, x1, wx0, wx1);
+      const f32x4* R0 = reinterpret_cast<const f32x4*>(R + roff[s]) + x0 * C4;
+      const f32x4* R1 = reinterpret_cast<const f32x4*>(R + roff[s]) + x1 * C4;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c4 = min(gl + j * G, C4 - 1);
+        acc[j] += R0[c4] * wx0 + R1[c4] * wx1;
+      }
+    }
+    const f32x4* sc = reinterpret_cast<const f32x4*>(a.shortcut + (rowbase + x) * C);
+    f32x4* dst = reinterpret_cast<f32x4*>(a.out + (rowbase + x) * C);
+    f32x4 v[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c4 = min(gl + j * G, C4 - 1);
+      const f32x4 o = sc[c4] + acc[j] * bs;
+      v[j] = live[j] ? o : f32x4{0, 0, 0, 0};
+      if (live[j]) dst[c4] = o;
+    }
+    if (a.stats) {
+      float mean, rstd;
+      row_stats<G, V>(v, live, (float)C, a.eps, mean, rstd);
+      if (gl == 0) {
+        a.stats[2 * (rowbase + x)] = mean;
+        a.stats[2 * (rowbase + x) + 1] = rstd;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // proj_out: channel-last (B, S, C) -> [non-affine LayerNorm] -> NCDHW (B, C, S).
 // Tile = TP positions of one batch; row groups normalise into an LDS [C][TP+1] image, then
@@ -222,11 +336,19 @@ extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* b
   WF_REQUIRE_PTR(x);
   WF_REQUIRE_PTR(w);
   WF_REQUIRE_PTR(out);
-  const size_t lds = ((size_t)Cin * 8 * W + (size_t)Cout * Cin * 8 + Cout) * sizeof(float);
+  WF_REQUIRE(Cout <= 256, "PatchEmbed: at most 256 output channels");
+  const size_t lds = (size_t)Cin * 8 * W * sizeof(float);
   WF_REQUIRE(lds <= 64 * 1024, "PatchEmbed row tile exceeds 64 KB of LDS");
-  hipLaunchKernelGGL(patch_embed_kernel, dim3((unsigned)(B * D * H)), dim3(256), lds,
-                     (hipStream_t)stream, x, w, bias, out, (int)Cin, (int)Cout, (int)D, (int)H,
-                     (int)W);
+  const dim3 grid((unsigned)(B * D * H)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  const int ci = (int)Cin, co = (int)Cout, d = (int)D, h = (int)H, ww = (int)W;
+  switch (Cin) {
+    case 1: hipLaunchKernelGGL(patch_embed_kernel<1>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
+    case 2: hipLaunchKernelGGL(patch_embed_kernel<2>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
+    case 3: hipLaunchKernelGGL(patch_embed_kernel<3>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
+    case 4: hipLaunchKernelGGL(patch_embed_kernel<4>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
+    default: hipLaunchKernelGGL(patch_embed_kernel<0>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
+  }
   return check_launch("wf_patch_embed_fwd");
 }
 
@@ -260,8 +382,15 @@ extern "C" int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, in
   a.H = (int)H;
   a.W = (int)W;
   const int64_t total = B * D * H * W;
+  int64_t rlds = 0;
+  for (int s = 0; s < nsrc; ++s) rlds += (int64_t)a.sw[s] * C * 4;
   return dispatch_gv(C / 4, [&](auto G_, auto V_) -> int {
     constexpr int G = decltype(G_)::value, V = decltype(V_)::value;
+    if (rlds <= 64 * 1024 && B * D * H < ((int64_t)1 << 31)) {
+      hipLaunchKernelGGL((msfuse_row_kernel<G, V>), dim3((unsigned)(B * D * H)), dim3(256),
+                         (size_t)rlds, (hipStream_t)stream, a);
+      return check_launch("wf_msfuse_fwd");
+    }
     int64_t blocks = cdiv(total, 256 / G);
     if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL((msfuse_kernel<G, V>), dim3((unsigned)blocks), dim3(256), 0,

@@ -47,16 +47,36 @@ __device__ __forceinline__ float gelu_erf(float x) {
 // ---------------------------------------------------------------------------------------
 // sub-wave reductions: a "row group" is G consecutive lanes (G a power of two <= 64)
 // ---------------------------------------------------------------------------------------
+// Butterflies on the VALU's DPP lane crossbar where the partner lies in the same 16-lane row
+// (quad_perm xor 1 / xor 2, row_half_mirror, row_mirror -- each leaves every lane of the 2/4/
+// 8/16-lane group holding the group total), ds_swizzle (xor 16 inside 32 lanes) and one
+// ds_bpermute for the 32-lane halves: no LDS-routed shuffle below 32 lanes.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float swz_xor16(float v) {
+  // ds_swizzle bit-mask mode: and 0x1F, or 0, xor 0x10 (within each 32-lane half)
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
+}
 template <int G>
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (G >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (G >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (G >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
+  if (G >= 16) v += dpp_mov<0x140>(v); // row_mirror
+  if (G >= 32) v += swz_xor16(v);
+  if (G >= 64) v += __shfl_xor(v, 32, 64);
   return v;
 }
 template <int G>
 __device__ __forceinline__ float group_max(float v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if (G >= 2) v = fmaxf(v, dpp_mov<0xB1>(v));
+  if (G >= 4) v = fmaxf(v, dpp_mov<0x4E>(v));
+  if (G >= 8) v = fmaxf(v, dpp_mov<0x141>(v));
+  if (G >= 16) v = fmaxf(v, dpp_mov<0x140>(v));
+  if (G >= 32) v = fmaxf(v, swz_xor16(v));
+  if (G >= 64) v = fmaxf(v, __shfl_xor(v, 32, 64));
   return v;
 }
 

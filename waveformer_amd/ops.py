@@ -309,14 +309,31 @@ def ccf_ffn(xh: torch.Tensor, stats: Optional[torch.Tensor], norm2: Optional[tor
     n2w = n2b = None
     if stats is not None:
         n2w, n2b = norm2.weight, norm2.bias
-    _lib.call("wf_ccf_ffn_fwd", xh.data_ptr(), _ptr(stats), _ptr(n2w), _ptr(n2b),
-              pw.data_ptr(), _ptr(mlp.pwconv.bias), mlp.norm1.weight.data_ptr(),
-              mlp.norm1.bias.data_ptr(), float(mlp.norm1.eps), mlp.dwconv.weight.data_ptr(),
-              mlp.dwconv.bias.data_ptr(), mlp.norm2.weight.data_ptr(), mlp.norm2.bias.data_ptr(),
-              float(mlp.norm2.eps), fc.data_ptr(), _ptr(mlp.fc.bias), _ptr(branch_scale),
-              out.data_ptr(),
-              work.data_ptr(), B, C, hid, D, H, W, prec, _stream())
+    args = (xh.data_ptr(), _ptr(stats), _ptr(n2w), _ptr(n2b),
+            pw.data_ptr(), _ptr(mlp.pwconv.bias), mlp.norm1.weight.data_ptr(),
+            mlp.norm1.bias.data_ptr(), float(mlp.norm1.eps), mlp.dwconv.weight.data_ptr(),
+            mlp.dwconv.bias.data_ptr(), mlp.norm2.weight.data_ptr(), mlp.norm2.bias.data_ptr(),
+            float(mlp.norm2.eps), fc.data_ptr(), _ptr(mlp.fc.bias), _ptr(branch_scale),
+            out.data_ptr(), work.data_ptr(), B, C, hid, D, H, W, prec, _stream())
+    # the three launches are issued separately so they can be timed one by one (bench.py)
+    ccf_ffn_pwconv(args)
+    ccf_ffn_dwconv(args, B * D * H * W, hid)
+    ccf_ffn_fc(args)
     return out
+
+
+def ccf_ffn_pwconv(args):
+    _lib.call("wf_ccf_ffn_stage", 1, *args)
+
+
+def ccf_ffn_dwconv(args, positions: int, hidden: int):
+    """Depthwise 3^3 conv over the (positions, hidden) h1 of the workspace -> h2 + LN partials
+    (positions/hidden are only used by the bench's byte count)."""
+    _lib.call("wf_ccf_ffn_stage", 2, *args)
+
+
+def ccf_ffn_fc(args):
+    _lib.call("wf_ccf_ffn_stage", 3, *args)
 
 
 # ------------------------------------------------------------------------------------------
