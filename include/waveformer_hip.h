@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 3
+#define WF_ABI_VERSION 4
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1 };
 
@@ -184,6 +184,43 @@ int wf_patch_merging_fwd(const float* x, const float* ln_w, const float* ln_b, f
  * x channel-last (B, S, C) (S = D*H*W) -> out NCDHW (B, C, S).  normalize=0 only transposes. */
 int wf_proj_out_fwd(const float* x, float* out, int normalize, float eps, int64_t B,
                     int64_t C, int64_t S, void* stream);
+
+/* ---- sliding-window inference (config 3) ----------------------- */
+/* Replaces monai.data.utils.compute_importance_map (monai/data/utils.py:1088-1138) as called
+ * by sliding_window_inference (monai/inferers/utils.py:194-207).  mode 0 = 'constant' (ones),
+ * 1 = 'gaussian': exp(x^2 / (-2 sigma^2)) per axis with x = -(n-1)/2 .. (n-1)/2 and
+ * sigma = sigma_scale[axis] * n, multiplied out in (z, y, x) order and clamped below at
+ * max(min, 1e-3).  out: (rd, rh, rw) fp32.  sigma_scale: 3 host floats (NULL for mode 0).   */
+int wf_importance_map(int mode, const float* sigma_scale, float* out, int64_t rd, int64_t rh,
+                      int64_t rw, void* stream);
+
+/* Replaces the accumulation loop of sliding_window_inference (monai/inferers/utils.py:216-299:
+ * out[slice] += pred * w, count[slice] += w, out /= count) for predictor outputs of the
+ * window's own spatial size.  Gather form: every output voxel sums the windows covering it
+ * in ascending window order with the reference's fp32 operation order.
+ * starts: host int64 array of nwin[0] + nwin[1] + nwin[2] window starts (z, then y, then x;
+ *   strictly ascending per axis, spanning the axis -- dense_patch_slices,
+ *   monai/data/utils.py:171-211); windows are numbered in its 'ij' meshgrid order and images
+ *   batch-major: g = b * nwin_total + (iz * nwin[1] + iy) * nwin[2] + ix.
+ * patches: (rows, C, rd, rh, rw) fp32.  Window g lives in row
+ *   ((j / slots_per_round) * world + g % world) * slots_per_round + j % slots_per_round,
+ *   j = g / world: the layout of per-round all-gathers of round-robin shards (window g on
+ *   rank g % world, slot j).  world = 1 (any slots_per_round) is plain window order.
+ * importance_map: (rd, rh, rw) fp32 (wf_importance_map or a caller's roi_weight_map).
+ * out: (B, C, D, H, W) fp32, D/H/W the (padded) image size.                                 */
+int wf_sliding_window_stitch(const float* patches, int64_t world, int64_t slots_per_round,
+                             const float* importance_map, const int64_t* starts,
+                             const int64_t* nwin, float* out, int64_t B, int64_t C, int64_t D,
+                             int64_t H, int64_t W, int64_t rd, int64_t rh, int64_t rw,
+                             void* stream);
+
+/* Flip test-time augmentation merge of Predictor.maybe_mirror_and_predict
+ * (light_training/prediction.py:110-160): out = (sum_p flip_p(pred[p])) / npass, summed in
+ * pass order.  pred: (npass, C, D, H, W) fp32, pass p computed on the input flipped along the
+ * axes of flips[p] (host int mask: bit 0 = D, bit 1 = H, bit 2 = W; 0 = no flip), npass <= 8.
+ * out: (C, D, H, W) fp32.                                                                    */
+int wf_tta_merge(const float* pred, const int* flips, int npass, float* out, int64_t C,
+                 int64_t D, int64_t H, int64_t W, void* stream);
 
 #ifdef __cplusplus
 }

@@ -43,9 +43,13 @@ SIGNATURES = {
     "wf_patch_merging_fwd": (_I, [_P, _P, _P, _F, _P, _I, _P, _I64, _I64, _I64, _I64, _I64,
                                   _I, _P]),
     "wf_proj_out_fwd": (_I, [_P, _P, _I, _F, _I64, _I64, _I64, _P]),
+    "wf_importance_map": (_I, [_I, _P, _P, _I64, _I64, _I64, _P]),
+    "wf_sliding_window_stitch": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _I64,
+                                      _I64, _I64, _I64, _I64, _P]),
+    "wf_tta_merge": (_I, [_P, _P, _I, _P, _I64, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _lock = threading.Lock()
 _lib = None
 _err = None

@@ -1,0 +1,251 @@
+// stitch.hip -- sliding-window inference: importance map and the gather-form stitch.
+//
+// Replaces the accumulation half of MONAI's sliding_window_inference as WaveFormer's
+// prediction path calls it (SlidingWindowInferer(roi 128^3, sw_batch 2, overlap 0.5,
+// 'gaussian'), 4_predict.py:199-205):
+//   * compute_importance_map (monai/data/utils.py:1088-1138): separable gaussian
+//     exp(x^2 / (-2 sigma^2)) per axis, multiplied out, clamped below at max(min, 1e-3);
+//   * the per-window `out[slice] += pred * w` / `count[slice] += w` loop and the final
+//     `out /= count` (monai/inferers/utils.py:216-299).
+// The scatter of the reference becomes a gather: one thread per output voxel walks the windows
+// that cover it in ascending window order, so the fp32 sums are formed in exactly the
+// reference's order (explicit _rn intrinsics, no FMA contraction) with no atomics and one
+// write per output element.  The patches may come from an RCCL all-gather of round-robin
+// shards (see wf_sliding_window_stitch in include/waveformer_hip.h for the row mapping).
+#include "wf_common.hpp"
+
+namespace wf {
+
+constexpr int SW_MAX_WIN = 64;  // windows per axis
+
+struct StitchArgs {
+  const float* patches;  // (rows, C, rd, rh, rw)
+  const float* map;      // (rd, rh, rw)
+  float* out;            // (B, C, D, H, W)
+  int B, C, D, H, W;
+  int rd, rh, rw;
+  int n[3];              // windows per axis (z, y, x)
+  int world, sb;         // row mapping of the gathered shards
+  int starts[3][SW_MAX_WIN];
+};
+
+__device__ __forceinline__ void cover(const int* st, int n, int r, int p, int& lo, int& hi) {
+  lo = n;
+  hi = -1;
+  for (int i = 0; i < n; ++i) {
+    const int s = st[i];
+    if (s <= p && p < s + r) {
+      lo = min(lo, i);
+      hi = i;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
+  const int64_t total = (int64_t)a.B * a.D * a.H * a.W;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  int64_t t = idx;
+  const int x = (int)(t % a.W);
+  t /= a.W;
+  const int y = (int)(t % a.H);
+  t /= a.H;
+  const int z = (int)(t % a.D);
+  const int b = (int)(t / a.D);
+  int z0, z1, y0, y1, x0, x1;
+  cover(a.starts[0], a.n[0], a.rd, z, z0, z1);
+  cover(a.starts[1], a.n[1], a.rh, y, y0, y1);
+  cover(a.starts[2], a.n[2], a.rw, x, x0, x1);
+  const int64_t R3 = (int64_t)a.rd * a.rh * a.rw;
+  const int64_t nwin = (int64_t)a.n[0] * a.n[1] * a.n[2];
+  const int64_t S = (int64_t)a.D * a.H * a.W;
+  float* dst = a.out + (int64_t)b * a.C * S + ((int64_t)z * a.H + y) * a.W + x;
+
+  // count map: sum of the window weights in window order (monai/inferers/utils.py:262-269)
+  float cnt = 0.f;
+  for (int iz = z0; iz <= z1; ++iz)
+    for (int iy = y0; iy <= y1; ++iy)
+      for (int ix = x0; ix <= x1; ++ix) {
+        const int64_t loc = ((int64_t)(z - a.starts[0][iz]) * a.rh + (y - a.starts[1][iy])) * a.rw +
+                            (x - a.starts[2][ix]);
+        cnt = __fadd_rn(cnt, a.map[loc]);
+      }
+
+  for (int c0 = 0; c0 < a.C; c0 += 4) {
+    const int nc = min(4, a.C - c0);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int iz = z0; iz <= z1; ++iz)
+      for (int iy = y0; iy <= y1; ++iy)
+        for (int ix = x0; ix <= x1; ++ix) {
+          const int64_t loc =
+              ((int64_t)(z - a.starts[0][iz]) * a.rh + (y - a.starts[1][iy])) * a.rw +
+              (x - a.starts[2][ix]);
+          const float w = a.map[loc];
+          // global window index (batch-major, then the 'ij' meshgrid order of
+          // dense_patch_slices) -> row of the gathered patch tensor
+          const int64_t g = (int64_t)b * nwin + ((int64_t)iz * a.n[1] + iy) * a.n[2] + ix;
+          const int64_t r = g % a.world, j = g / a.world;
+          const int64_t row = ((j / a.sb) * a.world + r) * a.sb + (j % a.sb);
+          const float* p = a.patches + (row * a.C + c0) * R3 + loc;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (c < nc) acc[c] = __fadd_rn(acc[c], __fmul_rn(p[c * R3], w));
+        }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < nc) dst[(int64_t)(c0 + c) * S] = __fdiv_rn(acc[c], cnt);
+  }
+}
+
+__global__ __launch_bounds__(256) void importance_map_kernel(float* out, int rd, int rh, int rw,
+                                                             int mode, float sz, float sy,
+                                                             float sx) {
+  const int64_t total = (int64_t)rd * rh * rw;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  if (mode == 0) {
+    out[idx] = 1.f;
+    return;
+  }
+  const int x = (int)(idx % rw), y = (int)((idx / rw) % rh), z = (int)(idx / ((int64_t)rw * rh));
+  // x_i = -(n-1)/2 + i; g = exp(x^2 / (-2 sigma^2)) (monai/data/utils.py:1121-1128)
+  auto g = [](int i, int n, float s) {
+    const float v = -(float)(n - 1) / 2.0f + (float)i;
+    return expf(__fdiv_rn(__fmul_rn(v, v), -2.0f * __fmul_rn(s, s)));
+  };
+  const float m = __fmul_rn(__fmul_rn(g(z, rd, sz), g(y, rh, sy)), g(x, rw, sx));
+  // the minimum of the map is the product of the three end-point values (all factors are
+  // positive and fp multiplication is monotone); clamp below at max(min, 1e-3) (:1134-1136)
+  const float mn = fmaxf(__fmul_rn(__fmul_rn(g(0, rd, sz), g(0, rh, sy)), g(0, rw, sx)), 1e-3f);
+  out[idx] = fmaxf(m, mn);
+}
+
+// Flip-TTA merge (light_training/prediction.py:123-155): pass p of `pred` was computed on the
+// image flipped along the axes of flips[p] (bit 0 = D, 1 = H, 2 = W); it is read back through
+// the mirrored index instead of materialising torch.flip copies, summed in pass order and
+// divided by the pass count.
+constexpr int TTA_MAX_PASSES = 8;
+struct TtaArgs {
+  const float* pred;  // (P, C, D, H, W)
+  float* out;         // (C, D, H, W)
+  int P, C, D, H, W;
+  int flips[TTA_MAX_PASSES];
+};
+
+__global__ __launch_bounds__(256) void tta_merge_kernel(TtaArgs a) {
+  const int64_t S = (int64_t)a.D * a.H * a.W;
+  const int64_t total = (int64_t)a.C * S;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int x = (int)(idx % a.W);
+  const int y = (int)((idx / a.W) % a.H);
+  const int z = (int)((idx / ((int64_t)a.W * a.H)) % a.D);
+  const int64_t c = idx / S;
+  float acc = 0.f;
+  for (int p = 0; p < a.P; ++p) {
+    const int f = a.flips[p];
+    const int zz = (f & 1) ? a.D - 1 - z : z;
+    const int yy = (f & 2) ? a.H - 1 - y : y;
+    const int xx = (f & 4) ? a.W - 1 - x : x;
+    const float v = a.pred[((int64_t)p * a.C + c) * S + ((int64_t)zz * a.H + yy) * a.W + xx];
+    acc = p == 0 ? v : __fadd_rn(acc, v);
+  }
+  a.out[idx] = __fdiv_rn(acc, (float)a.P);
+}
+
+}  // namespace wf
+
+using namespace wf;
+
+extern "C" int wf_tta_merge(const float* pred, const int* flips, int npass, float* out,
+                            int64_t C, int64_t D, int64_t H, int64_t W, void* stream) {
+  WF_REQUIRE_PTR(pred);
+  WF_REQUIRE_PTR(flips);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE(npass >= 1 && npass <= TTA_MAX_PASSES, "1..8 passes");
+  WF_REQUIRE(C >= 1 && D >= 1 && H >= 1 && W >= 1, "empty volume");
+  TtaArgs a{};
+  a.pred = pred;
+  a.out = out;
+  a.P = npass;
+  a.C = (int)C;
+  a.D = (int)D;
+  a.H = (int)H;
+  a.W = (int)W;
+  for (int p = 0; p < npass; ++p) {
+    WF_REQUIRE(flips[p] >= 0 && flips[p] <= 7, "flip mask must be in [0, 7]");
+    a.flips[p] = flips[p];
+  }
+  const int64_t total = C * D * H * W;
+  hipLaunchKernelGGL(tta_merge_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("tta_merge");
+}
+
+extern "C" int wf_importance_map(int mode, const float* sigma_scale, float* out, int64_t rd,
+                                 int64_t rh, int64_t rw, void* stream) {
+  WF_REQUIRE(mode == 0 || mode == 1, "mode must be 0 (constant) or 1 (gaussian)");
+  WF_REQUIRE(rd >= 1 && rh >= 1 && rw >= 1, "empty window");
+  WF_REQUIRE_PTR(out);
+  if (mode == 1) WF_REQUIRE_PTR(sigma_scale);
+  const float sz = mode ? sigma_scale[0] * (float)rd : 0.f;
+  const float sy = mode ? sigma_scale[1] * (float)rh : 0.f;
+  const float sx = mode ? sigma_scale[2] * (float)rw : 0.f;
+  if (mode) WF_REQUIRE(sz > 0.f && sy > 0.f && sx > 0.f, "sigma_scale must be positive");
+  const int64_t total = rd * rh * rw;
+  hipLaunchKernelGGL(importance_map_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, out, (int)rd, (int)rh, (int)rw, mode, sz, sy, sx);
+  return check_launch("importance_map");
+}
+
+extern "C" int wf_sliding_window_stitch(const float* patches, int64_t world,
+                                        int64_t slots_per_round, const float* importance_map,
+                                        const int64_t* starts, const int64_t* nwin, float* out,
+                                        int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                                        int64_t rd, int64_t rh, int64_t rw, void* stream) {
+  WF_REQUIRE_PTR(patches);
+  WF_REQUIRE_PTR(importance_map);
+  WF_REQUIRE_PTR(starts);
+  WF_REQUIRE_PTR(nwin);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE(B >= 1 && C >= 1 && D >= 1 && H >= 1 && W >= 1, "empty output");
+  WF_REQUIRE(world >= 1 && slots_per_round >= 1, "world and slots_per_round must be >= 1");
+  WF_REQUIRE(rd <= D && rh <= H && rw <= W, "window larger than the (padded) image");
+  StitchArgs a{};
+  a.patches = patches;
+  a.map = importance_map;
+  a.out = out;
+  a.B = (int)B;
+  a.C = (int)C;
+  a.D = (int)D;
+  a.H = (int)H;
+  a.W = (int)W;
+  a.rd = (int)rd;
+  a.rh = (int)rh;
+  a.rw = (int)rw;
+  a.world = (int)world;
+  a.sb = (int)slots_per_round;
+  const int64_t size[3] = {D, H, W}, roi[3] = {rd, rh, rw};
+  int64_t off = 0;
+  for (int ax = 0; ax < 3; ++ax) {
+    WF_REQUIRE(nwin[ax] >= 1 && nwin[ax] <= SW_MAX_WIN, "1..64 windows per axis");
+    a.n[ax] = (int)nwin[ax];
+    int64_t prev = -1;
+    for (int64_t i = 0; i < nwin[ax]; ++i) {
+      const int64_t s = starts[off + i];
+      WF_REQUIRE(s >= 0 && s + roi[ax] <= size[ax], "window start out of range");
+      WF_REQUIRE(s > prev, "window starts must be strictly ascending");
+      a.starts[ax][i] = (int)s;
+      prev = s;
+    }
+    // every voxel must be covered (dense_patch_slices guarantees it; a gap would divide by 0)
+    WF_REQUIRE(a.starts[ax][0] == 0 && prev + roi[ax] == size[ax], "windows do not span the axis");
+    for (int64_t i = 1; i < nwin[ax]; ++i)
+      WF_REQUIRE(a.starts[ax][i] <= a.starts[ax][i - 1] + roi[ax], "gap between windows");
+    off += nwin[ax];
+  }
+  const int64_t total = B * D * H * W;
+  hipLaunchKernelGGL(stitch_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("sliding_window_stitch");
+}

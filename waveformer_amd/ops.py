@@ -352,6 +352,73 @@ def patch_merging(x_cl: torch.Tensor, norm: torch.nn.LayerNorm, reduction: torch
 
 
 # ------------------------------------------------------------------------------------------
+# config 3: sliding-window inference (importance map + stitch)
+# ------------------------------------------------------------------------------------------
+BLEND_MODES = {"constant": 0, "gaussian": 1}
+
+
+def importance_map(roi: Sequence[int], mode: str = "constant",
+                   sigma_scale: Sequence[float] = (0.125, 0.125, 0.125),
+                   device: Optional[torch.device] = None) -> torch.Tensor:
+    """compute_importance_map (monai/data/utils.py:1088-1138) for a 3-D window, on the GPU."""
+    if mode not in BLEND_MODES:
+        raise ValueError(f"Unsupported mode: {mode}, available options are {sorted(BLEND_MODES)}.")
+    rd, rh, rw = (int(v) for v in roi)
+    device = torch.device(device) if device is not None else torch.device(
+        "cuda", torch.cuda.current_device())
+    if device.type != "cuda":
+        raise RuntimeError("importance_map: GPU only")
+    out = torch.empty((rd, rh, rw), dtype=torch.float32, device=device)
+    sig = (ctypes.c_float * 3)(*[float(s) for s in sigma_scale])
+    _lib.call("wf_importance_map", BLEND_MODES[mode], sig, out.data_ptr(), rd, rh, rw, _stream())
+    return out
+
+
+def sliding_window_stitch(patches: torch.Tensor, weight_map: torch.Tensor,
+                          starts: Sequence[Sequence[int]], image_size: Sequence[int],
+                          batch: int, world: int = 1, slots_per_round: int = 1) -> torch.Tensor:
+    """sum_w pred_w * map / sum_w map over the windows covering each voxel (the accumulation of
+    monai/inferers/utils.py:216-299) -> (batch, C, *image_size).  `patches` is
+    (rows, C, *roi); see wf_sliding_window_stitch for the row layout of sharded gathers."""
+    _check(patches, "patches")
+    _check(weight_map, "importance_map")
+    rows, C = patches.shape[:2]
+    roi = tuple(patches.shape[2:])
+    if tuple(weight_map.shape) != roi:
+        raise ValueError(f"sliding_window_stitch: map {tuple(weight_map.shape)} != roi {roi}")
+    nwin = [len(s) for s in starts]
+    total = batch * nwin[0] * nwin[1] * nwin[2]
+    slots = -(-total // world)
+    slots = -(-slots // slots_per_round) * slots_per_round
+    if rows < slots * world:
+        raise ValueError(f"sliding_window_stitch: {rows} patch rows < {slots * world} needed")
+    D, H, W = (int(v) for v in image_size)
+    out = torch.empty((batch, C, D, H, W), dtype=torch.float32, device=patches.device)
+    flat = [int(s) for ax in starts for s in ax]
+    sarr = (ctypes.c_int64 * len(flat))(*flat)
+    narr = (ctypes.c_int64 * 3)(*nwin)
+    _lib.call("wf_sliding_window_stitch", patches.data_ptr(), int(world), int(slots_per_round),
+              weight_map.data_ptr(), sarr, narr, out.data_ptr(), batch, C, D, H, W, *roi,
+              _stream())
+    return out
+
+
+def tta_merge(pred: torch.Tensor, passes: Sequence[Sequence[int]]) -> torch.Tensor:
+    """(P, C, D, H, W) per-pass predictions on flipped inputs -> (1, C, D, H, W) average of the
+    flipped-back passes (light_training/prediction.py:123-155).  passes[p] lists the flipped
+    tensor dims (2, 3, 4) of pass p."""
+    _check(pred, "pred")
+    P, C, D, H, W = pred.shape
+    if len(passes) != P:
+        raise ValueError(f"tta_merge: {len(passes)} passes for {P} predictions")
+    masks = [sum(1 << (d - 2) for d in f) for f in passes]
+    out = torch.empty((1, C, D, H, W), dtype=torch.float32, device=pred.device)
+    _lib.call("wf_tta_merge", pred.data_ptr(), (ctypes.c_int * P)(*masks), P, out.data_ptr(),
+              C, D, H, W, _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
 # a10: proj_out
 # ------------------------------------------------------------------------------------------
 def proj_out(x_cl: torch.Tensor, normalize: bool, eps: float = 1e-5) -> torch.Tensor:
