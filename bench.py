@@ -43,7 +43,7 @@ METRIC = "128³×4 volumes/sec fwd (1/2/4/8 MI355X) + Dice Δ vs reference"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 # bench op name -> kernel-name substring in the PMC summary (profiles/*pmc*.json)
-PMC_KERNEL = {"ccf_ffn_dwconv": "dwconv3d_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
+PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_dwfc_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
               "msfuse": "msfuse", "proj_out": "proj_out"}
 
 
@@ -70,12 +70,22 @@ def parse():
 # ------------------------------------------------------------------------------------------
 # per-launch timing of one op with HIP events on its stream
 # ------------------------------------------------------------------------------------------
+def _dwfc_fused(a):
+    """ops.ccf_ffn_dwconv(args, positions, hidden): stage 2 runs the fused back half of the FFN
+    (ffn_dwfc.hip) for C = 48, hidden = 192 (args[20] = C)."""
+    return a[0][20] == 48 and a[2] == 192
+
+
 def _dw_bytes(a, kw, out):
-    """CCF_FFN depthwise conv: read h1 + write h2 (positions x hidden, fp32 for bf16x3, bf16
-    for bf16) + the (mean, M2) partial per 32 channels of every position."""
+    """CCF_FFN stage 2.  Fused (C 48 / hidden 192): read h1 (positions x hidden, fp32 for
+    bf16x3, bf16 for bf16) + the residual rows x and their norm2 stats, write out.  Unfused:
+    read h1 + write h2 + the (mean, M2) partial per 32 channels of every position."""
     from waveformer_amd import ops
     P, Hd = a[1], a[2]
     e = 4 if ops.get_precision() == "bf16x3" else 2
+    if _dwfc_fused(a):
+        C = a[0][20]
+        return P * Hd * e + 2 * P * C * 4 + (P * 8 if a[0][1] else 0)
     return 2 * P * Hd * e + P * (Hd // 32) * 8
 
 

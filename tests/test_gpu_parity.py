@@ -158,6 +158,40 @@ def test_attention_vs_oracle(ws, heads, dim, B_):
         assert C.rel_l2(out, ref) <= tol, prec
 
 
+@pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (1, 16, 16, 16), (1, 3, 12, 9)])
+@pytest.mark.parametrize("block", [False, True])
+def test_ccf_ffn_stage1_fused_vs_oracle(shape, block):
+    """C = 48, hidden = 192: the fused dwconv + LN2 + GELU + fc + residual kernel
+    (ffn_dwfc.hip), ragged tiles included; Block form (norm2 + Q4 double residual, per-sample
+    DropPath factors) and bare CCF_FFN.forward."""
+    import waveformer_amd.network_models as NM
+    from oracle.weight_rule import rule_state_dict
+    from waveformer_amd import ops
+    B = shape[0]
+    mlp = NM.CCF_FFN(48, 192, img_size=shape[1:])
+    sd = rule_state_dict(mlp.state_dict())
+    mlp.load_state_dict(sd)
+    mlp = mlp.eval().to(DEV)
+    norm2 = torch.nn.LayerNorm(48, eps=1e-6)
+    with torch.no_grad():
+        norm2.weight.copy_(seeded_randn((48,), 31) * 0.2 + 1)
+        norm2.bias.copy_(seeded_randn((48,), 32) * 0.1)
+    norm2 = norm2.to(DEV)
+    x = seeded_randn(shape + (48,), 33)
+    bs = torch.tensor([0.5, 2.0][:B])
+    if block:
+        n2 = F.layer_norm(x, [48], norm2.weight.detach().cpu(), norm2.bias.detach().cpu(), 1e-6)
+        ref = x + R.ccf_ffn(sd, "", n2) * bs.view(-1, 1, 1, 1, 1)
+    else:
+        ref = x + (R.ccf_ffn(sd, "", x) - x) * bs.view(-1, 1, 1, 1, 1)
+    for prec, tol in (("bf16x3", 5e-5), ("bf16", 1e-2)):
+        with torch.no_grad(), ops.precision(prec):
+            xc = cuda(x)
+            stats = ops.msfuse([], xc, 1e-6)[1] if block else None
+            out = ops.ccf_ffn(xc, stats, norm2 if block else None, mlp, cuda(bs))
+        assert C.rel_l2(out, ref) <= tol, prec
+
+
 def test_window_attention_q1_layout_on_raster():
     """Raster attention == window_partition -> Attention -> plain reshape (quirk Q1)."""
     import waveformer_amd.network_models as NM

@@ -477,9 +477,34 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   int rc = 0;
   if (stage == 0 || stage == 1) rc = launch_gemm(g, s, "wf_ccf_ffn_fwd(pwconv)");
   if (rc) return rc;
-  // dwconv + LN2 + GELU: either fused in one kernel (LN over the full 4C row per position in
-  // LDS), or the z-marching depthwise conv with LN2 + GELU moved into the fc loader
+  // dwconv + LN2 + GELU (+ fc + residual): the stage-1 shape runs the fused back half
+  // (ffn_dwfc.hip, h2 stays on chip); other shapes either fuse dwconv + LN over the full 4C row
+  // in LDS, or run the z-marching depthwise conv with LN2 + GELU moved into the fc loader
   static const bool fused_dw = getenv("WF_FFN_FUSED_DW") != nullptr;
+  static const bool no_dwfc = getenv("WF_FFN_NO_DWFC") != nullptr;
+  if (!no_dwfc && C == 48 && hidden == 192) {
+    if (stage == 1 || stage == 3) return rc;  // stage 3 (fc) is part of the fused kernel
+    DwFcArgs d{};
+    d.h1 = h1;
+    d.dw_w = dw_w;
+    d.dw_b = dw_b;
+    d.ln2_w = ln2_w;
+    d.ln2_b = ln2_b;
+    d.eps2 = eps2;
+    d.fc = fc_bf16x2;
+    d.fc_b = fc_b;
+    d.x = xh;
+    d.stats = stats;
+    d.n2_w = n2_w;
+    d.n2_b = n2_b;
+    d.bscale = branch_scale;
+    d.out = out;
+    d.B = (int)B;
+    d.D = (int)D;
+    d.H = (int)H;
+    d.W = (int)W;
+    return launch_ffn_dwfc(d, precision, s);
+  }
   const bool split_ln = !fused_dw && hidden % 32 == 0;
   float* pst = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 2 * one);
   if (stage == 0 || stage == 2) {

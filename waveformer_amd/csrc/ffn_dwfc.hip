@@ -1,0 +1,332 @@
+// ffn_dwfc.hip -- the back half of CCF_FFN fused into one kernel for the stage-1 shape
+// (C = 48, hidden = 192; the largest FFN of the encoder):
+//
+//   h2  = dwconv3x3x3(h1) + b          (wave_helper.py:285, groups = hidden, pad 1)
+//   g   = GELU(LN_eps2(h2))            (:286-287)
+//   ffn = fc(g) + fc_b                 (:289, Linear hidden -> C)
+//   out = x + (n2 + ffn) * bs          (Block residual + CCF_FFN residual, quirk Q4, :293/:509)
+//         with n2 = LN(x; stats, n2_w, n2_b), or out = x + ffn * bs for a bare CCF_FFN.
+//
+// h2 never touches HBM (the unfused path writes and re-reads 2 x 805 MB of it per stage-1
+// block at B = 4).  A workgroup owns a 4 x 8 (y, x) tile and marches z through a segment of
+// ZS output planes:
+//   1. the haloed 6 x 10 x 192 input plane of h1 is prefetched into registers one plane
+//      ahead and committed to LDS (46 KB fp32);
+//   2. every thread owns two channels of one x column (768 threads = 96 channel pairs x 8
+//      columns; 12 waves, the register-file limit at ~160 VGPRs) and scatters each input row
+//      into the three output planes it feeds (rolling
+//      accumulators, packed v_pk_fma_f32 on the channel pair, the 27 weight pairs in
+//      registers): 27 FMAs per output and no re-reads of a plane;
+//   3. when an output plane is complete its 32 x 192 h2 tile goes to LDS (over the dead input
+//      plane); 16 lanes per position take the LayerNorm statistics, apply LN2 + GELU and
+//      rewrite the row in place as bf16 hi/lo halves (the split MFMA operand);
+//   4. six waves run the fc GEMM as 2 position tiles x 3 output-channel tiles of
+//      v_mfma_f32_16x16x32_bf16 (x3 for the fp32-faithful split), the fc weight hi/lo planes
+//      staged once per workgroup in LDS, and the epilogue adds bias + the Q4 residual and
+//      stores 16-byte rows.
+#include "kernels.hpp"
+
+namespace wf {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int C, int HID, int TY, int TX>
+struct DwFcCfg {
+  static constexpr int NTH = (HID / 2) * TX;        // one thread per (channel pair, column)
+  static constexpr int PY = TY + 2, PX = TX + 2, PP = PY * PX;
+  static constexpr int NPOS = TY * TX;
+  static constexpr int HS = HID + 4;                // h2 row stride in floats (bank spread)
+  static constexpr int WKP = HID + 8;               // fc weight row stride in bf16
+  static constexpr int PLANE_F = PP * HID;          // input plane floats
+  static constexpr int H2_F = NPOS * HS;
+  static constexpr int BUF_F = PLANE_F > H2_F ? PLANE_F : H2_F;
+  static constexpr int NV = HID / 4;                // 16-byte fp32 vectors per row
+  static constexpr int NLD = (PP * NV + NTH - 1) / NTH;
+  static constexpr int WAVES = NTH / 64;
+  static constexpr int RT = NPOS / 16, CT = C / 16;  // fc tiles
+  static constexpr int LN_LANES = 16;               // lanes per position for LN2
+  static constexpr int LN_CH = HID / LN_LANES;
+  static_assert(NTH % 64 == 0, "whole waves");
+  static_assert(RT * CT <= WAVES, "at most one fc tile per wave");
+  static_assert(NPOS * LN_LANES <= NTH, "LN2 lanes");
+  static_assert(LN_CH % 4 == 0, "LN2 vector width");
+  static constexpr size_t LDS_BYTES = (size_t)BUF_F * 4 + (size_t)2 * C * WKP * 2 +
+                                      (size_t)(2 * HID + C) * 4;
+};
+
+template <typename T>
+struct H1Load;
+template <>
+struct H1Load<float> {
+  typedef f32x4 raw;
+  static __device__ __forceinline__ raw load(const float* p, int64_t i) {
+    return *reinterpret_cast<const f32x4*>(p + i);
+  }
+  static __device__ __forceinline__ f32x4 up(raw u) { return u; }
+};
+template <>
+struct H1Load<uint16_t> {
+  typedef bf16x4 raw;
+  static __device__ __forceinline__ raw load(const uint16_t* p, int64_t i) {
+    return *reinterpret_cast<const bf16x4*>(p + i);
+  }
+  static __device__ __forceinline__ f32x4 up(raw u) {
+    return f32x4{bf2f((uint16_t)u[0]), bf2f((uint16_t)u[1]), bf2f((uint16_t)u[2]),
+                 bf2f((uint16_t)u[3])};
+  }
+};
+
+template <int C, int HID, int TY, int TX, bool SPLIT, typename T>
+__global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
+  typedef DwFcCfg<C, HID, TY, TX> K;
+  typedef H1Load<T> L;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* buf = lds;                                              // plane / h2 tile
+  uint16_t* wf = reinterpret_cast<uint16_t*>(lds + K::BUF_F);     // [2][C][WKP]
+  float* lnw = reinterpret_cast<float*>(wf + 2 * C * K::WKP);     // [HID]
+  float* lnb = lnw + HID;                                         // [HID]
+  float* fcb = lnb + HID;                                         // [C]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const int D = a.D, H = a.H, W = a.W;
+
+  // ---- tile of this workgroup (XCD-contiguous order: neighbouring tiles, which share halo
+  // rows of h1, run on the same XCD and meet in its L2)
+  const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY, nzs = (D + a.ZS - 1) / a.ZS;
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int xt = t % ntx;
+  t /= ntx;
+  const int yt = t % nty;
+  t /= nty;
+  const int zt = t % nzs;
+  const int b = t / nzs;
+  const int x0 = xt * TX, y0 = yt * TY, z0 = zt * a.ZS, z1 = min(z0 + a.ZS, D);
+
+  // ---- per-workgroup constants into LDS
+  for (int i = tid; i < 2 * C * (HID / 8); i += K::NTH) {
+    const int pl = i / (C * (HID / 8)), r = i % (C * (HID / 8));
+    const int n = r / (HID / 8), k8 = r % (HID / 8);
+    const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16x8 v = (SPLIT || pl == 0)
+                         ? *reinterpret_cast<const bf16x8*>(a.fc + ((size_t)pl * C + n) * HID + 8 * k8)
+                         : z8;
+    *reinterpret_cast<bf16x8*>(wf + ((size_t)pl * C + n) * K::WKP + 8 * k8) = v;
+  }
+  for (int i = tid; i < HID; i += K::NTH) {
+    lnw[i] = a.ln2_w[i];
+    lnb[i] = a.ln2_b[i];
+  }
+  for (int i = tid; i < C; i += K::NTH) fcb[i] = a.fc_b ? a.fc_b[i] : 0.f;
+
+  // ---- depthwise role: channel pair cp, column xi
+  const int cp = tid % (HID / 2), xi = tid / (HID / 2);
+  f32x2 w2[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k)
+    w2[k] = f32x2{a.dw_w[(2 * cp) * 27 + k], a.dw_w[(2 * cp + 1) * 27 + k]};
+  const f32x2 bias2 = f32x2{a.dw_b[2 * cp], a.dw_b[2 * cp + 1]};
+
+  // ---- h1 plane staging: item i -> (haloed position i / NV, 4-channel vector i % NV).  The
+  // in-plane offsets and the (y, x) validity of this thread's items are fixed for the whole
+  // z march; a plane is one scalar base + 32-bit offsets, the loads are unconditional (clamped)
+  // and the zero padding is applied at commit time, so nothing waits on them before then.
+  const T* src = reinterpret_cast<const T*>(a.h1) + (int64_t)b * D * H * W * HID;
+  const int64_t plane_elems = (int64_t)H * W * HID;
+  int off[K::NLD];
+  unsigned okmask = 0;
+#pragma unroll
+  for (int j = 0; j < K::NLD; ++j) {
+    const int i = min(j * K::NTH + tid, K::PP * K::NV - 1);
+    const int pos = i / K::NV, v = i - pos * K::NV;
+    const int yy = y0 - 1 + pos / K::PX, xx = x0 - 1 + pos % K::PX;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    const int yc = min(max(yy, 0), H - 1), xc = min(max(xx, 0), W - 1);
+    off[j] = (yc * W + xc) * HID + 4 * v;
+    okmask |= (ok ? 1u : 0u) << j;
+  }
+  typename L::raw stg[K::NLD];
+  auto fetch = [&](int p) {
+    const T* base = src + (int64_t)min(max(p, 0), D - 1) * plane_elems;
+#pragma unroll
+    for (int j = 0; j < K::NLD; ++j) stg[j] = L::load(base, off[j]);
+  };
+  auto commit = [&](int p) {
+    const bool pz = p >= 0 && p < D;
+#pragma unroll
+    for (int j = 0; j < K::NLD; ++j) {
+      const int i = j * K::NTH + tid;
+      const bool ok = pz && ((okmask >> j) & 1u);
+      const f32x4 u = L::up(stg[j]);
+      if (i < K::PP * K::NV)
+        *reinterpret_cast<f32x4*>(buf + (size_t)i * 4) = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  f32x2 accA[TY], accB[TY], accC[TY];
+#pragma unroll
+  for (int o = 0; o < TY; ++o) accA[o] = accB[o] = accC[o] = f32x2{0.f, 0.f};
+
+  // fc role of this wave: position tile rt, output-channel tile ct
+  const int rt = wid / K::CT, ct = wid % K::CT;
+  const int64_t plane_sz = (int64_t)H * W;
+
+  fetch(z0 - 1);
+  for (int p = z0 - 1; p <= z1; ++p) {
+    __syncthreads();  // previous plane's fc phase is done with buf
+    commit(p);
+    __syncthreads();
+    if (p + 1 <= z1) fetch(p + 1);  // next plane in flight behind this plane's work
+
+    // ---- scatter plane p into output planes p+1 (kz 0), p (kz 1), p-1 (kz 2)
+    {
+      const float* P = buf + xi * HID + 2 * cp;
+#pragma unroll
+      for (int r = 0; r < K::PY; ++r) {
+        const f32x2 v0 = *reinterpret_cast<const f32x2*>(P + (r * K::PX + 0) * HID);
+        const f32x2 v1 = *reinterpret_cast<const f32x2*>(P + (r * K::PX + 1) * HID);
+        const f32x2 v2 = *reinterpret_cast<const f32x2*>(P + (r * K::PX + 2) * HID);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int o = r - ky;
+          if (o < 0 || o >= TY) continue;
+          accC[o] += w2[ky * 3 + 0] * v0 + w2[ky * 3 + 1] * v1 + w2[ky * 3 + 2] * v2;
+          accB[o] += w2[9 + ky * 3 + 0] * v0 + w2[9 + ky * 3 + 1] * v1 + w2[9 + ky * 3 + 2] * v2;
+          accA[o] += w2[18 + ky * 3 + 0] * v0 + w2[18 + ky * 3 + 1] * v1 + w2[18 + ky * 3 + 2] * v2;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one input row in flight at a time (VGPRs)
+      }
+    }
+
+    const int zo = p - 1;  // output plane completed by this input plane
+    if (zo >= z0) {
+      __syncthreads();  // every thread is done reading the input plane
+      // ---- h2 tile (+ bias) into LDS: row = position o * TX + xi
+#pragma unroll
+      for (int o = 0; o < TY; ++o) {
+        f32x2 h = accA[o] + bias2;
+        if (sizeof(T) == 2) {  // bf16 mode: h2 carries bf16 rounding like the stored path
+          h.x = bf2f(f2bf(h.x));
+          h.y = bf2f(f2bf(h.y));
+        }
+        *reinterpret_cast<f32x2*>(buf + (o * TX + xi) * K::HS + 2 * cp) = h;
+      }
+      __syncthreads();
+      // ---- LN2 + GELU per position, rewritten in place as bf16 {hi[HID], lo[HID]}
+      if (tid < K::NPOS * K::LN_LANES) {
+        const int pos = tid / K::LN_LANES, g = tid % K::LN_LANES;
+        float* row = buf + pos * K::HS;
+        float v[K::LN_CH];
+#pragma unroll
+        for (int j = 0; j < K::LN_CH / 4; ++j) {
+          const f32x4 u = *reinterpret_cast<const f32x4*>(row + g * K::LN_CH + 4 * j);
+          v[4 * j] = u.x;
+          v[4 * j + 1] = u.y;
+          v[4 * j + 2] = u.z;
+          v[4 * j + 3] = u.w;
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < K::LN_CH; ++j) s += v[j];
+        const float mean = group_sum<K::LN_LANES>(s) * (1.f / HID);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < K::LN_CH; ++j) {
+          const float d = v[j] - mean;
+          q += d * d;
+        }
+        const float rstd = rsqrtf(group_sum<K::LN_LANES>(q) * (1.f / HID) + a.eps2);
+        uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
+#pragma unroll
+        for (int j = 0; j < K::LN_CH / 4; ++j) {
+          bf16x4 hi4, lo4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = g * K::LN_CH + 4 * j + e;
+            const float y = gelu_erf((v[4 * j + e] - mean) * rstd * lnw[c] + lnb[c]);
+            const uint16_t hb = f2bf(y);
+            hi4[e] = (short)hb;
+            lo4[e] = SPLIT ? (short)f2bf(y - bf2f(hb)) : (short)0;
+          }
+          *reinterpret_cast<bf16x4*>(rowh + g * K::LN_CH + 4 * j) = hi4;
+          if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + g * K::LN_CH + 4 * j) = lo4;
+        }
+      }
+      // residual inputs of this lane's epilogue row, in flight during the barrier + GEMM
+      const int lp = rt * 16 + l15;                 // tile position of this lane's row
+      const int yo = y0 + lp / TX, xo = x0 + lp % TX;
+      const bool rv = yo < H && xo < W;
+      const int64_t gpos = (int64_t)b * D * plane_sz + (int64_t)zo * plane_sz +
+                           (int64_t)min(yo, H - 1) * W + min(xo, W - 1);
+      const int col = ct * 16 + 4 * g4;
+      const f32x4 xr = *reinterpret_cast<const f32x4*>(a.x + gpos * C + col);
+      float smu = 0.f, srs = 1.f;
+      if (a.stats) {
+        smu = a.stats[2 * gpos];
+        srs = a.stats[2 * gpos + 1];
+      }
+      __syncthreads();
+      // ---- fc GEMM (waves 0 .. RT*CT-1): acc[i] = ffn[position lp][channel col + i]
+      if (wid < K::RT * K::CT) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const uint16_t* Bh = reinterpret_cast<const uint16_t*>(buf) + (size_t)lp * (2 * K::HS);
+      const uint16_t* Wh = wf + (size_t)(ct * 16 + l15) * K::WKP;
+#pragma unroll
+      for (int ks = 0; ks < HID / 32; ++ks) {
+        const int k = ks * 32 + 8 * g4;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bh + k);
+        const bf16x8 wh = *reinterpret_cast<const bf16x8*>(Wh + k);
+        if (SPLIT) {
+          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
+          const bf16x8 wl = *reinterpret_cast<const bf16x8*>(Wh + C * K::WKP + k);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, bh, acc, 0, 0, 0);
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bh, acc, 0, 0, 0);
+      }
+      // ---- epilogue: bias + Q4 residual, 16-byte store
+      f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+      const float bs = a.bscale ? a.bscale[b] : 1.f;
+      if (a.stats) {
+        const f32x4 lw = *reinterpret_cast<const f32x4*>(a.n2_w + col);
+        const f32x4 lb = *reinterpret_cast<const f32x4*>(a.n2_b + col);
+        const f32x4 n2 = (xr - smu) * srs * lw + lb;
+        v = xr + (n2 + v) * bs;
+      } else {
+        v = xr + v * bs;
+      }
+      if (rv) *reinterpret_cast<f32x4*>(a.out + gpos * C + col) = v;
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < TY; ++o) {
+      accA[o] = accB[o];
+      accB[o] = accC[o];
+      accC[o] = f32x2{0.f, 0.f};
+    }
+  }
+}
+
+int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s) {
+  constexpr int C = 48, HID = 192, TY = 4, TX = 8;
+  typedef DwFcCfg<C, HID, TY, TX> K;
+  DwFcArgs g = a;
+  // z segment: enough workgroups for ~4 rounds over the 256 CUs (1 workgroup per CU fits the
+  // LDS), but long enough that the two halo planes per segment stay a small overhead
+  const int64_t base = (int64_t)g.B * cdiv(g.H, TY) * cdiv(g.W, TX);
+  int ZS = g.D;
+  while (ZS > 8 && base * cdiv(g.D, ZS) < 1024) ZS = (ZS + 1) / 2;
+  g.ZS = ZS;
+  const int64_t blocks = base * cdiv(g.D, ZS);
+  void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_dwfc_kernel<C, HID, TY, TX, true, float>
+                                              : ffn_dwfc_kernel<C, HID, TY, TX, false, uint16_t>;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::LDS_BYTES);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(K::NTH), K::LDS_BYTES, s, g);
+  return check_launch("ffn_dwfc");
+}
+
+}  // namespace wf

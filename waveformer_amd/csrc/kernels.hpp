@@ -79,6 +79,26 @@ int launch_dwconv_ln_gelu(const void* in, const float* w, const float* b, const 
 int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, float* pstats,
                     int B, int Hd, int D, int H, int W, int prec, hipStream_t s);
 constexpr int DW_STAT_GROUP = 32;
+// ---- CCF_FFN back half fused (ffn_dwfc.hip): dwconv + bias + LN2 + GELU + fc + bias + the
+// Block's Q4 residual, for C = 48, hidden = 192 (h1 fp32 for PREC_SPLIT, bf16 for PREC_BF16)
+struct DwFcArgs {
+  const void* h1;        // (B, D, H, W, HID) fp32 (SPLIT) or bf16
+  const float* dw_w;     // (HID, 27)
+  const float* dw_b;     // (HID)
+  const float* ln2_w;    // (HID)
+  const float* ln2_b;
+  float eps2;
+  const uint16_t* fc;    // [2][C][HID] bf16 {hi, lo}
+  const float* fc_b;     // (C) or NULL
+  const float* x;        // (B, D, H, W, C) residual rows
+  const float* stats;    // (M, 2) {mean, rstd} of x for norm2, or NULL
+  const float* n2_w;
+  const float* n2_b;
+  const float* bscale;   // (B) or NULL
+  float* out;            // (B, D, H, W, C)
+  int B, D, H, W, ZS;
+};
+int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s);
 // K-chunked MFMA GEMM (gemm_kc.hip) for the shapes whose weight does not fit gemm_rows' LDS
 // in one column chunk; returns 1 if it took the shape
 int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s);

@@ -9,7 +9,7 @@
 //     `out /= count` (monai/inferers/utils.py:216-299).
 // The scatter of the reference becomes a gather: one thread per output voxel walks the windows
 // that cover it in ascending window order, so the fp32 sums are formed in exactly the
-// reference's order (explicit _rn intrinsics, no FMA contraction) with no atomics and one
+// reference's order (product and sum rounded separately, no FMA) with no atomics and one
 // write per output element.  The patches may come from an RCCL all-gather of round-robin
 // shards (see wf_sliding_window_stitch in include/waveformer_hip.h for the row mapping).
 #include "wf_common.hpp"
@@ -42,6 +42,10 @@ __device__ __forceinline__ void cover(const int* st, int n, int r, int p, int& l
 }
 
 __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
+  // hipcc contracts a*b+c into an FMA by default (also across the inlined __fmul_rn /
+  // __fadd_rn intrinsics); the reference rounds the product and the sum separately, so the
+  // arithmetic below uses plain operators under contract(off)
+#pragma clang fp contract(off)
   const int64_t total = (int64_t)a.B * a.D * a.H * a.W;
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
@@ -68,7 +72,7 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
       for (int ix = x0; ix <= x1; ++ix) {
         const int64_t loc = ((int64_t)(z - a.starts[0][iz]) * a.rh + (y - a.starts[1][iy])) * a.rw +
                             (x - a.starts[2][ix]);
-        cnt = __fadd_rn(cnt, a.map[loc]);
+        cnt = cnt + a.map[loc];
       }
 
   for (int c0 = 0; c0 < a.C; c0 += 4) {
@@ -89,7 +93,10 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
           const float* p = a.patches + (row * a.C + c0) * R3 + loc;
 #pragma unroll
           for (int c = 0; c < 4; ++c)
-            if (c < nc) acc[c] = __fadd_rn(acc[c], __fmul_rn(p[c * R3], w));
+            if (c < nc) {
+              const float prod = p[c * R3] * w;  // rounded on its own (no FMA)
+              acc[c] = acc[c] + prod;
+            }
         }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
