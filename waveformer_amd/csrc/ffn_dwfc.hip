@@ -10,15 +10,15 @@
 // h2 never touches HBM (the unfused path writes and re-reads 2 x 805 MB of it per stage-1
 // block at B = 4).  A workgroup owns a 4 x 8 (y, x) tile and marches z through a segment of
 // ZS output planes:
-//   1. the haloed 6 x 10 x 192 input plane of h1 is prefetched into registers one plane
-//      ahead and committed to LDS (46 KB fp32);
+//   1. the haloed 6 x 10 x 192 input plane of h1 is prefetched into registers two planes
+//      ahead and committed to a double-buffered LDS plane (2 x 46 KB fp32) one plane ahead;
 //   2. every thread owns two channels of one x column (768 threads = 96 channel pairs x 8
 //      columns; 12 waves, the register-file limit at ~160 VGPRs) and scatters each input row
 //      into the three output planes it feeds (rolling
 //      accumulators, packed v_pk_fma_f32 on the channel pair, the 27 weight pairs in
 //      registers): 27 FMAs per output and no re-reads of a plane;
-//   3. when an output plane is complete its 32 x 192 h2 tile goes to LDS (over the dead input
-//      plane); 16 lanes per position take the LayerNorm statistics, apply LN2 + GELU and
+//   3. when an output plane is complete its 32 x 192 h2 tile goes to LDS (25 KB);
+//      16 lanes per position take the LayerNorm statistics, apply LN2 + GELU (packed) and
 //      rewrite the row in place as bf16 hi/lo halves (the split MFMA operand);
 //   4. six waves run the fc GEMM as 2 position tiles x 3 output-channel tiles of
 //      v_mfma_f32_16x16x32_bf16 (x3 for the fp32-faithful split), the fc weight hi/lo planes
@@ -27,8 +27,6 @@
 #include "kernels.hpp"
 
 namespace wf {
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int C, int HID, int TY, int TX>
 struct DwFcCfg {
@@ -39,7 +37,7 @@ struct DwFcCfg {
   static constexpr int WKP = HID + 8;               // fc weight row stride in bf16
   static constexpr int PLANE_F = PP * HID;          // input plane floats
   static constexpr int H2_F = NPOS * HS;
-  static constexpr int BUF_F = PLANE_F > H2_F ? PLANE_F : H2_F;
+  static constexpr int BUF_F = 2 * PLANE_F + H2_F;  // double-buffered plane + h2 tile
   static constexpr int NV = HID / 4;                // 16-byte fp32 vectors per row
   static constexpr int NLD = (PP * NV + NTH - 1) / NTH;
   static constexpr int WAVES = NTH / 64;
@@ -77,11 +75,12 @@ struct H1Load<uint16_t> {
 };
 
 template <int C, int HID, int TY, int TX, bool SPLIT, typename T>
-__global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
+__global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_kernel(DwFcArgs a) {
   typedef DwFcCfg<C, HID, TY, TX> K;
   typedef H1Load<T> L;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* buf = lds;                                              // plane / h2 tile
+  float* planes = lds;                                           // [2][PP][HID]
+  float* h2t = lds + 2 * K::PLANE_F;                              // [NPOS][HS]
   uint16_t* wf = reinterpret_cast<uint16_t*>(lds + K::BUF_F);     // [2][C][WKP]
   float* lnw = reinterpret_cast<float*>(wf + 2 * C * K::WKP);     // [HID]
   float* lnb = lnw + HID;                                         // [HID]
@@ -154,7 +153,7 @@ __global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
 #pragma unroll
     for (int j = 0; j < K::NLD; ++j) stg[j] = L::load(base, off[j]);
   };
-  auto commit = [&](int p) {
+  auto commit = [&](int p, float* dst) {
     const bool pz = p >= 0 && p < D;
 #pragma unroll
     for (int j = 0; j < K::NLD; ++j) {
@@ -162,7 +161,7 @@ __global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
       const bool ok = pz && ((okmask >> j) & 1u);
       const f32x4 u = L::up(stg[j]);
       if (i < K::PP * K::NV)
-        *reinterpret_cast<f32x4*>(buf + (size_t)i * 4) = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(dst + (size_t)i * 4) = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
 
@@ -174,16 +173,19 @@ __global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
   const int rt = wid / K::CT, ct = wid % K::CT;
   const int64_t plane_sz = (int64_t)H * W;
 
+  // Schedule per input plane p (3 barriers): scatter(p) | C | commit(p+1) into the other plane
+  // buffer, fetch(p+2), h2 tile of output p-1 | A | LN2 + GELU in place | B | fc + store.
+  // Waves without an fc tile run ahead into the next plane's scatter while the fc runs.
   fetch(z0 - 1);
+  commit(z0 - 1, planes);
+  fetch(z0);
+  __syncthreads();
   for (int p = z0 - 1; p <= z1; ++p) {
-    __syncthreads();  // previous plane's fc phase is done with buf
-    commit(p);
-    __syncthreads();
-    if (p + 1 <= z1) fetch(p + 1);  // next plane in flight behind this plane's work
-
+    const float* cur = planes + ((p - z0 + 1) & 1) * K::PLANE_F;
+    float* nxt = planes + ((p - z0) & 1) * K::PLANE_F;
     // ---- scatter plane p into output planes p+1 (kz 0), p (kz 1), p-1 (kz 2)
     {
-      const float* P = buf + xi * HID + 2 * cp;
+      const float* P = cur + xi * HID + 2 * cp;
 #pragma unroll
       for (int r = 0; r < K::PY; ++r) {
         const f32x2 v0 = *reinterpret_cast<const f32x2*>(P + (r * K::PX + 0) * HID);
@@ -202,8 +204,10 @@ __global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
     }
 
     const int zo = p - 1;  // output plane completed by this input plane
+    __syncthreads();  // C: scatter(p) done everywhere (nxt is free), fc(p-2) done (h2t is free)
+    if (p + 1 <= z1) commit(p + 1, nxt);
+    if (p + 2 <= z1) fetch(p + 2);  // in flight behind the next plane's work
     if (zo >= z0) {
-      __syncthreads();  // every thread is done reading the input plane
       // ---- h2 tile (+ bias) into LDS: row = position o * TX + xi
 #pragma unroll
       for (int o = 0; o < TY; ++o) {
@@ -212,13 +216,15 @@ __global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
           h.x = bf2f(f2bf(h.x));
           h.y = bf2f(f2bf(h.y));
         }
-        *reinterpret_cast<f32x2*>(buf + (o * TX + xi) * K::HS + 2 * cp) = h;
+        *reinterpret_cast<f32x2*>(h2t + (o * TX + xi) * K::HS + 2 * cp) = h;
       }
-      __syncthreads();
+    }
+    __syncthreads();  // A: h2 tile and plane p+1 visible
+    if (zo >= z0) {
       // ---- LN2 + GELU per position, rewritten in place as bf16 {hi[HID], lo[HID]}
       if (tid < K::NPOS * K::LN_LANES) {
         const int pos = tid / K::LN_LANES, g = tid % K::LN_LANES;
-        float* row = buf + pos * K::HS;
+        float* row = h2t + pos * K::HS;
         float v[K::LN_CH];
 #pragma unroll
         for (int j = 0; j < K::LN_CH / 4; ++j) {
@@ -242,17 +248,23 @@ __global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
         uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
 #pragma unroll
         for (int j = 0; j < K::LN_CH / 4; ++j) {
+          const int c = g * K::LN_CH + 4 * j;
+          const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + c);
+          const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + c);
+          const f32x2 y0 = gelu_erf2((f32x2{v[4 * j], v[4 * j + 1]} - mean) * rstd *
+                                         f32x2{lw4.x, lw4.y} + f32x2{lb4.x, lb4.y});
+          const f32x2 y1 = gelu_erf2((f32x2{v[4 * j + 2], v[4 * j + 3]} - mean) * rstd *
+                                         f32x2{lw4.z, lw4.w} + f32x2{lb4.z, lb4.w});
+          const float y[4] = {y0.x, y0.y, y1.x, y1.y};
           bf16x4 hi4, lo4;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int c = g * K::LN_CH + 4 * j + e;
-            const float y = gelu_erf((v[4 * j + e] - mean) * rstd * lnw[c] + lnb[c]);
-            const uint16_t hb = f2bf(y);
+            const uint16_t hb = f2bf(y[e]);
             hi4[e] = (short)hb;
-            lo4[e] = SPLIT ? (short)f2bf(y - bf2f(hb)) : (short)0;
+            lo4[e] = SPLIT ? (short)f2bf(y[e] - bf2f(hb)) : (short)0;
           }
-          *reinterpret_cast<bf16x4*>(rowh + g * K::LN_CH + 4 * j) = hi4;
-          if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + g * K::LN_CH + 4 * j) = lo4;
+          *reinterpret_cast<bf16x4*>(rowh + c) = hi4;
+          if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + c) = lo4;
         }
       }
       // residual inputs of this lane's epilogue row, in flight during the barrier + GEMM
@@ -262,17 +274,21 @@ __global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
       const int64_t gpos = (int64_t)b * D * plane_sz + (int64_t)zo * plane_sz +
                            (int64_t)min(yo, H - 1) * W + min(xo, W - 1);
       const int col = ct * 16 + 4 * g4;
-      const f32x4 xr = *reinterpret_cast<const f32x4*>(a.x + gpos * C + col);
+      const bool fcw = wid < K::RT * K::CT;  // this wave owns an fc tile
+      f32x4 xr = f32x4{0.f, 0.f, 0.f, 0.f};
       float smu = 0.f, srs = 1.f;
-      if (a.stats) {
-        smu = a.stats[2 * gpos];
-        srs = a.stats[2 * gpos + 1];
+      if (fcw) {
+        xr = *reinterpret_cast<const f32x4*>(a.x + gpos * C + col);
+        if (a.stats) {
+          smu = a.stats[2 * gpos];
+          srs = a.stats[2 * gpos + 1];
+        }
       }
-      __syncthreads();
+      __syncthreads();  // B: LN2 + GELU rows visible
       // ---- fc GEMM (waves 0 .. RT*CT-1): acc[i] = ffn[position lp][channel col + i]
-      if (wid < K::RT * K::CT) {
+      if (fcw) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      const uint16_t* Bh = reinterpret_cast<const uint16_t*>(buf) + (size_t)lp * (2 * K::HS);
+      const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)lp * (2 * K::HS);
       const uint16_t* Wh = wf + (size_t)(ct * 16 + l15) * K::WKP;
 #pragma unroll
       for (int ks = 0; ks < HID / 32; ++ks) {
@@ -310,15 +326,16 @@ __global__ __launch_bounds__((HID / 2) * TX) void ffn_dwfc_kernel(DwFcArgs a) {
   }
 }
 
-int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s) {
-  constexpr int C = 48, HID = 192, TY = 4, TX = 8;
+template <int TY, int TX>
+static int go_dwfc(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks) {
+  constexpr int C = 48, HID = 192;
   typedef DwFcCfg<C, HID, TY, TX> K;
   DwFcArgs g = a;
-  // z segment: enough workgroups for ~4 rounds over the 256 CUs (1 workgroup per CU fits the
-  // LDS), but long enough that the two halo planes per segment stay a small overhead
+  // z segment: enough workgroups for a few rounds over the CUs, but long enough that the two
+  // halo planes per segment stay a small overhead
   const int64_t base = (int64_t)g.B * cdiv(g.H, TY) * cdiv(g.W, TX);
   int ZS = g.D;
-  while (ZS > 8 && base * cdiv(g.D, ZS) < 1024) ZS = (ZS + 1) / 2;
+  while (ZS > 8 && base * cdiv(g.D, ZS) < min_blocks) ZS = (ZS + 1) / 2;
   g.ZS = ZS;
   const int64_t blocks = base * cdiv(g.D, ZS);
   void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_dwfc_kernel<C, HID, TY, TX, true, float>
@@ -327,6 +344,12 @@ int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::LDS_BYTES);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(K::NTH), K::LDS_BYTES, s, g);
   return check_launch("ffn_dwfc");
+}
+
+int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s) {
+  // 4 x 8 tiles: 12 waves (the register-file limit at ~168 VGPRs) and ~154 KB of LDS, one
+  // workgroup per CU.  (4 x 4 tiles with two 6-wave workgroups per CU measured 1.5x slower.)
+  return go_dwfc<4, 8>(a, prec, s, 1024);
 }
 
 }  // namespace wf

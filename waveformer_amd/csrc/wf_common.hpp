@@ -58,6 +58,24 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return fmaf(hx, copysignf(erfa, x), hx);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// gelu_erf on a pair: the same arithmetic, the FMA-class steps as packed v_pk_*_f32 ops
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 u = f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752f;
+  const f32x2 d = u * 0.3275911f + 1.0f;
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = t * 1.061405429f + -1.453152027f;
+  p = t * p + 1.421413741f;
+  p = t * p + -0.284496736f;
+  p = t * p + 0.254829592f;
+  p = p * t;
+  const f32x2 q = (x * x) * -0.72134752044448170f;
+  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  const f32x2 erfa = 1.0f - p * e;
+  const f32x2 hx = 0.5f * x;
+  return hx * f32x2{copysignf(erfa.x, x.x), copysignf(erfa.y, x.y)} + hx;
+}
+
 // ---------------------------------------------------------------------------------------
 // sub-wave reductions: a "row group" is G consecutive lanes (G a power of two <= 64)
 // ---------------------------------------------------------------------------------------
