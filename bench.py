@@ -59,10 +59,11 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--parity", type=int, default=1)
     ap.add_argument("--img", type=int, default=128)
-    ap.add_argument("--workload", default="encoder", choices=["encoder", "sliding"],
+    ap.add_argument("--workload", default="encoder", choices=["encoder", "sliding", "train"],
                     help="encoder: config 2 (the driver's line); sliding: config 3, one "
                          "240x240x155x4 case through the full Waveformer with the windows "
-                         "sharded over the ranks and all-gathered over RCCL")
+                         "sharded over the ranks and all-gathered over RCCL; train: config 4, "
+                         "fwd + DiceCE + bwd + clip + AdamW of the full Waveformer, DDP")
     ap.add_argument("--tta", type=int, default=0, help="sliding: 8-way flip TTA")
     return ap.parse_args()
 
@@ -307,6 +308,82 @@ def main_sliding(args, world, rank, dev):
         dist.destroy_process_group()
 
 
+def main_train(args, world, rank, dev):
+    """Config 4: one training step of the full Waveformer on 128^3 x 4 random crops, per GPU
+    batch args.batch, as BraTSTrainer does it (3_train.py:96-102, trainer.py:458-466):
+    DiceCE(to_onehot_y, softmax) -> backward -> clip_grad_norm_(12) -> AdamW(1e-4).  N > 1: DDP
+    over RCCL (bucketed all-reduce of the fp32 gradients, overlapped with the backward).
+    Encoder forward = HIP kernels (bf16x3 MFMA), encoder backward = HIP kernels + hipBLASLt
+    fp32 GEMM gradients, decoder convolutions = MIOpen (as in the reference)."""
+    import waveformer_amd.network_models as NM
+    from waveformer_amd.losses import DiceCELoss
+    torch.manual_seed(0)
+    model = NM.Waveformer(img_size=(args.img,) * 3, in_chans=4, out_chans=4,
+                          depths=[2, 2, 2, 2], feat_size=[48, 96, 192, 384],
+                          num_heads=[3, 6, 12, 24]).train().to(dev)
+    ddp = model
+    if world > 1:
+        ddp = torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[dev.index], bucket_cap_mb=64, gradient_as_bucket_view=True)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4)
+    loss_fn = DiceCELoss(to_onehot_y=True, softmax=True)
+    g = torch.Generator(device=dev).manual_seed(1 + rank)
+    x = torch.randn(args.batch, 4, args.img, args.img, args.img, device=dev, generator=g)
+    y = torch.randint(0, 4, (args.batch, 1, args.img, args.img, args.img), device=dev,
+                      generator=g)
+    losses = []
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = loss_fn(ddp(x), y)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 12)
+        opt.step()
+        return loss
+
+    for i in range(max(1, args.warmup)):
+        t1 = time.perf_counter()
+        losses.append(step().item())
+        print(f"[bench] warm-up step {i}: {time.perf_counter() - t1:.2f} s "
+              f"(loss {losses[-1]:.4f})", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        last = step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    losses.append(last.item())
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    if rank == 0:
+        vols = args.batch * args.steps * world
+        out = {
+            "metric": "128^3x4 volumes/sec train step (fwd + DiceCE + bwd + AdamW), config 4",
+            "value": vols / dt, "unit": "volumes/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32 (bf16x3 MFMA forward, fp32 backward)",
+            "data": "synthetic: randn 128^3x4 crops + randint(0,4) labels resident in HBM, "
+                    "reference-init random weights",
+            "config": {"workload": f"Waveformer {args.img}^3x4 train step, DiceCE, AdamW 1e-4, "
+                                   f"clip 12", "global_batch": args.batch * world,
+                       "per_gpu_batch": args.batch,
+                       "parallelism": f"DDP x{world} (RCCL all-reduce)" if world > 1 else "x1"},
+            "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -321,6 +398,8 @@ def main():
     ops.set_precision(args.precision)
     if args.workload == "sliding":
         return main_sliding(args, world, rank, dev)
+    if args.workload == "train":
+        return main_train(args, world, rank, dev)
 
     model = build_encoder(args.img, dev)
     x = torch.randn(args.batch, 4, args.img, args.img, args.img, device=dev,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 4
+#define WF_ABI_VERSION 5
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1 };
 
@@ -159,7 +159,9 @@ int wf_ccf_ffn_fwd(const float* xh, const float* stats, const float* n2_w, const
 /* The same three launches one at a time (stage 1: pwconv GEMM -> workspace h1; 2: depthwise
  * conv h1 -> h2 + per-32-channel LayerNorm partials; 3: LN2 + GELU + fc GEMM + residuals ->
  * out), with the same arguments; stage 0 runs all three (== wf_ccf_ffn_fwd).  Lets a caller
- * time or interleave the stages.                                                           */
+ * time or interleave the stages.  stage | 16 (training) forces the staged kernels for every
+ * shape, so that on return the workspace holds h1 = GELU(LN1(pwconv(n))) at offset 0 and
+ * h2 = dwconv(h1) + dw_b (before LN2) at the next 256-B boundary, both fp32 (WF_PREC_BF16X3). */
 int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats, const float* n2_w,
                      const float* n2_b, const uint16_t* pw_bf16x2, const float* pw_b,
                      const float* ln1_w, const float* ln1_b, float eps1, const float* dw_w,
@@ -221,6 +223,111 @@ int wf_sliding_window_stitch(const float* patches, int64_t world, int64_t slots_
  * out: (C, D, H, W) fp32.                                                                    */
 int wf_tta_merge(const float* pred, const int* flips, int npass, float* out, int64_t C,
                  int64_t D, int64_t H, int64_t W, void* stream);
+
+/* ======================================================================================
+ * Training (config 4: fwd + bwd DiceCE on 128^3 x 4 crops, DDP).  The reference trains with
+ * PyTorch autograd through the modules of SURVEY 8a (3_train.py:99-135, trainer.py:454); these
+ * entry points are the backward halves of the forward ops above, plus the few gather/reduce
+ * primitives the Python autograd.Functions need.  Dense GEMM gradients are left to the
+ * caller's BLAS (hipBLASLt).  All fp32.  Reductions are two-pass (partials + a final pass),
+ * so results are deterministic run to run; scratch is caller-owned as elsewhere.
+ * ====================================================================================== */
+
+/* Attention forward that also writes the per-row log-sum-exp of the softmax, in the log2
+ * domain: lse[(bw * heads + h) * N + q] = log2 sum_k exp2(S'_qk), S' = (scale q.k + bias) log2 e.
+ * Same arguments as wf_window_attention_fwd otherwise; the workspace (qkv, then the
+ * attention output o at the next 256-B boundary) is what the backward consumes.            */
+int wf_window_attention_fwd_train(const float* x, const float* ln_w, const float* ln_b,
+                                  float ln_eps, const uint16_t* wqkv_bf16x2, const float* bqkv,
+                                  const float* bias, const uint16_t* wproj_bf16x2,
+                                  const float* bproj, float* out, void* workspace, float* lse,
+                                  int64_t B, int64_t C, int64_t D1, int64_t H1, int64_t W1,
+                                  int64_t ws, int64_t heads, float scale, int precision,
+                                  void* stream);
+
+/* Backward of softmax(scale q k^T + bias) v per window and head (attention.py:92-101).
+ * qkv (B*nW*N, 3C) and o (B*nW*N, C) window-major fp32 as saved by the forward, dout the
+ * gradient of o (window-major), lse from wf_window_attention_fwd_train.
+ * dqkv: (B*D1*H1*W1, 3C) in RASTER row order (the inverse of window_partition,
+ * wave_helper.py:450-461), so the qkv weight gradient pairs it with the un-permuted input.
+ * dbias: (heads, N, N), the bias gradient summed over all windows.  Both are zeroed here.
+ * head_dim in {16, 32, 48, 64}.                                                             */
+int wf_window_attention_bwd_core(const float* qkv, const float* o, const float* dout,
+                                 const float* bias, const float* lse, float* dqkv, float* dbias,
+                                 int64_t B, int64_t C, int64_t D1, int64_t H1, int64_t W1,
+                                 int64_t ws, int64_t heads, float scale, void* stream);
+
+/* dtable[index[i][j]][h] += dbias[h][i][j] (the gather at attention.py:94-97, adjoint);
+ * dtable (table_rows, heads) is zeroed first.                                               */
+int wf_rel_pos_bias_bwd(const float* dbias, const int64_t* index, float* dtable, int64_t N,
+                        int64_t heads, int64_t table_rows, void* stream);
+
+/* out[c] = sum_r in[r][c] * (row_scale ? row_scale[r / rows_per_scale] : 1): bias gradients.
+ * partials: wf_colsum_parts(R) * N floats.                                                  */
+int64_t wf_colsum_parts(int64_t R);
+int wf_colsum(const float* in, int64_t R, int64_t N, const float* row_scale,
+              int64_t rows_per_scale, float* partials, float* out, void* stream);
+
+/* y = GELU?(LayerNorm(x)) over rows of N <= 1536 (w == NULL: no affine).  The LN -> GELU pairs
+ * of CCF_FFN (wave_helper.py:278-286), Block.norm1/norm2, PatchMerging.norm and proj_out.    */
+int wf_ln_act_fwd(const float* x, const float* w, const float* b, float eps, int gelu, float* y,
+                  int64_t M, int64_t N, void* stream);
+/* Backward of wf_ln_act_fwd: dx = [dadd +] dLN(dy * GELU'(z)); dw / db (when w != NULL) the
+ * affine gradients.  partials: wf_ln_bwd_workspace_floats(M, N) floats.                     */
+int64_t wf_ln_bwd_workspace_floats(int64_t M, int64_t N);
+int wf_ln_act_bwd(const float* x, const float* w, const float* b, float eps, int gelu,
+                  const float* dy, const float* dadd, float* dx, float* partials, float* dw,
+                  float* db, int64_t M, int64_t N, void* stream);
+
+/* Adjoint of wf_dwt3d_haar_fwd (without its fused LayerNorm): dx (B, D, H, W, C) channel-last
+ * from the 8 band gradients dband[k] (NULL = zero), element (b, z, y, x, c) of band k at
+ * dband[k][b*s[5k] + z*s[5k+1] + y*s[5k+2] + x*s[5k+3] + c*s[5k+4]].                        */
+int wf_dwt3d_haar_bwd(const float* const* dband, const int64_t* strides, float* dx, int64_t B,
+                      int64_t C, int64_t D, int64_t H, int64_t W, void* stream);
+
+/* One Haar analysis level of an NCDHW tensor (the adjoint of one wf_idwt3d_haar level):
+ * in (B, C, 2d, 2h, 2w), element (b, c, ...) at in + b*in_bstride + c*in_cstride, spatially
+ * contiguous.  ll: (B, C, d, h, w) contiguous; det[k] (k = 0..6, key 'aad'..'ddd') element
+ * (b, c, z, y, x) at det[k][b*s[0] + c*s[1] + z*s[2] + y*s[3] + x*s[4]].                    */
+int wf_haar_analysis_ncdhw(const float* in, int64_t in_bstride, int64_t in_cstride, float* ll,
+                           float* const* det, const int64_t* det_strides, int64_t B, int64_t C,
+                           int64_t d, int64_t h, int64_t w, void* stream);
+
+/* Adjoint of F.interpolate(trilinear, align_corners=False) along one axis
+ * (wave_helper.py:500): in (outer, Lout, inner) -> out (outer, Lin, inner), optionally times
+ * outer_scale[o / outer_per_scale] (the DropPath factor of the attention branch).           */
+int wf_interp_adjoint_axis(const float* in, float* out, int64_t outer, int64_t Lout,
+                           int64_t Lin, int64_t inner, const float* outer_scale,
+                           int64_t outer_per_scale, void* stream);
+
+/* Depthwise 3^3 conv, channel-last, padding 1 (CCF_FFN.dwconv, wave_helper.py:285):
+ * w (C, 27), bias (C) or NULL; flip != 0 convolves with the flipped kernel (the input
+ * gradient).  C % 4 == 0.                                                                  */
+int wf_dwconv3d_cl(const float* in, const float* w, const float* bias, int flip, float* out,
+                   int64_t B, int64_t C, int64_t D, int64_t H, int64_t W, void* stream);
+/* dw (C, 27) = sum over positions of dy[pos][c] x[pos + offset_k][c].
+ * partials: wf_dwconv_wgrad_ws_floats(B*D*H*W, C) floats.                                  */
+int64_t wf_dwconv_wgrad_ws_floats(int64_t positions, int64_t C);
+int wf_dwconv3d_wgrad(const float* dy, const float* x, float* partials, float* dw, int64_t B,
+                      int64_t C, int64_t D, int64_t H, int64_t W, void* stream);
+
+/* PatchMerging's 8-way sub-lattice gather (wave_helper.py:183-191, Q3 duplicates; v2 = the
+ * itertools.product order of :154-156): merged (B, D/2, H/2, W/2, 8C).  The scatter is its
+ * adjoint: dx sums every slot a position was gathered into (0, 1 or 2 under Q3).           */
+int wf_patch_merging_gather(const float* x, int v2, float* merged, int64_t B, int64_t C,
+                            int64_t D, int64_t H, int64_t W, void* stream);
+int wf_patch_merging_scatter(const float* dmerged, int v2, float* dx, int64_t B, int64_t C,
+                             int64_t D, int64_t H, int64_t W, void* stream);
+
+/* PatchEmbed patches (patchembedding.py:214, Conv3d k=2 s=2): x NCDHW (B, Cin, 2D, 2H, 2W)
+ * <-> rows (B*D*H*W, Cin*8) in the flattened weight order (ci, kz, ky, kx); dir 0 gathers x
+ * into rows, dir 1 scatters rows into x.                                                    */
+int wf_patchify(float* x, float* rows, int dir, int64_t B, int64_t Cin, int64_t D, int64_t H,
+                int64_t W, void* stream);
+
+/* (B, C, S) -> (B, S, C): the NCDHW -> channel-last transpose (proj_out's adjoint,
+ * waveformer.py:289).                                                                       */
+int wf_transpose_cs(const float* in, float* out, int64_t B, int64_t C, int64_t S, void* stream);
 
 #ifdef __cplusplus
 }

@@ -192,3 +192,73 @@ def flatten_output(case: Case, out) -> Dict[str, torch.Tensor]:
                 for k, v in d.items():
                     res[f"{n}_hf{s}_{li}_{k}"] = v
     return res
+
+
+# ------------------------------------------------------------------------------------------
+# gradient cases (config 4's backward; tests/golden/gen_reference_fixtures.py::_grads)
+# ------------------------------------------------------------------------------------------
+def grad_loss(outs):
+    """sum_k <out_k, R_k>, R_k = seeded_randn(out_k.shape, 900 + k) -- the generator's loss."""
+    tot = 0.0
+    for k, t in enumerate(outs):
+        r = seeded_randn(tuple(t.shape), 900 + k).to(t.device)
+        tot = tot + (t * r).sum()
+    return tot
+
+
+def flat_outputs(r):
+    """The generator's flat_outputs: main output, then detail tensors (level-major, key order)."""
+    if isinstance(r, torch.Tensor):
+        return [r]
+    a, b = r
+    if isinstance(a, torch.Tensor):
+        return [a] + [d[k] for d in b for k in sorted(d)]
+    return list(a) + [d[k] for h in b for d in h for k in sorted(d)]
+
+
+@dataclass
+class GradCase:
+    name: str
+    ctor: Callable[[], nn.Module]
+    input_shape: tuple
+    seed: int
+    oracle: Callable  # (sd, x) -> output
+    full: bool        # every parameter gradient stored in full (else a summary triple)
+
+
+def grad_cases() -> Dict[str, GradCase]:
+    import waveformer_amd.network_models as NM
+    base = cases()
+    c: Dict[str, GradCase] = {}
+    for n in ("attn_ws8", "attn_ws4_h2", "block_l3", "block_l1", "block_l0", "block_ss_l2",
+              "merge", "ccf_ffn"):
+        k = base[n]
+        c[n] = GradCase(n, k.ctor, k.input_shape, k.seed, k.oracle, True)
+    c["enc32h"] = GradCase("enc32h", partial(NM.MultiscaleTransformer, img_size=(32,) * 3,
+                                             in_chans=4, qkv_bias=True, norm_layer=_ln6()),
+                           (1, 4, 32, 32, 32), 24,
+                           lambda sd, x: R.encoder(sd, x, heads=[3, 6, 12, 24], depths=[2] * 4),
+                           False)
+    k = base["full32"]
+    c["full32"] = GradCase("full32", k.ctor, k.input_shape, k.seed, k.oracle, False)
+    return c
+
+
+def grad_summary(gr: torch.Tensor) -> torch.Tensor:
+    g = gr.detach().double().cpu().reshape(-1)
+    r = seeded_randn(tuple(gr.shape), 777).double().reshape(-1)
+    return torch.tensor([g.sum().item(), (g * g).sum().item(), (g * r).sum().item()],
+                        dtype=torch.float64)
+
+
+def oracle_grads(case: GradCase, sd, x):
+    """d grad_loss / d (x, every floating state_dict entry) through the oracle on the CPU."""
+    sdg = {k: (v.detach().clone().requires_grad_(True) if v.is_floating_point() else v)
+           for k, v in sd.items()}
+    xg = x.detach().clone().requires_grad_(True)
+    grad_loss(flat_outputs(case.oracle(sdg, xg))).backward()
+    res = {"x": xg.grad}
+    for k, v in sdg.items():
+        if v.is_floating_point() and v.grad is not None:
+            res[k] = v.grad
+    return res

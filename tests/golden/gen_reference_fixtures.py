@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--reference", default="/root/reference")
     ap.add_argument("--skip-128", action="store_true")
     ap.add_argument("--groups", default="small,128",
-                    help="comma list of: small, 128, hf32, 192.  Arrays of groups not listed "
+                    help="comma list of: small, grad, loss, 128, hf32, 192.  Arrays of groups not listed "
                          "are kept from the existing ref_fixtures.npz")
     args = ap.parse_args()
     groups = set(args.groups.split(","))
@@ -125,6 +125,22 @@ def main():
         net = apply_rule(Waveformer(img_size=(32,) * 3, in_chans=4, out_chans=4,
                                     network_config={"transformer": {"hf_refinement": True}})).eval()
         _full("full32hf", net(seeded_randn((1, 4, 32, 32, 32), 23)), out)
+    if "grad" in groups:
+        with torch.enable_grad():
+            _grads(out, ln6, Attention, Block, CCF_FFN, MultiscaleTransformer, PatchMerging,
+                   Waveformer)
+    if "loss" in groups:
+        # 3_train.py:72 DiceCELoss(to_onehot_y=True, softmax=True) (vendored MONAI): value and
+        # logits gradient on a seeded (2, 4, 8, 8, 8) batch
+        from monai.losses import DiceCELoss
+        with torch.enable_grad():
+            logits = seeded_randn((2, 4, 8, 8, 8), 30).requires_grad_(True)
+            lab = torch.randint(0, 4, (2, 1, 8, 8, 8), generator=torch.Generator().manual_seed(31))
+            loss = DiceCELoss(to_onehot_y=True, softmax=True)(logits, lab)
+            loss.backward()
+        out["dicece__labels"] = lab.to(torch.uint8).numpy()
+        out["dicece__loss"] = np.array([loss.item()])
+        out["dicece__grad"] = logits.grad.numpy()
     if "128" in groups:
         _big128(out, ln6, MultiscaleTransformer, Waveformer)
     if "192" in groups:
@@ -208,6 +224,70 @@ def _small(out, ln6, Attention, Block, CCF_FFN, MultiscaleTransformer, PatchMerg
         spec = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()]
         out[tag + "__keys"] = np.frombuffer(json.dumps(spec).encode(), dtype=np.uint8)
 
+
+
+def grad_loss(outs):
+    """The scalar every gradient fixture differentiates: sum_k <out_k, R_k>, R_k a seeded
+    normal cotangent of out_k's shape (seed 900 + k), outputs in the flattened order of
+    flat_outputs()."""
+    tot = 0.0
+    for k, t in enumerate(outs):
+        tot = tot + (t * seeded_randn(tuple(t.shape), 900 + k)).sum()
+    return tot
+
+
+def flat_outputs(r):
+    """module output -> list of tensors: the main output, then the detail dicts' tensors
+    (level-major, ptwt key order) for Blocks; stage outputs then details for the encoder."""
+    if isinstance(r, torch.Tensor):
+        return [r]
+    a, b = r
+    if isinstance(a, torch.Tensor):  # Block: (out, tuple of dicts)
+        return [a] + [d[k] for d in b for k in sorted(d)]
+    return list(a) + [d[k] for h in b for d in h for k in sorted(d)]  # encoder
+
+
+def _grads(out, ln6, Attention, Block, CCF_FFN, MultiscaleTransformer, PatchMerging,
+           Waveformer):
+    """Gradient fixtures (config 4's backward): d grad_loss / d input and / d every parameter
+    of the reference modules (eval mode, rule weights).  Small modules keep every gradient;
+    full32 keeps the input gradient plus a (sum, sum of squares, seeded dot) triple per
+    parameter."""
+    t0 = time.time()
+    cases = []
+    for name, dim, heads, ws, B_ in (("attn_ws8", 48, 3, 8, 1), ("attn_ws4_h2", 32, 2, 4, 3)):
+        cases.append((name, Attention(dim, num_heads=heads, qkv_bias=True, window_size=ws),
+                      (B_, ws ** 3, dim), 11, True))
+    for name, dim, heads, level, img, ms, B in (
+            ("block_l3", 32, 2, 3, 16, True, 1), ("block_l1", 32, 2, 1, 16, True, 1),
+            ("block_l0", 32, 2, 0, 8, True, 2), ("block_ss_l2", 32, 2, 2, 16, False, 1)):
+        cases.append((name, Block(dim, heads, qkv_bias=True, norm_layer=ln6, level=level,
+                                  ms_attention=ms, img_size=(img,) * 3),
+                      (B, img, img, img, dim), 13, True))
+    cases.append(("merge", PatchMerging(32, norm_layer=ln6), (2, 8, 8, 8, 32), 14, True))
+    cases.append(("ccf_ffn", CCF_FFN(32, 128, img_size=(8, 8, 8)), (2, 8, 8, 8, 32), 15, True))
+    cases.append(("enc32h", MultiscaleTransformer(img_size=(32,) * 3, in_chans=4,
+                                                  qkv_bias=True, norm_layer=ln6),
+                  (1, 4, 32, 32, 32), 24, False))
+    cases.append(("full32", Waveformer(img_size=(32, 32, 32), in_chans=4, out_chans=4,
+                                       depths=[2, 2, 2, 2], feat_size=[48, 96, 192, 384],
+                                       num_heads=[3, 6, 12, 24]), (1, 4, 32, 32, 32), 22, False))
+    for name, m, shape, seed, full in cases:
+        m = apply_rule(m).eval()
+        x = seeded_randn(shape, seed).requires_grad_(True)
+        grad_loss(flat_outputs(m(x))).backward()
+        out[f"grad_{name}__x"] = x.grad.numpy()
+        for pn, p in m.named_parameters():
+            if p.grad is None:
+                continue
+            if full:
+                out[f"grad_{name}__{pn}"] = p.grad.numpy()
+            else:
+                gg = p.grad.double().reshape(-1)
+                r = seeded_randn(tuple(p.shape), 777).double().reshape(-1)
+                out[f"grad_{name}__{pn}"] = np.array(
+                    [gg.sum().item(), (gg * gg).sum().item(), (gg * r).sum().item()])
+    print(f"grad fixtures done in {time.time() - t0:.1f}s")
 
 
 def _big128(out, ln6, MultiscaleTransformer, Waveformer):

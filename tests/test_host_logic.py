@@ -26,9 +26,11 @@ def test_cpu_tensors_fail_loudly():
         enc(torch.zeros(1, 1, 32, 32, 32))
 
 
-def test_training_with_grad_is_refused_until_backward_exists():
+def test_training_path_has_no_cpu_fallback():
+    """Under autograd the modules take the HIP training Functions; on CPU tensors they raise
+    instead of computing anything on the host."""
     enc = NM.MultiscaleTransformer(img_size=(32,) * 3, in_chans=1)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="GPU"):
         enc(torch.zeros(1, 1, 32, 32, 32))
 
 
@@ -54,3 +56,19 @@ def test_unsupported_wavelet_is_refused():
     wt = NM.WaveletTransform3D(wavelet="db2")
     with pytest.raises(NotImplementedError):
         wt._check()
+
+
+def test_dicece_loss_vs_reference_monai():
+    """waveformer_amd.losses.DiceCELoss against the reference trainer's MONAI DiceCELoss
+    (3_train.py:72), value and logits gradient (fixtures from gen_reference_fixtures.py
+    --groups loss)."""
+    import torch
+    from oracle.weight_rule import seeded_randn
+    from tests import cases as C
+    from waveformer_amd.losses import DiceCELoss
+    logits = seeded_randn((2, 4, 8, 8, 8), 30).requires_grad_(True)
+    lab = C.g("dicece__labels").long()
+    loss = DiceCELoss(to_onehot_y=True, softmax=True)(logits, lab)
+    loss.backward()
+    assert abs(loss.item() - C.g("dicece__loss").item()) <= 1e-6
+    assert C.rel_l2(logits.grad, C.g("dicece__grad")) <= 1e-6

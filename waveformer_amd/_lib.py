@@ -47,9 +47,32 @@ SIGNATURES = {
     "wf_sliding_window_stitch": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _I64,
                                       _I64, _I64, _I64, _I64, _P]),
     "wf_tta_merge": (_I, [_P, _P, _I, _P, _I64, _I64, _I64, _I64, _P]),
+    # training (config 4)
+    "wf_window_attention_fwd_train": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _P,
+                                           _I64, _I64, _I64, _I64, _I64, _I64, _I64, _F, _I,
+                                           _P]),
+    "wf_window_attention_bwd_core": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64,
+                                          _I64, _I64, _I64, _F, _P]),
+    "wf_rel_pos_bias_bwd": (_I, [_P, _P, _P, _I64, _I64, _I64, _P]),
+    "wf_colsum_parts": (_I64, [_I64]),
+    "wf_colsum": (_I, [_P, _I64, _I64, _P, _I64, _P, _P, _P]),
+    "wf_ln_act_fwd": (_I, [_P, _P, _P, _F, _I, _P, _I64, _I64, _P]),
+    "wf_ln_bwd_workspace_floats": (_I64, [_I64, _I64]),
+    "wf_ln_act_bwd": (_I, [_P, _P, _P, _F, _I, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
+    "wf_dwt3d_haar_bwd": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_haar_analysis_ncdhw": (_I, [_P, _I64, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _I64,
+                                    _P]),
+    "wf_interp_adjoint_axis": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _I64, _P]),
+    "wf_dwconv3d_cl": (_I, [_P, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_dwconv_wgrad_ws_floats": (_I64, [_I64, _I64]),
+    "wf_dwconv3d_wgrad": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_patch_merging_gather": (_I, [_P, _I, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_patch_merging_scatter": (_I, [_P, _I, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_patchify": (_I, [_P, _P, _I, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _lock = threading.Lock()
 _lib = None
 _err = None

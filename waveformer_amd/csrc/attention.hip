@@ -41,7 +41,8 @@ __device__ __forceinline__ void load8_split(const void* base, int64_t off, bf16x
 template <int HD, int KT, bool SPLIT>
 __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__ qkv,
                                                         const float* __restrict__ bias,
-                                                        void* __restrict__ out, int N,
+                                                        void* __restrict__ out,
+                                                        float* __restrict__ lse, int N,
                                                         int heads, float scale_log2) {
   constexpr int NC = HD / 16;  // 16-wide head_dim chunks
   constexpr int NKT = KT / 16; // 16-key sub-tiles per tile
@@ -185,6 +186,8 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
   // full column sums: the 4 lane groups hold disjoint key subsets
   lrun += __shfl_xor(lrun, 16, 64);
   lrun += __shfl_xor(lrun, 32, 64);
+  // training: the row log-sum-exp (log2 domain) that the backward recomputes P from
+  if (lse && qv && lane < 16) lse[(bw * heads + h) * N + q] = mrun + __log2f(lrun);
   if (qv) {
     const float inv = 1.f / lrun;
     const int64_t off = (row0 + q) * C + h * HD + g4;
@@ -202,8 +205,8 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
   }
 }
 
-int launch_attn_core(const void* qkv, const float* bias, void* out, int64_t Bw, int N,
-                     int heads, int hd, float scale, int prec, hipStream_t s) {
+int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, int64_t Bw,
+                     int N, int heads, int hd, float scale, int prec, hipStream_t s) {
   if (Bw <= 0) return WF_OK;
   if (Bw > 65535) return fail(WF_E_SHAPE, "attention: more than 65535 windows per call");
   dim3 grid((unsigned)cdiv(N, kQB), (unsigned)heads, (unsigned)Bw);
@@ -213,10 +216,10 @@ int launch_attn_core(const void* qkv, const float* bias, void* out, int64_t Bw, 
   case HDV:                                                                                \
     if (split)                                                                             \
       hipLaunchKernelGGL((attn_core_kernel<HDV, (HDV >= 192 ? 32 : 64), true>), grid,      \
-                         dim3(256), 0, s, qkv, bias, out, N, heads, sl2);                  \
+                         dim3(256), 0, s, qkv, bias, out, lse, N, heads, sl2);             \
     else                                                                                   \
       hipLaunchKernelGGL((attn_core_kernel<HDV, 64, false>), grid, dim3(256), 0, s, qkv,   \
-                         bias, out, N, heads, sl2);                                        \
+                         bias, out, lse, N, heads, sl2);                                   \
     break;
   switch (hd) {
     WF_ATTN_CASE(16)
@@ -269,13 +272,14 @@ extern "C" int64_t wf_window_attention_workspace_bytes(int64_t B, int64_t C, int
   return qkv + ao;
 }
 
-extern "C" int wf_window_attention_fwd(const float* x, const float* ln_w, const float* ln_b,
-                                       float ln_eps, const uint16_t* wqkv_bf16x2,
-                                       const float* bqkv, const float* bias,
-                                       const uint16_t* wproj_bf16x2, const float* bproj,
-                                       float* out, void* workspace, int64_t B, int64_t C,
-                                       int64_t D1, int64_t H1, int64_t W1, int64_t ws,
-                                       int64_t heads, float scale, int precision, void* stream) {
+extern "C" int wf_window_attention_fwd_train(const float* x, const float* ln_w,
+                                             const float* ln_b, float ln_eps,
+                                             const uint16_t* wqkv_bf16x2, const float* bqkv,
+                                             const float* bias, const uint16_t* wproj_bf16x2,
+                                             const float* bproj, float* out, void* workspace,
+                                             float* lse, int64_t B, int64_t C, int64_t D1,
+                                             int64_t H1, int64_t W1, int64_t ws, int64_t heads,
+                                             float scale, int precision, void* stream) {
   WF_REQUIRE(B >= 1 && C >= 8 && C % 8 == 0, "C must be a positive multiple of 8");
   WF_REQUIRE(ws >= 1 && D1 % ws == 0 && H1 % ws == 0 && W1 % ws == 0,
              "the raster must tile into ws^3 windows (window_partition, wave_helper.py:459)");
@@ -325,7 +329,7 @@ extern "C" int wf_window_attention_fwd(const float* x, const float* ln_w, const 
   int rc = launch_gemm(g, s, "wf_window_attention_fwd(qkv)");
   if (rc) return rc;
   // 2. softmax(q k^T * scale + bias) v
-  rc = launch_attn_core(qkv, bias, ao, Bw, (int)N, (int)heads, (int)(C / heads), scale,
+  rc = launch_attn_core(qkv, bias, ao, lse, Bw, (int)N, (int)heads, (int)(C / heads), scale,
                         precision, s);
   if (rc) return rc;
   // 3. proj; window-major rows == the reshaped raster (Q1)
@@ -347,4 +351,16 @@ extern "C" int wf_window_attention_fwd(const float* x, const float* ln_w, const 
   p.out_bf16 = 0;
   p.ldo = C;
   return launch_gemm(p, s, "wf_window_attention_fwd(proj)");
+}
+
+extern "C" int wf_window_attention_fwd(const float* x, const float* ln_w, const float* ln_b,
+                                       float ln_eps, const uint16_t* wqkv_bf16x2,
+                                       const float* bqkv, const float* bias,
+                                       const uint16_t* wproj_bf16x2, const float* bproj,
+                                       float* out, void* workspace, int64_t B, int64_t C,
+                                       int64_t D1, int64_t H1, int64_t W1, int64_t ws,
+                                       int64_t heads, float scale, int precision, void* stream) {
+  return wf_window_attention_fwd_train(x, ln_w, ln_b, ln_eps, wqkv_bf16x2, bqkv, bias,
+                                       wproj_bf16x2, bproj, out, workspace, nullptr, B, C, D1,
+                                       H1, W1, ws, heads, scale, precision, stream);
 }

@@ -424,6 +424,10 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
                                 const float* fc_b, const float* branch_scale, float* out,
                                 void* workspace, int64_t B, int64_t C, int64_t hidden,
                                 int64_t D, int64_t H, int64_t W, int precision, void* stream) {
+  // bit 4: training -- take the staged path even where the fused back half exists, so the
+  // workspace keeps h1 = GELU(LN1(pwconv)) and h2 = dwconv (pre-LN2) for the backward
+  const bool keep = (stage & 16) != 0;
+  stage &= ~16;
   WF_REQUIRE(stage >= 0 && stage <= 3, "stage must be 0 (all), 1 (pwconv), 2 (dwconv) or 3 (fc)");
   WF_REQUIRE(B >= 1 && D >= 1 && H >= 1 && W >= 1, "empty volume");
   WF_REQUIRE(C % 8 == 0 && hidden % 8 == 0, "C and hidden must be multiples of 8");
@@ -482,7 +486,7 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   // in LDS, or run the z-marching depthwise conv with LN2 + GELU moved into the fc loader
   static const bool fused_dw = getenv("WF_FFN_FUSED_DW") != nullptr;
   static const bool no_dwfc = getenv("WF_FFN_NO_DWFC") != nullptr;
-  if (!no_dwfc && C == 48 && hidden == 192) {
+  if (!keep && !no_dwfc && C == 48 && hidden == 192) {
     if (stage == 1 || stage == 3) return rc;  // stage 3 (fc) is part of the fused kernel
     DwFcArgs d{};
     d.h1 = h1;
@@ -505,7 +509,8 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
     d.W = (int)W;
     return launch_ffn_dwfc(d, precision, s);
   }
-  const bool split_ln = !fused_dw && hidden % 32 == 0;
+  const bool split_ln = (keep || !fused_dw) && hidden % 32 == 0;
+  WF_REQUIRE(!keep || split_ln, "training needs hidden % 32 == 0 (h2 kept pre-LayerNorm)");
   float* pst = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 2 * one);
   if (stage == 0 || stage == 2) {
     if (split_ln)

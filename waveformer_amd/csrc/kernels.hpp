@@ -65,8 +65,8 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);
 int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_only);
 
 // ---- windowed attention core over a (B_, N, 3C) qkv buffer (bf16, or fp32 when SPLIT) ----
-int launch_attn_core(const void* qkv, const float* bias, void* out, int64_t Bw, int N,
-                     int heads, int hd, float scale, int prec, hipStream_t s);
+int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, int64_t Bw,
+                     int N, int heads, int hd, float scale, int prec, hipStream_t s);
 
 // ---- depthwise 3^3 conv + bias + LayerNorm + GELU over a channel-last volume ------------
 // (bf16 storage for PREC_BF16, fp32 for PREC_SPLIT)

@@ -12,6 +12,7 @@ from typing import Optional, Tuple
 import torch
 import torch.nn as nn
 
+from .. import autograd as wfa
 from .. import ops
 
 
@@ -58,10 +59,6 @@ class Attention(nn.Module):
         return self._bias
 
     def _check_train(self):
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError(
-                "waveformer_amd: the attention backward kernels are not built yet; "
-                "run the module in eval() or under torch.no_grad()")
         if self.training and (self.attn_drop.p > 0 or self.proj_drop.p > 0):
             raise NotImplementedError("waveformer_amd: attention dropout > 0 is not supported")
 
@@ -72,6 +69,8 @@ class Attention(nn.Module):
         quirk Q1).  Row r of the result (as a (B*D*H*W, C) matrix) is token r % N of window
         r // N; viewed as (B, D, H, W, C) it is exactly the reference's attn_windows."""
         self._check_train()
+        if wfa.needs_grad(x_cl, *self.parameters(), *(ln[:2] if ln is not None else ())):
+            return wfa.window_attention(self, x_cl, ln)
         return ops.window_attention(
             x_cl, self.qkv.weight, self.qkv.bias, self.dense_bias(), self.proj.weight,
             self.proj.bias, self.window_size, self.num_heads, self.scale, ln)

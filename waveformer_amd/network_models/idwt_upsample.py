@@ -12,6 +12,7 @@ from typing import Any, Dict, Sequence, Tuple, Union
 import torch
 import torch.nn as nn
 
+from .. import autograd as wfa
 from .. import ops
 from ..blocks import UnetBasicBlock, UnetResBlock, get_conv_layer
 
@@ -70,6 +71,10 @@ class UnetrIDWTBlock(nn.Module):
         size = tuple(s * 2 ** L for s in inp.shape[2:])
         if skip.shape[0] != B or tuple(skip.shape[2:]) != size:
             raise ValueError(f"skip {tuple(skip.shape)} does not match the IDWT output {(B, C) + size}")
+        if torch.is_grad_enabled() and (inp.requires_grad or skip.requires_grad or any(
+                t.requires_grad for d in hf_coeffs for t in d.values())):
+            out = wfa.idwt3d_haar(inp, hf_coeffs)
+            return self.conv_block(torch.cat((out, skip), dim=1))
         buf = torch.empty((B, C + skip.shape[1]) + size, dtype=inp.dtype, device=inp.device)
         ops.idwt3d_haar(inp, hf_coeffs, out=buf)   # channels [0, C)
         buf[:, C:].copy_(skip)                      # torch.cat((out, skip), 1)

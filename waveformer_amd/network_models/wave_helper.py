@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import autograd as wfa
 from .. import ops
 from .attention import Attention
 
@@ -136,7 +137,10 @@ class PatchMergingV2(nn.Module):
         b, d, h, w, c = x.shape
         if d % 2 or h % 2 or w % 2:  # F.pad branch of the reference (never hit by WaveFormer)
             x = F.pad(x, (0, 0, 0, w % 2, 0, h % 2, 0, d % 2))
-        return ops.patch_merging(x.contiguous(), self.norm, self.reduction, v2=self._v2)
+        x = x.contiguous()
+        if wfa.needs_grad(x, *self.parameters()):
+            return wfa.patch_merging(x, self.norm, self.reduction, self._v2)
+        return ops.patch_merging(x, self.norm, self.reduction, v2=self._v2)
 
 
 class PatchMerging(PatchMergingV2):
@@ -176,7 +180,10 @@ class CCF_FFN(nn.Module):
     def forward(self, x):
         B, D, H, W, C = x.shape
         assert D * H * W == self.D * self.H * self.W
-        return ops.ccf_ffn(x.contiguous(), None, None, self)
+        x = x.contiguous()
+        if wfa.needs_grad(x, *self.parameters()):
+            return wfa.ccf_ffn(x, None, None, self)
+        return ops.ccf_ffn(x, None, None, self)
 
     def flops(self):
         n = self.D * self.H * self.W
@@ -231,6 +238,14 @@ class WaveletTransform3D(nn.Module):
         return cur, bands
 
     def forward(self, x, level):
+        if wfa.needs_grad(x):
+            self._check()
+            cur = x.permute(0, 2, 3, 4, 1).contiguous()
+            yh = []
+            for _ in range(level):
+                cur, det = wfa.dwt3d_haar(cur)
+                yh.append(det)
+            return cur.permute(0, 4, 1, 2, 3), list(reversed(yh))
         ll, bands = self.decompose_cl(x.permute(0, 2, 3, 4, 1).contiguous(), level)
         yh = [ops.bands_to_coeffs(b)[1] for b in reversed(bands)]
         return ll.permute(0, 4, 1, 2, 3), yh
@@ -307,6 +322,8 @@ class Block(nn.Module):
         x = self._prep(x)
         s_attn, s_mlp = self._branch_scales(x.shape[0], x.device)
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        if wfa.needs_grad(x, *self.parameters()):
+            return self._multi_scale_train(x, ln1, s_attn, s_mlp)
         if self.level > 0:
             self.dwt_downsamples._check()
             srcs, hfs = [], []
@@ -325,11 +342,46 @@ class Block(nn.Module):
             return out, tuple(reversed(hfs))
         return out
 
+    def _multi_scale_train(self, x, ln1, s_attn, s_mlp):
+        """multi_scale_forward under autograd: the same dataflow through the differentiable
+        Functions of waveformer_amd.autograd (HIP forward + backward kernels)."""
+        if self.level > 0:
+            self.dwt_downsamples._check()
+            srcs, hfs = [], []
+            cur = x
+            for i in range(self.attn_computation_level):
+                cur, det = wfa.dwt3d_haar(cur, ln1 if i == 0 else None)
+                srcs.append(self.attn.forward_raster(cur))
+                hfs.append(det)
+        else:
+            srcs = [self.attn.forward_raster(x, ln1)]
+            hfs = None
+        xh, stats = wfa.MsFuse.apply(x, s_attn, float(self.norm2.eps), *srcs)
+        out = wfa.ccf_ffn(xh, stats, self.norm2, self.mlp, s_mlp)
+        if self.level > 0:
+            return out, tuple(reversed(hfs))
+        return out
+
     def single_scale_forward(self, x):
         """wave_helper.py:515-549: one L-level DWT, one attention pass, one interpolation."""
         x = self._prep(x)
         s_attn, s_mlp = self._branch_scales(x.shape[0], x.device)
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        if wfa.needs_grad(x, *self.parameters()):
+            x_h = None
+            if self.level > 0:
+                self.dwt_downsamples._check()
+                cur, x_h = x, []
+                for i in range(self.level):
+                    cur, det = wfa.dwt3d_haar(cur, ln1 if i == 0 else None)
+                    x_h.append(det)
+                a = self.attn.forward_raster(cur)
+                x_h = list(reversed(x_h))
+            else:
+                a = self.attn.forward_raster(x, ln1)
+            xh, stats = wfa.MsFuse.apply(x, s_attn, float(self.norm2.eps), a)
+            out = wfa.ccf_ffn(xh, stats, self.norm2, self.mlp, s_mlp)
+            return (out, x_h) if self.level > 0 else out
         x_h = None
         if self.level > 0:
             ll, bands = self.dwt_downsamples.decompose_cl(x, self.level, ln1)

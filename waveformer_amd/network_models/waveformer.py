@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.init as init
 
+from .. import autograd as wfa
 from .. import ops
 from ..blocks import PatchEmbed as _MonaiPatchEmbed
 from .wave_helper import Block, PatchMerging
@@ -105,15 +106,16 @@ class MultiscaleTransformer(nn.Module):
                          ) -> Tuple[List[torch.Tensor], List]:
         """waveformer.py:260-322: PatchEmbed -> 4 stages (Blocks, PatchMerging) -> proj_out.
         Returns (outs: 4 NCDHW tensors, outs_hf: the last block's detail dicts of stages 1-3)."""
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError(
-                "waveformer_amd: backward kernels are not built yet; use eval() / no_grad()")
         if self.patch_norm:
             raise NotImplementedError("waveformer_amd: patch_norm=True is not implemented")
         if x_rgb.dtype != torch.float32:
             raise TypeError("waveformer_amd: float32 input expected")
-        x = ops.patch_embed(x_rgb.contiguous(), self.patch_embed.proj.weight,
-                            self.patch_embed.proj.bias)
+        pe = self.patch_embed.proj
+        train = wfa.needs_grad(x_rgb, *self.parameters())
+        if train:
+            x = wfa.PatchEmbedFn.apply(x_rgb.contiguous(), pe.weight, pe.bias)
+        else:
+            x = ops.patch_embed(x_rgb.contiguous(), pe.weight, pe.bias)
         outs, outs_hf = [], []
         for s in range(4):
             if s > 0:
@@ -126,7 +128,10 @@ class MultiscaleTransformer(nn.Module):
                 else:
                     x = r
             B, D, H, W, C = x.shape
-            outs.append(ops.proj_out(x, normalize))
+            if train:
+                outs.append(wfa.ProjOutFn.apply(x, bool(normalize), 1e-5))
+            else:
+                outs.append(ops.proj_out(x, normalize))
             if s < 3:
                 outs_hf.append(x_h if x_h is not None else ())
         return outs, outs_hf

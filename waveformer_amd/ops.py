@@ -341,13 +341,18 @@ def ccf_ffn_fc(args):
 # ------------------------------------------------------------------------------------------
 def patch_merging(x_cl: torch.Tensor, norm: torch.nn.LayerNorm, reduction: torch.nn.Linear,
                   v2: bool = False) -> torch.Tensor:
+    return _patch_merging_raw(x_cl, norm.weight, norm.bias, float(norm.eps), reduction.weight,
+                              v2, _prec())
+
+
+def _patch_merging_raw(x_cl, ln_w, ln_b, eps, red_w, v2, prec) -> torch.Tensor:
     _check(x_cl, "x")
     B, D, H, W, C = x_cl.shape
-    red = split_weight(reduction.weight)
+    red = split_weight(red_w)
     out = torch.empty((B, D // 2, H // 2, W // 2, 2 * C), dtype=torch.float32, device=x_cl.device)
-    _lib.call("wf_patch_merging_fwd", x_cl.data_ptr(), norm.weight.data_ptr(),
-              norm.bias.data_ptr(), float(norm.eps), red.data_ptr(), int(bool(v2)), out.data_ptr(),
-              B, C, D, H, W, _prec(), _stream())
+    _lib.call("wf_patch_merging_fwd", x_cl.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
+              float(eps), red.data_ptr(), int(bool(v2)), out.data_ptr(), B, C, D, H, W, prec,
+              _stream())
     return out
 
 
