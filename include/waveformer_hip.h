@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 5
+#define WF_ABI_VERSION 6
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1 };
 
@@ -92,6 +92,27 @@ int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float* ln_b, floa
 int wf_idwt3d_haar(const float* ll, int64_t ll_bstride, const float* const* det,
                    const int64_t* det_s, int levels, float* out, int64_t out_bstride,
                    int64_t B, int64_t C, int64_t d, int64_t h, int64_t w, void* stream);
+
+/* ---- C5: general wavelets (db1..db4), NCDHW, any sizes ------------------------------- */
+/* One analysis level of ptwt.wavedec3(x, wavelet, mode='zero') (wave_helper.py:350 with a
+ * wavelet other than 'db1'; BASELINE config 5 "db2 3-level DWT").  dec_lo / dec_hi are HOST
+ * arrays of `taps` floats (pywt Wavelet.dec_lo / dec_hi, taps in {2,4,6,8}).
+ * x: P contiguous (D, H, W) planes (P = B*C of an NCDHW tensor).
+ * bands: (8, P, d, h, w) with d = (D + taps - 1) / 2 (same for h, w); band k bits
+ * (z, y, x) = (k>>2, k>>1 & 1, k & 1), 'a' = 0 -- band 0 is LL, bands 1..7 'aad'..'ddd'.     */
+int wf_dwt3d_fwd(const float* x, float* bands, int64_t P, int64_t D, int64_t H, int64_t W,
+                 const float* dec_lo, const float* dec_hi, int taps, void* stream);
+
+/* One synthesis level of ptwt.waverec3 (idwt_upsample.py:160 with a wavelet other than
+ * 'db1').  coef[8]: band k as above (coef[0] = LL, already cropped to the details' shape by
+ * the caller, pywt's rule), each (B, C, n_z, n_y, n_x) with its own 5 element strides
+ * coef_strides[5k .. 5k+4] = (b, c, z, y, x).  rec_lo / rec_hi: HOST arrays of `taps` floats.
+ * out: element (b, c, z, y, x) at b*out_bstride + c*out_cstride + (z*Oy + y)*Ox + x with
+ * O = 2n - taps + 2 per axis.                                                               */
+int wf_idwt3d_level(const float* const* coef, const int64_t* coef_strides, int64_t B, int64_t C,
+                    int64_t n_z, int64_t n_y, int64_t n_x, const float* rec_lo,
+                    const float* rec_hi, int taps, float* out, int64_t out_bstride,
+                    int64_t out_cstride, void* stream);
 
 /* ---- a2: relative-position bias ------------------------------------------------------ */
 /* bias[h][i][j] = table[index[i][j]][h]  (attention.py:94-97), index is the int64

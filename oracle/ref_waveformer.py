@@ -34,6 +34,26 @@ FILTERS = {
             (-0.48296291314453416, 0.8365163037378079, -0.2241438680420134, -0.12940952255126037),
             (0.48296291314453416, 0.8365163037378079, 0.2241438680420134, -0.12940952255126037),
             (-0.12940952255126037, -0.2241438680420134, 0.8365163037378079, -0.48296291314453416)),
+    "db3": ((0.03522629188570953, -0.08544127388202666, -0.13501102001025458,
+             0.45987750211849154, 0.8068915093110925, 0.33267055295008263),
+            (-0.33267055295008263, 0.8068915093110925, -0.45987750211849154,
+             -0.13501102001025458, 0.08544127388202666, 0.03522629188570953),
+            (0.33267055295008263, 0.8068915093110925, 0.45987750211849154,
+             -0.13501102001025458, -0.08544127388202666, 0.03522629188570953),
+            (0.03522629188570953, 0.08544127388202666, -0.13501102001025458,
+             -0.45987750211849154, 0.8068915093110925, -0.33267055295008263)),
+    "db4": ((-0.010597401785069032, 0.0328830116668852, 0.030841381835560764,
+             -0.18703481171909309, -0.027983769416859854, 0.6308807679298589,
+             0.7148465705529157, 0.2303778133088965),
+            (-0.2303778133088965, 0.7148465705529157, -0.6308807679298589,
+             -0.027983769416859854, 0.18703481171909309, 0.030841381835560764,
+             -0.0328830116668852, -0.010597401785069032),
+            (0.2303778133088965, 0.7148465705529157, 0.6308807679298589,
+             -0.027983769416859854, -0.18703481171909309, 0.030841381835560764,
+             0.0328830116668852, -0.010597401785069032),
+            (-0.010597401785069032, -0.0328830116668852, 0.030841381835560764,
+             0.18703481171909309, -0.027983769416859854, -0.6308807679298589,
+             0.7148465705529157, -0.2303778133088965)),
 }
 DETAIL_KEYS = ("aad", "ada", "add", "daa", "dad", "dda", "ddd")
 
@@ -48,8 +68,8 @@ def _analysis_axis(x: Tensor, dim: int, lo, hi) -> Tuple[Tensor, Tensor]:
     x = x.movedim(dim, -1)
     xp = F.pad(x, (padl, padr))
     win = xp.unfold(-1, L, 2)  # (..., nout, L)
-    flo = torch.tensor(lo[::-1], dtype=x.dtype)
-    fhi = torch.tensor(hi[::-1], dtype=x.dtype)
+    flo = torch.tensor(lo[::-1], dtype=x.dtype, device=x.device)
+    fhi = torch.tensor(hi[::-1], dtype=x.dtype, device=x.device)
     a = (win * flo).sum(-1).movedim(-1, dim)
     d = (win * fhi).sum(-1).movedim(-1, dim)
     return a, d
@@ -62,7 +82,7 @@ def _synthesis_axis(a: Tensor, d: Tensor, dim: int, rlo, rhi) -> Tensor:
     a = a.movedim(dim, -1)
     d = d.movedim(dim, -1)
     N = a.shape[-1]
-    y = torch.zeros(a.shape[:-1] + (2 * N + L - 2,), dtype=a.dtype)
+    y = torch.zeros(a.shape[:-1] + (2 * N + L - 2,), dtype=a.dtype, device=a.device)
     for j in range(L):
         y[..., j:j + 2 * N:2] += rlo[j] * a + rhi[j] * d
     padl = (2 * L - 3) // 2

@@ -26,6 +26,8 @@ def main():
         ("haar", (1, 2, 4, 6, 10), 2),
         ("db2", (1, 2, 12, 12, 12), 2),
         ("db2", (1, 1, 11, 9, 7), 2),
+        ("db3", (1, 2, 13, 10, 17), 2),
+        ("db4", (1, 1, 20, 19, 9), 2),
     ]
     for ci, (wav, shape, levels) in enumerate(cases):
         x = rs.standard_normal(shape)

@@ -22,7 +22,7 @@ FP32_TOL = 2e-6
 def test_pywt_vectors():
     z = np.load(C.PYWT_PATH)
     ncase = len([k for k in z.files if k.endswith("_meta")])
-    assert ncase == 4
+    assert ncase == 6
     for ci in range(ncase):
         x = torch.from_numpy(z[f"c{ci}_x"])
         wav = bytes(z[f"c{ci}_wavelet"]).decode()

@@ -30,6 +30,9 @@ SIGNATURES = {
     "wf_patch_embed_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwt3d_haar_fwd": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_dwt3d_fwd": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _I, _P]),
+    "wf_idwt3d_level": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _P, _I, _P, _I64, _I64,
+                             _P]),
     "wf_rel_pos_bias": (_I, [_P, _P, _P, _I64, _I64, _I64, _P]),
     "wf_window_attention_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I]),
     "wf_window_attention_fwd": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P,
@@ -72,7 +75,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _lock = threading.Lock()
 _lib = None
 _err = None

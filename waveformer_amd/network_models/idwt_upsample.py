@@ -60,12 +60,28 @@ class UnetrIDWTBlock(nn.Module):
                               kernel_size=kernel_size, stride=1, norm_name=norm_name)
 
     def forward(self, inp, skip, hf_coeffs):
-        if str(self.wavelet) not in ("db1", "haar"):
-            raise NotImplementedError(f"waveformer_amd: IDWT wavelet {self.wavelet!r} not implemented")
         inp = self.conv_lf_block(inp)
         if self.hf_refinement:
             hf_coeffs = tuple({k: self.hf_ref[i](d[k]) for k in d}
                               for i, d in enumerate(hf_coeffs))
+        wname = str(getattr(self.wavelet, "name", self.wavelet))
+        if wname not in ("db1", "haar"):
+            # longer filters (config 5): one wf_idwt3d_level launch per level, the finest
+            # written into the concatenation buffer; inference only
+            if torch.is_grad_enabled() and (inp.requires_grad or any(
+                    t.requires_grad for d in hf_coeffs for t in d.values())):
+                raise NotImplementedError(
+                    f"waveformer_amd: backward through wavelet {self.wavelet!r} not implemented")
+            shp = hf_coeffs[-1]["aad"].shape
+            size = tuple(2 * n - len(ops.WAVELETS[wname][0]) + 2 for n in shp[2:])
+            B, C = inp.shape[:2]
+            if skip.shape[0] != B or tuple(skip.shape[2:]) != size:
+                raise ValueError(f"skip {tuple(skip.shape)} does not match the IDWT output "
+                                 f"{(B, C) + size}")
+            buf = torch.empty((B, C + skip.shape[1]) + size, dtype=inp.dtype, device=inp.device)
+            ops.waverec3((inp,) + tuple(hf_coeffs), self.wavelet, out=buf[:, :C])
+            buf[:, C:].copy_(skip)
+            return self.conv_block(buf)
         B, C = inp.shape[:2]
         L = len(hf_coeffs)
         size = tuple(s * 2 ** L for s in inp.shape[2:])

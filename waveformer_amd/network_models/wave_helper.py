@@ -223,8 +223,8 @@ class WaveletTransform3D(nn.Module):
     def _check(self):
         if str(self.wavelet) not in ("db1", "haar") or self.mode != "zero":
             raise NotImplementedError(
-                f"waveformer_amd: wavelet {self.wavelet!r} / mode {self.mode!r} not implemented "
-                "(Haar + 'zero' only; db2 is a SURVEY 8f item)")
+                f"waveformer_amd: the fused channel-last path is Haar only (got {self.wavelet!r}, "
+                f"mode {self.mode!r}); forward() takes db2..db4")
 
     def decompose_cl(self, x_cl: torch.Tensor, level: int, ln=None):
         """Channel-last variant used by Block: returns (LL (B,d,h,w,C), [band buffers] fine->coarse)."""
@@ -238,6 +238,15 @@ class WaveletTransform3D(nn.Module):
         return cur, bands
 
     def forward(self, x, level):
+        if self.mode != "zero":
+            raise NotImplementedError(f"waveformer_amd: wavelet mode {self.mode!r} not implemented")
+        if str(getattr(self.wavelet, "name", self.wavelet)) not in ("db1", "haar"):
+            # longer filters (config 5: db2 3-level): NCDHW per-op kernels, inference only
+            if wfa.needs_grad(x):
+                raise NotImplementedError(
+                    f"waveformer_amd: backward through wavelet {self.wavelet!r} not implemented")
+            co = ops.wavedec3(x, self.wavelet, level)
+            return co[0], co[1:]
         if wfa.needs_grad(x):
             self._check()
             cur = x.permute(0, 2, 3, 4, 1).contiguous()

@@ -213,6 +213,124 @@ def idwt3d_haar(ll: torch.Tensor, details: Sequence[Dict[str, torch.Tensor]],
 
 
 # ------------------------------------------------------------------------------------------
+# C5: general orthogonal wavelets (db1..db4), NCDHW, any sizes
+# ------------------------------------------------------------------------------------------
+# pywt.Wavelet(name).(dec_lo, dec_hi, rec_lo, rec_hi) -- PyWavelets' filter banks, which ptwt
+# 0.1.9 uses (requirements.txt:45); values printed by PyWavelets 1.1.1.
+WAVELETS: Dict[str, Tuple[Tuple[float, ...], ...]] = {
+    "db1": ((0.7071067811865476, 0.7071067811865476), (-0.7071067811865476, 0.7071067811865476),
+            (0.7071067811865476, 0.7071067811865476), (0.7071067811865476, -0.7071067811865476)),
+    "db2": ((-0.12940952255126037, 0.2241438680420134, 0.8365163037378079, 0.48296291314453416),
+            (-0.48296291314453416, 0.8365163037378079, -0.2241438680420134, -0.12940952255126037),
+            (0.48296291314453416, 0.8365163037378079, 0.2241438680420134, -0.12940952255126037),
+            (-0.12940952255126037, -0.2241438680420134, 0.8365163037378079, -0.48296291314453416)),
+    "db3": ((0.03522629188570953, -0.08544127388202666, -0.13501102001025458,
+             0.45987750211849154, 0.8068915093110925, 0.33267055295008263),
+            (-0.33267055295008263, 0.8068915093110925, -0.45987750211849154,
+             -0.13501102001025458, 0.08544127388202666, 0.03522629188570953),
+            (0.33267055295008263, 0.8068915093110925, 0.45987750211849154,
+             -0.13501102001025458, -0.08544127388202666, 0.03522629188570953),
+            (0.03522629188570953, 0.08544127388202666, -0.13501102001025458,
+             -0.45987750211849154, 0.8068915093110925, -0.33267055295008263)),
+    "db4": ((-0.010597401785069032, 0.0328830116668852, 0.030841381835560764,
+             -0.18703481171909309, -0.027983769416859854, 0.6308807679298589,
+             0.7148465705529157, 0.2303778133088965),
+            (-0.2303778133088965, 0.7148465705529157, -0.6308807679298589,
+             -0.027983769416859854, 0.18703481171909309, 0.030841381835560764,
+             -0.0328830116668852, -0.010597401785069032),
+            (0.2303778133088965, 0.7148465705529157, 0.6308807679298589,
+             -0.027983769416859854, -0.18703481171909309, 0.030841381835560764,
+             0.0328830116668852, -0.010597401785069032),
+            (-0.010597401785069032, -0.0328830116668852, 0.030841381835560764,
+             0.18703481171909309, -0.027983769416859854, -0.6308807679298589,
+             0.7148465705529157, -0.2303778133088965)),
+}
+WAVELETS["haar"] = WAVELETS["db1"]
+
+
+def _filters(wavelet: str):
+    name = str(getattr(wavelet, "name", wavelet))
+    if name not in WAVELETS:
+        raise NotImplementedError(f"wavelet {name!r}: only {sorted(WAVELETS)} are implemented")
+    return [(ctypes.c_float * len(f))(*f) for f in WAVELETS[name]], len(WAVELETS[name][0])
+
+
+def dwt3d(x: torch.Tensor, wavelet: str) -> torch.Tensor:
+    """One level of ptwt.wavedec3(x, wavelet, mode='zero') over the last three axes of an
+    NCDHW tensor -> bands (8, B, C, d, h, w), d = (D + L - 1) // 2; band 0 = LL, 1..7 = the
+    DETAIL_KEYS (wave_helper.py:350 with a non-Haar wavelet; config 5)."""
+    _check(x, "x", contiguous=False)
+    if x.dim() != 5:
+        raise ValueError(f"dwt3d: expected (B, C, D, H, W), got {tuple(x.shape)}")
+    x = x.contiguous()
+    (lo, hi, _, _), L = _filters(wavelet)
+    B, C, D, H, W = x.shape
+    bands = torch.empty((8, B, C, (D + L - 1) // 2, (H + L - 1) // 2, (W + L - 1) // 2),
+                        dtype=torch.float32, device=x.device)
+    _lib.call("wf_dwt3d_fwd", x.data_ptr(), bands.data_ptr(), B * C, D, H, W, lo, hi, L,
+              _stream())
+    return bands
+
+
+def wavedec3(x: torch.Tensor, wavelet: str, level: int) -> List:
+    """ptwt.wavedec3(x, wavelet, mode='zero', level=level) -> [LL, dict_coarsest, ...,
+    dict_finest] (wave_helper.py:350); every tensor is a view of its level's band buffer."""
+    if level < 1:
+        raise ValueError("wavedec3: level must be >= 1")
+    dets = []
+    cur = x
+    for _ in range(level):
+        bands = dwt3d(cur, wavelet)
+        dets.append({k: bands[i + 1] for i, k in enumerate(DETAIL_KEYS)})
+        cur = bands[0]
+    return [cur] + dets[::-1]
+
+
+def waverec3(coeffs: Sequence, wavelet: str, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ptwt.waverec3((LL, dict_coarsest, ..., dict_finest), wavelet) (idwt_upsample.py:160).
+
+    Each level is one wf_idwt3d_level launch reading LL and the 7 details through their own
+    strides (an LL one sample longer than the details is cropped to them, pywt's rule).  If
+    `out` is given it receives the finest level: a (B, C, Oz, Oy, Ox) view whose (z, y, x) block
+    is contiguous, e.g. the first C channels of the decoder's concatenation buffer."""
+    (_, _, rlo, rhi), L = _filters(wavelet)
+    x = coeffs[0]
+    _check(x, "LL", contiguous=False)
+    nlev = len(coeffs) - 1
+    if nlev < 1:
+        raise ValueError("waverec3: need at least one detail level")
+    for li, det in enumerate(coeffs[1:]):
+        ts = [det[k] for k in DETAIL_KEYS]
+        shp = tuple(ts[0].shape)
+        for k, t in zip(DETAIL_KEYS, ts):
+            _check(t, f"detail {k}", contiguous=False)
+            if tuple(t.shape) != shp or t.device != x.device:
+                raise ValueError(f"waverec3: level {li} detail {k} has shape {tuple(t.shape)}, "
+                                 f"expected {shp}")
+        if x.dim() != 5 or tuple(x.shape[:2]) != shp[:2] or any(
+                a < b or a > b + 1 for a, b in zip(x.shape[2:], shp[2:])):
+            raise ValueError(f"waverec3: LL {tuple(x.shape)} does not fit details {shp}")
+        x = x[..., :shp[2], :shp[3], :shp[4]]
+        B, C, nz, ny, nx = shp
+        O = tuple(2 * n - L + 2 for n in shp[2:])
+        last = li == nlev - 1
+        if last and out is not None:
+            if tuple(out.shape) != (B, C) + O or out.stride()[2:] != (O[1] * O[2], O[2], 1):
+                raise ValueError(f"waverec3: out {tuple(out.shape)} / {out.stride()} does not "
+                                 f"fit ({B},{C})+{O} with a contiguous (z, y, x) block")
+            o = out
+        else:
+            o = torch.empty((B, C) + O, dtype=torch.float32, device=x.device)
+        src = [x] + ts
+        ptrs = (ctypes.c_void_p * 8)(*[t.data_ptr() for t in src])
+        st = (ctypes.c_int64 * 40)(*[s for t in src for s in t.stride()])
+        _lib.call("wf_idwt3d_level", ptrs, st, B, C, nz, ny, nx, rlo, rhi, L, o.data_ptr(),
+                  o.stride(0), o.stride(1), _stream())
+        x = o
+    return x
+
+
+# ------------------------------------------------------------------------------------------
 # a2/a3: attention
 # ------------------------------------------------------------------------------------------
 def rel_pos_bias(table: torch.Tensor, index: torch.Tensor) -> torch.Tensor:
