@@ -114,6 +114,35 @@ int wf_idwt3d_level(const float* const* coef, const int64_t* coef_strides, int64
                     const float* rec_hi, int taps, float* out, int64_t out_bstride,
                     int64_t out_cstride, void* stream);
 
+/* ---- decoder: 3x3x3 convolution ------------------------------------- */
+/* Replaces the decoder's Conv3d(Cin, Cout, 3, stride 1, padding 1) of MONAI's Convolution /
+ * get_conv_layer (monai/networks/blocks/dynunet_block.py:98-111, :270-301), as called by
+ * UnetResBlock / UnetBasicBlock / UnetrIDWTBlock.conv_lf_block (network_backbone.py:380-407).
+ * Activations channel-last: position p = ((b*D + z)*H + y)*W + x at x[p*ldx + c] (a
+ * channels_last_3d tensor, or a channel slice of one with ldx = its channel count), out the
+ * same with ldo.  Cin % 4 == 0, Cout % 16 == 0.  bias (Cout) or NULL.
+ * w_packed: wf_conv3d_k3_packed_elems(Cin, Cout) bf16 made by wf_conv3d_k3_pack from the
+ * fp32 (Cout, Cin, 3, 3, 3) weight ([2] hi / lo planes, K-step-major).  precision WF_PREC_*. */
+int64_t wf_conv3d_k3_packed_elems(int64_t Cin, int64_t Cout);
+int wf_conv3d_k3_pack(const float* w, uint16_t* packed, int64_t Cin, int64_t Cout, void* stream);
+int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed, const float* bias,
+                     float* out, int64_t ldo, int64_t B, int64_t Cin, int64_t Cout, int64_t D,
+                     int64_t H, int64_t W, int precision, void* stream);
+
+/* InstanceNorm3d(affine=False) statistics of a channel-last tensor: P positions per sample,
+ * element (b, p, c) at x[(b*P + p)*ldx + c].  stats: (B, 2, C) fp32 {mean row, rstd row},
+ * rstd = 1/sqrt(biased var + eps).  workspace: wf_instnorm_workspace_bytes(B, C) bytes.
+ * The norm / act / residual glue of MONAI UnetResBlock / UnetBasicBlock
+ * (monai/networks/blocks/dynunet_block.py:98-111, :170-185):
+ *   out = act((a - mean_a) * rstd_a + r'),  r' = (r - mean_r) * rstd_r if stats_r, r if only
+ *   r, 0 if r == NULL;  act = LeakyReLU(slope) (slope 1.0 = identity).  out may alias a.  */
+int64_t wf_instnorm_workspace_bytes(int64_t B, int64_t C);
+int wf_instnorm_stats_cl(const float* x, int64_t ldx, int64_t B, int64_t C, int64_t P, float eps,
+                         float* stats, void* workspace, void* stream);
+int wf_norm_act_cl(const float* a, int64_t lda, const float* stats_a, const float* r, int64_t ldr,
+                   const float* stats_r, float* out, int64_t ldo, int64_t B, int64_t C, int64_t P,
+                   float slope, void* stream);
+
 /* ---- a2: relative-position bias ------------------------------------------------------ */
 /* bias[h][i][j] = table[index[i][j]][h]  (attention.py:94-97), index is the int64
  * relative_position_index buffer (N, N), table (T, heads).                                */

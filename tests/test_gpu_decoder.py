@@ -1,0 +1,108 @@
+"""GPU parity of the decoder convolution stack: the channel-last implicit-GEMM
+3x3x3 convolution (csrc/conv3d.hip), the InstanceNorm statistics / fused norm + residual +
+LeakyReLU pass (csrc/instnorm.hip) and the MONAI blocks that use them, against the oracle's
+fp32 PyTorch arithmetic on the CPU (F.conv3d / F.instance_norm / F.leaky_relu, the reference's
+ops, monai/networks/blocks/dynunet_block.py:98-185).
+
+Tolerances: convolution rel-L2 <= 1e-5 in the fp32-faithful bf16x3 mode (operand error 2^-17,
+fp32 accumulation over up to 2592 terms; measured against fp32 CPU convolution), <= 1e-2 in
+plain bf16; InstanceNorm / norm_act rel-L2 <= 1e-6 (fp64 statistics); whole blocks rel-L2
+<= 2e-5 (bf16x3; InstanceNorm renormalises every conv output).  The full model's parity
+(tests/test_gpu_parity.py: full32 / full32hf rel-L2 1e-4, 128^3 and 192^3 Dice) runs through
+these kernels as well.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ref_waveformer as R
+from oracle.weight_rule import seeded_randn
+from tests import cases as C
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from waveformer_amd import _lib
+    _lib.load()
+    yield
+
+
+@pytest.mark.parametrize("prec,tol", [("bf16x3", 1e-5), ("bf16", 1e-2)])
+@pytest.mark.parametrize("B,Cin,Cout,S", [
+    (1, 4, 48, (20, 18, 70)),     # encoder1's first conv (Cin 4), W > 64: two x tiles, ragged
+    (2, 96, 48, (9, 13, 33)),     # decoder conv_block conv1 (2C -> C), W in (32, 64]
+    (1, 48, 48, (8, 5, 17)),      # W in (16, 32]
+    (1, 192, 96, (6, 7, 11)),     # Cout 96 = 2 workgroup column blocks, W <= 16
+    (1, 384, 192, (8, 8, 8)),     # decoder4.conv_lf_block shape
+    (1, 20, 32, (3, 4, 5)),       # Cin not a multiple of 16, Cout not a multiple of 48
+])
+def test_conv3d_k3_vs_cpu(B, Cin, Cout, S, prec, tol):
+    from waveformer_amd import ops
+    x = seeded_randn((B, Cin) + S, 1) * 2 + 0.1
+    w = seeded_randn((Cout, Cin, 3, 3, 3), 2) * (Cin * 27) ** -0.5
+    b = seeded_randn((Cout,), 3)
+    want = F.conv3d(x.double(), w.double(), b.double(), padding=1)
+    with ops.precision(prec):
+        got = ops.conv3d_k3(x.cuda(), w.cuda(), b.cuda())
+    assert got.is_contiguous(memory_format=torch.channels_last_3d)
+    assert C.rel_l2(got, want) <= tol
+
+
+def test_conv3d_k3_channel_slices():
+    """Input = channels [8, 56) of a wider channel-last buffer, output into channels [16, 64)
+    of another: the ld arguments of the C-ABI."""
+    from waveformer_amd import ops
+    xb = seeded_randn((2, 72, 6, 9, 20), 4).cuda().contiguous(memory_format=torch.channels_last_3d)
+    ob = torch.zeros((2, 80, 6, 9, 20), device="cuda").contiguous(
+        memory_format=torch.channels_last_3d)
+    w = (seeded_randn((48, 48, 3, 3, 3), 5) * 0.03).cuda()
+    ops.conv3d_k3(xb[:, 8:56], w, None, out=ob[:, 16:64])
+    want = F.conv3d(xb[:, 8:56].double().cpu(), w.double().cpu(), padding=1)
+    assert C.rel_l2(ob[:, 16:64], want) <= 1e-5
+    assert float(ob[:, :16].abs().max()) == 0.0 and float(ob[:, 64:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("shape", [(2, 48, 16, 16, 16), (1, 4, 7, 9, 5), (3, 96, 4, 4, 4)])
+def test_instnorm_and_norm_act(shape):
+    from waveformer_amd import ops
+    a = (seeded_randn(shape, 6) * 3 + 5).cuda().contiguous(memory_format=torch.channels_last_3d)
+    r = (seeded_randn(shape, 7) - 2).cuda().contiguous(memory_format=torch.channels_last_3d)
+    sa = ops.instnorm_stats(a, 1e-5)
+    sr = ops.instnorm_stats(r, 1e-5)
+    ad, rd = a.double().cpu(), r.double().cpu()
+    na, nr = F.instance_norm(ad, eps=1e-5), F.instance_norm(rd, eps=1e-5)
+    assert C.rel_l2(ops.norm_act(a, sa, slope=1.0), na) <= 1e-6
+    assert C.rel_l2(ops.norm_act(a, sa, r, sr), F.leaky_relu(na + nr, 0.01)) <= 1e-6
+    assert C.rel_l2(ops.norm_act(a, sa, r), F.leaky_relu(na + rd, 0.01)) <= 1e-6
+    out = a.clone(memory_format=torch.channels_last_3d)
+    ops.norm_act(out, ops.instnorm_stats(out, 1e-5), slope=0.01, out=out)  # in place
+    assert C.rel_l2(out, F.leaky_relu(na, 0.01)) <= 1e-6
+
+
+@pytest.mark.parametrize("cin,cout,S", [(4, 48, 24), (96, 48, 16), (48, 48, 12)])
+def test_unet_res_block_fast_path(cin, cout, S):
+    """UnetResBlock (downsample residual when cin != cout) on the HIP path vs the oracle."""
+    from waveformer_amd.blocks import UnetResBlock
+    torch.manual_seed(0)
+    blk = UnetResBlock(3, cin, cout, 3, 1, "instance").eval()
+    sd = {k: v.clone() for k, v in blk.state_dict().items()}
+    x = seeded_randn((1, cin, S, S, S), 8)
+    want = R.unet_res_block(sd, "", x)
+    with torch.no_grad():
+        got = blk.cuda()(x.cuda())
+    assert C.rel_l2(got, want) <= 2e-5
+
+
+def test_unet_basic_block_fast_path():
+    from waveformer_amd.blocks import UnetBasicBlock
+    torch.manual_seed(1)
+    blk = UnetBasicBlock(3, 32, 16, 3, 1, "instance").eval()
+    x = seeded_randn((2, 32, 10, 12, 14), 9)
+    with torch.no_grad():
+        want = blk(x)                      # CPU: the PyTorch modules
+        got = blk.cuda()(x.cuda())         # GPU: the HIP fast path
+    assert C.rel_l2(got, want) <= 2e-5

@@ -33,6 +33,13 @@ SIGNATURES = {
     "wf_dwt3d_fwd": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _I, _P]),
     "wf_idwt3d_level": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _P, _I, _P, _I64, _I64,
                              _P]),
+    "wf_conv3d_k3_packed_elems": (_I64, [_I64, _I64]),
+    "wf_conv3d_k3_pack": (_I, [_P, _P, _I64, _I64, _P]),
+    "wf_conv3d_k3_fwd": (_I, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64,
+                              _I, _P]),
+    "wf_instnorm_workspace_bytes": (_I64, [_I64, _I64]),
+    "wf_instnorm_stats_cl": (_I, [_P, _I64, _I64, _I64, _I64, _F, _P, _P, _P]),
+    "wf_norm_act_cl": (_I, [_P, _I64, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "wf_rel_pos_bias": (_I, [_P, _P, _P, _I64, _I64, _I64, _P]),
     "wf_window_attention_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I]),
     "wf_window_attention_fwd": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P,

@@ -1,10 +1,14 @@
 """Decoder building blocks with the module names / state_dict keys of the MONAI blocks the
 reference uses (vendored MONAI, monai/networks/blocks/{dynunet_block,unetr_block}.py).
 
-These are the decoder's full-resolution 3^3 convolutions ("next"): in this
-round they run as PyTorch-ROCm convolutions (MIOpen) on the GPU; only the wavelet synthesis
-between them (UnetrIDWTBlock) is a waveformer_amd kernel.  norm_name is always "instance"
-(InstanceNorm3d, affine=False) and the activation LeakyReLU(0.01), as Waveformer builds them.
+These are the decoder's full-resolution 3^3 convolutions.  Inference
+(no autograd recording) on the GPU runs UnetResBlock / UnetBasicBlock / Convolution(3^3, stride
+1) on the waveformer_amd kernels, channel-last end to end: the implicit-GEMM MFMA convolution
+(ops.conv3d_k3), InstanceNorm statistics and one fused norm + residual + LeakyReLU pass
+(ops.instnorm_stats / ops.norm_act), the 1x1 residual conv as one GEMM.  Training (autograd)
+and the other layers (transposed / depthwise / 1x1 convs) run as PyTorch-ROCm modules (MIOpen),
+as in the reference.  norm_name is always "instance" (InstanceNorm3d, affine=False) and the
+activation LeakyReLU(0.01), as Waveformer builds them.
 """
 from __future__ import annotations
 
@@ -12,6 +16,31 @@ from typing import Sequence, Tuple, Union
 
 import torch
 import torch.nn as nn
+
+from . import ops
+
+
+def _records_grad(x: torch.Tensor, *mods: nn.Module) -> bool:
+    if not torch.is_grad_enabled():
+        return False
+    return x.requires_grad or any(p.requires_grad for m in mods for p in m.parameters())
+
+
+def _k3_ok(conv: nn.Module, cin: int) -> bool:
+    """A Conv3d the channel-last MFMA kernel implements: 3^3, stride 1, padding 1, dense."""
+    return (type(conv) is nn.Conv3d and conv.kernel_size == (3, 3, 3) and conv.stride == (1, 1, 1)
+            and conv.padding == (1, 1, 1) and conv.dilation == (1, 1, 1) and conv.groups == 1
+            and conv.padding_mode == "zeros" and cin % 4 == 0 and conv.out_channels % 16 == 0)
+
+
+def _in_ok(norm: nn.Module) -> bool:
+    return (type(norm) is nn.InstanceNorm3d and not norm.affine
+            and not norm.track_running_stats)
+
+
+def _fast_ok(x: torch.Tensor, *mods: nn.Module) -> bool:
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 5
+            and not _records_grad(x, *mods))
 
 
 def _norm(norm_name, channels: int) -> nn.Module:
@@ -40,6 +69,12 @@ class Convolution(nn.Sequential):
         else:
             conv = nn.Conv3d(in_channels, out_channels, kernel_size, stride, padding, bias=bias)
         self.add_module("conv", conv)
+
+    def forward(self, x):
+        conv = self.conv
+        if _fast_ok(x, self) and _k3_ok(conv, x.shape[1]):
+            return ops.conv3d_k3(x, conv.weight, conv.bias)
+        return conv(x)
 
 
 def get_conv_layer(spatial_dims: int, in_channels: int, out_channels: int,
@@ -78,7 +113,28 @@ class UnetResBlock(nn.Module):
             self.conv3 = get_conv_layer(spatial_dims, in_channels, out_channels, 1, stride)
             self.norm3 = _norm(norm_name, out_channels)
 
+    def _fast(self, inp) -> bool:
+        c3 = self.conv3.conv if self.downsample else None
+        return (_fast_ok(inp, self) and _k3_ok(self.conv1.conv, inp.shape[1])
+                and _k3_ok(self.conv2.conv, self.conv2.conv.in_channels)
+                and _in_ok(self.norm1) and _in_ok(self.norm2)
+                and (c3 is None or (type(c3) is nn.Conv3d and c3.kernel_size == (1, 1, 1)
+                                    and c3.stride == (1, 1, 1) and _in_ok(self.norm3))))
+
     def forward(self, inp):
+        if self._fast(inp):
+            slope = self.lrelu.negative_slope
+            x = ops.to_cl(inp)
+            h = ops.conv3d_k3(x, self.conv1.conv.weight, self.conv1.conv.bias)
+            ops.norm_act(h, ops.instnorm_stats(h, self.norm1.eps), slope=slope, out=h)
+            out = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias)
+            s2 = ops.instnorm_stats(out, self.norm2.eps)
+            if self.downsample:
+                c3 = self.conv3.conv
+                res = ops.conv1x1_cl(x, c3.weight, c3.bias)
+                return ops.norm_act(out, s2, res, ops.instnorm_stats(res, self.norm3.eps),
+                                    slope=slope, out=out)
+            return ops.norm_act(out, s2, x, slope=slope, out=out)
         out = self.lrelu(self.norm1(self.conv1(inp)))
         out = self.norm2(self.conv2(out))
         res = self.norm3(self.conv3(inp)) if self.downsample else inp
@@ -98,6 +154,14 @@ class UnetBasicBlock(nn.Module):
         self.norm2 = _norm(norm_name, out_channels)
 
     def forward(self, inp):
+        if (_fast_ok(inp, self) and _k3_ok(self.conv1.conv, inp.shape[1])
+                and _k3_ok(self.conv2.conv, self.conv2.conv.in_channels)
+                and _in_ok(self.norm1) and _in_ok(self.norm2)):
+            slope = self.lrelu.negative_slope
+            h = ops.conv3d_k3(inp, self.conv1.conv.weight, self.conv1.conv.bias)
+            ops.norm_act(h, ops.instnorm_stats(h, self.norm1.eps), slope=slope, out=h)
+            out = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias)
+            return ops.norm_act(out, ops.instnorm_stats(out, self.norm2.eps), slope=slope, out=out)
         out = self.lrelu(self.norm1(self.conv1(inp)))
         return self.lrelu(self.norm2(self.conv2(out)))
 

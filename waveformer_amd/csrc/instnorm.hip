@@ -1,0 +1,156 @@
+// instnorm.hip -- InstanceNorm3d (affine=False, biased variance) + LeakyReLU + residual on
+// channel-last activations: the norm / act / add glue of MONAI's UnetResBlock and
+// UnetBasicBlock (monai/networks/blocks/dynunet_block.py:98-111, :170-185) around the
+// decoder's 3x3x3 convolutions (conv3d.hip).
+//
+//   stats:  per (b, c): mean and rstd = 1 / sqrt(var + eps) over the D*H*W positions of
+//           sample b.  Sums and sums of squares accumulate in fp64 (per thread, then per
+//           workgroup, then one fp64 atomic per channel and workgroup), so E[x^2] - mean^2
+//           loses nothing against PyTorch's fp32 Welford.
+//   apply:  out = act((a - mean_a) * rstd_a + r'), r' = (r - mean_r) * rstd_r (norm3 of the
+//           1x1 residual), r itself, or 0; act = LeakyReLU(slope) (slope 1 = identity).
+// Both are one streaming pass over the tensor (HBM roofline).
+#include "wf_common.hpp"
+
+namespace wf {
+
+// grid (chunks, B); block 256 = R rows x C4 channel groups (R = 256 / C4)
+__global__ __launch_bounds__(256) void instnorm_partial_kernel(
+    const float* __restrict__ x, int64_t ldx, int C, int64_t P, int64_t chunk,
+    double* __restrict__ acc) {
+  extern __shared__ double red[];  // [R][C4][8]
+  const int C4 = C >> 2;
+  const int R = 256 / C4;
+  const int tid = threadIdx.x;
+  const int row = tid / C4, g = tid - row * C4;
+  const int b = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * chunk;
+  const int64_t p1 = min(P, p0 + chunk);
+  double s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+  if (row < R) {
+    const float* base = x + ((int64_t)b * P) * ldx + 4 * g;
+    for (int64_t p = p0 + row; p < p1; p += R) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(base + p * ldx);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double d = (double)v[j];
+        s[j] += d;
+        q[j] += d * d;
+      }
+    }
+    double* r = red + ((int64_t)row * C4 + g) * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      r[j] = s[j];
+      r[4 + j] = q[j];
+    }
+  }
+  __syncthreads();
+  // one thread per (channel, moment): sum the R rows, one atomic
+  for (int i = tid; i < C * 2; i += blockDim.x) {
+    const int c = i >> 1, mom = i & 1;
+    const int gg = c >> 2, j = c & 3;
+    double t = 0;
+    for (int rr = 0; rr < R; ++rr) t += red[((int64_t)rr * C4 + gg) * 8 + 4 * mom + j];
+    atomicAdd(acc + ((int64_t)b * C + c) * 2 + mom, t);
+  }
+}
+
+__global__ void instnorm_finalize_kernel(const double* __restrict__ acc, float* __restrict__ stats,
+                                         int B, int C, int64_t P, float eps) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i - b * C;
+  const double n = (double)P;
+  const double mean = acc[2 * i] / n;
+  double var = acc[2 * i + 1] / n - mean * mean;
+  if (var < 0) var = 0;
+  stats[(int64_t)(b * 2) * C + c] = (float)mean;
+  stats[(int64_t)(b * 2 + 1) * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// one thread per (position, 4 channels)
+__global__ __launch_bounds__(256) void norm_act_kernel(
+    const float* __restrict__ a, int64_t lda, const float* __restrict__ sa,
+    const float* __restrict__ r, int64_t ldr, const float* __restrict__ sr,
+    float* __restrict__ out, int64_t ldo, int C, int64_t P, int64_t total, float slope) {
+  const int C4 = C >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pos = i / C4;  // over B * P
+    const int c = 4 * (int)(i - pos * C4);
+    const int b = (int)(pos / P);
+    const f32x4 av = *reinterpret_cast<const f32x4*>(a + pos * lda + c);
+    const f32x4 ma = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b) * C + c);
+    const f32x4 ra = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b + 1) * C + c);
+    f32x4 v = (av - ma) * ra;
+    if (r) {
+      f32x4 rv = *reinterpret_cast<const f32x4*>(r + pos * ldr + c);
+      if (sr) {
+        const f32x4 mr = *reinterpret_cast<const f32x4*>(sr + (int64_t)(2 * b) * C + c);
+        const f32x4 rr = *reinterpret_cast<const f32x4*>(sr + (int64_t)(2 * b + 1) * C + c);
+        rv = (rv - mr) * rr;
+      }
+      v += rv;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = v[j] >= 0.f ? v[j] : v[j] * slope;
+    *reinterpret_cast<f32x4*>(out + pos * ldo + c) = v;
+  }
+}
+
+}  // namespace wf
+
+using namespace wf;
+
+extern "C" int64_t wf_instnorm_workspace_bytes(int64_t B, int64_t C) {
+  return B * C * 2 * (int64_t)sizeof(double);
+}
+
+extern "C" int wf_instnorm_stats_cl(const float* x, int64_t ldx, int64_t B, int64_t C,
+                                    int64_t P, float eps, float* stats, void* workspace,
+                                    void* stream) {
+  WF_REQUIRE(B >= 1 && P >= 1, "empty tensor");
+  WF_REQUIRE(C >= 4 && C % 4 == 0 && C <= 1024 && ldx >= C && ldx % 4 == 0,
+             "C must be a multiple of 4 in [4, 1024] with ldx >= C, ldx % 4 == 0");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(stats);
+  WF_REQUIRE_PTR(workspace);
+  hipStream_t s = (hipStream_t)stream;
+  double* acc = reinterpret_cast<double*>(workspace);
+  if (hipMemsetAsync(acc, 0, (size_t)(B * C * 2) * sizeof(double), s) != hipSuccess)
+    return check_launch("wf_instnorm_stats_cl (memset)");
+  const int C4 = (int)(C / 4);
+  const int R = 256 / C4;
+  // ~1024 workgroups over the batch, at least 4 rows per thread
+  int64_t chunks = cdiv(1024, B);
+  int64_t chunk = cdiv(P, chunks);
+  if (chunk < 4 * R) chunk = 4 * R;
+  chunks = cdiv(P, chunk);
+  const size_t lds = (size_t)R * C4 * 8 * sizeof(double);
+  hipLaunchKernelGGL(instnorm_partial_kernel, dim3((unsigned)chunks, (unsigned)B), dim3(256), lds,
+                     s, x, ldx, (int)C, P, chunk, acc);
+  int rc = check_launch("wf_instnorm_stats_cl");
+  if (rc) return rc;
+  hipLaunchKernelGGL(instnorm_finalize_kernel, dim3((unsigned)cdiv(B * C, 256)), dim3(256), 0, s,
+                     acc, stats, (int)B, (int)C, P, eps);
+  return check_launch("wf_instnorm_stats_cl (finalize)");
+}
+
+extern "C" int wf_norm_act_cl(const float* a, int64_t lda, const float* stats_a, const float* r,
+                              int64_t ldr, const float* stats_r, float* out, int64_t ldo,
+                              int64_t B, int64_t C, int64_t P, float slope, void* stream) {
+  WF_REQUIRE(B >= 1 && P >= 1, "empty tensor");
+  WF_REQUIRE(C >= 4 && C % 4 == 0 && lda >= C && lda % 4 == 0 && ldo >= C && ldo % 4 == 0 &&
+             (!r || (ldr >= C && ldr % 4 == 0)),
+             "C must be a multiple of 4 and every ld >= C, a multiple of 4");
+  WF_REQUIRE_PTR(a);
+  WF_REQUIRE_PTR(stats_a);
+  WF_REQUIRE_PTR(out);
+  const int64_t total = B * P * (C / 4);
+  int64_t blocks = cdiv(total, 256);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(norm_act_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     a, lda, stats_a, r, ldr, stats_r, out, ldo, (int)C, P, total, slope);
+  return check_launch("wf_norm_act_cl");
+}

@@ -154,7 +154,8 @@ class Waveformer(nn.Module):
         up4 = self.learnable_up4(dec4)
         up3 = self.learnable_up3(dec3)
         dec1 = self.decoder1(torch.cat([up4, up3, dec2], dim=1), enc0)
-        return self.out(dec1)
+        # the HIP decoder path is channel-last; hand the caller the reference's NCDHW layout
+        return self.out(dec1).contiguous()
 
 
 def create_waveformer(network_config: dict) -> Waveformer:

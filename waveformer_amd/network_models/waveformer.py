@@ -113,9 +113,9 @@ class MultiscaleTransformer(nn.Module):
         pe = self.patch_embed.proj
         train = wfa.needs_grad(x_rgb, *self.parameters())
         if train:
-            x = wfa.PatchEmbedFn.apply(x_rgb.contiguous(), pe.weight, pe.bias)
+            x = wfa.PatchEmbedFn.apply(x_rgb.contiguous(), pe.weight.contiguous(), pe.bias)
         else:
-            x = ops.patch_embed(x_rgb.contiguous(), pe.weight, pe.bias)
+            x = ops.patch_embed(x_rgb.contiguous(), pe.weight.contiguous(), pe.bias)
         outs, outs_hf = [], []
         for s in range(4):
             if s > 0:

@@ -331,6 +331,128 @@ def waverec3(coeffs: Sequence, wavelet: str, out: Optional[torch.Tensor] = None)
 
 
 # ------------------------------------------------------------------------------------------
+# decoder convolution stack: channel-last 3x3x3 conv, InstanceNorm, act
+# ------------------------------------------------------------------------------------------
+def cl_ld(x: torch.Tensor) -> Optional[int]:
+    """Position stride of an NCDHW-shaped tensor stored channel-last (a channels_last_3d
+    tensor or a channel slice of one), or None if it is not laid out that way."""
+    if x.dim() != 5:
+        return None
+    B, C, D, H, W = x.shape
+    s = x.stride()
+    ld = s[4] if W > 1 else (s[3] if H > 1 else (s[2] if D > 1 else max(C, 1)))
+    if (C > 1 and s[1] != 1) or ld < C or ld % 4 or x.data_ptr() % 16:
+        return None
+    if (W > 1 and s[4] != ld) or (H > 1 and s[3] != W * ld) or (D > 1 and s[2] != H * W * ld):
+        return None
+    if B > 1 and s[0] != D * H * W * ld:
+        return None
+    return ld
+
+
+def to_cl(x: torch.Tensor) -> torch.Tensor:
+    """x itself if it is channel-last already, else a channels_last_3d copy."""
+    return x if cl_ld(x) is not None else x.contiguous(memory_format=torch.channels_last_3d)
+
+
+def empty_cl(B: int, C: int, D: int, H: int, W: int, device) -> torch.Tensor:
+    return torch.empty((B, C, D, H, W), dtype=torch.float32, device=device,
+                       memory_format=torch.channels_last_3d)
+
+
+def conv3d_k3_packed(weight: torch.Tensor) -> torch.Tensor:
+    """[2][K-steps][Cout][32] bf16 hi / lo planes of a (Cout, Cin, 3, 3, 3) conv weight
+    (wf_conv3d_k3_pack), cached on the parameter until it changes."""
+    ver = weight._version
+    ent = getattr(weight, "_wf_conv3", None)
+    if ent is not None and ent[0] == ver and ent[1] == weight.data_ptr():
+        return ent[2]
+    w = weight.detach()
+    _check(w, "conv weight")
+    Cout, Cin = w.shape[:2]
+    n = _lib.query("wf_conv3d_k3_packed_elems", Cin, Cout)
+    out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    _lib.call("wf_conv3d_k3_pack", w.data_ptr(), out.data_ptr(), Cin, Cout, _stream())
+    weight._wf_conv3 = (ver, weight.data_ptr(), out)
+    return out
+
+
+def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Conv3d(k=3, stride 1, padding 1) of an NCDHW-shaped fp32 tensor on the MFMA implicit-GEMM
+    kernel; the result is channels_last_3d (or written into `out`, a channel-last view)."""
+    _check(x, "x", contiguous=False)
+    x = to_cl(x)
+    B, Cin, D, H, W = x.shape
+    Cout = weight.shape[0]
+    if tuple(weight.shape) != (Cout, Cin, 3, 3, 3):
+        raise ValueError(f"conv3d_k3: weight {tuple(weight.shape)} does not fit Cin={Cin}")
+    if bias is not None:
+        _check(bias, "bias")
+    if out is None:
+        out = empty_cl(B, Cout, D, H, W, x.device)
+    ldo = cl_ld(out)
+    if ldo is None or tuple(out.shape) != (B, Cout, D, H, W):
+        raise ValueError("conv3d_k3: out must be a channel-last (B, Cout, D, H, W) tensor")
+    _lib.call("wf_conv3d_k3_fwd", x.data_ptr(), cl_ld(x), conv3d_k3_packed(weight).data_ptr(),
+              _ptr(bias), out.data_ptr(), ldo, B, Cin, Cout, D, H, W, _prec(), _stream())
+    return out
+
+
+def conv1x1_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None
+               ) -> torch.Tensor:
+    """1x1x1 Conv3d of a channel-last tensor as one fp32 GEMM over its position rows."""
+    x = to_cl(x)
+    B, Cin, D, H, W = x.shape
+    Cout = weight.shape[0]
+    rows = x.permute(0, 2, 3, 4, 1).reshape(-1, Cin)
+    w2 = weight.reshape(Cout, Cin)
+    y = torch.addmm(bias, rows, w2.t()) if bias is not None else torch.mm(rows, w2.t())
+    return y.view(B, D, H, W, Cout).permute(0, 4, 1, 2, 3)
+
+
+def instnorm_stats(x: torch.Tensor, eps: float) -> torch.Tensor:
+    """(B, 2, C) {mean, rstd} of InstanceNorm3d(affine=False) over a channel-last tensor."""
+    ld = cl_ld(x)
+    if ld is None:
+        raise ValueError("instnorm_stats: channel-last input expected")
+    B, C = x.shape[:2]
+    P = x.shape[2] * x.shape[3] * x.shape[4]
+    stats = torch.empty((B, 2, C), dtype=torch.float32, device=x.device)
+    ws = torch.empty(_lib.query("wf_instnorm_workspace_bytes", B, C), dtype=torch.uint8,
+                     device=x.device)
+    _lib.call("wf_instnorm_stats_cl", x.data_ptr(), ld, B, C, P, float(eps), stats.data_ptr(),
+              ws.data_ptr(), _stream())
+    return stats
+
+
+def norm_act(a: torch.Tensor, stats_a: torch.Tensor, r: Optional[torch.Tensor] = None,
+             stats_r: Optional[torch.Tensor] = None, slope: float = 0.01,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """act((a - mean) * rstd + r') on channel-last tensors (UnetResBlock's norm / add / lrelu);
+    r' = InstanceNorm(r) with stats_r, r, or nothing.  `out` may be `a` (in place)."""
+    lda = cl_ld(a)
+    if lda is None:
+        raise ValueError("norm_act: channel-last input expected")
+    B, C = a.shape[:2]
+    P = a.shape[2] * a.shape[3] * a.shape[4]
+    ldr = 0
+    if r is not None:
+        r = to_cl(r)
+        if tuple(r.shape) != tuple(a.shape):
+            raise ValueError(f"norm_act: residual {tuple(r.shape)} vs {tuple(a.shape)}")
+        ldr = cl_ld(r)
+    if out is None:
+        out = empty_cl(*a.shape, device=a.device)
+    ldo = cl_ld(out)
+    if ldo is None or tuple(out.shape) != tuple(a.shape):
+        raise ValueError("norm_act: out must be channel-last and shaped like a")
+    _lib.call("wf_norm_act_cl", a.data_ptr(), lda, stats_a.data_ptr(), _ptr(r), ldr,
+              _ptr(stats_r), out.data_ptr(), ldo, B, C, P, float(slope), _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
 # a2/a3: attention
 # ------------------------------------------------------------------------------------------
 def rel_pos_bias(table: torch.Tensor, index: torch.Tensor) -> torch.Tensor:
