@@ -143,6 +143,13 @@ int wf_norm_act_cl(const float* a, int64_t lda, const float* stats_a, const floa
                    const float* stats_r, float* out, int64_t ldo, int64_t B, int64_t C, int64_t P,
                    float slope, void* stream);
 
+/* nn.Upsample(scale_factor=s, mode='trilinear', align_corners) of a channel-last tensor
+ * (B, d, h, w, C) -> (B, D, H, W, C), PyTorch's upsample_trilinear3d index arithmetic: the
+ * decoder's ProjectionUpsample (network_models/wave_helper.py:33-81, align_corners=True).    */
+int wf_upsample_trilinear_cl(const float* in, float* out, int64_t B, int64_t C, int64_t d,
+                             int64_t h, int64_t w, int64_t D, int64_t H, int64_t W,
+                             int align_corners, void* stream);
+
 /* ---- a2: relative-position bias ------------------------------------------------------ */
 /* bias[h][i][j] = table[index[i][j]][h]  (attention.py:94-97), index is the int64
  * relative_position_index buffer (N, N), table (T, heads).                                */

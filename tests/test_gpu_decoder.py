@@ -106,3 +106,33 @@ def test_unet_basic_block_fast_path():
         want = blk(x)                      # CPU: the PyTorch modules
         got = blk.cuda()(x.cuda())         # GPU: the HIP fast path
     assert C.rel_l2(got, want) <= 2e-5
+
+
+@pytest.mark.parametrize("ac", [True, False])
+@pytest.mark.parametrize("src,dst", [((4, 5, 6), (16, 20, 24)), ((8, 8, 8), (16, 16, 16)),
+                                     ((3, 1, 7), (5, 4, 14))])
+def test_upsample_cl_vs_interpolate(src, dst, ac):
+    from waveformer_amd import ops
+    x = seeded_randn((2, 12) + src, 10)
+    want = F.interpolate(x, size=dst, mode="trilinear", align_corners=ac)
+    got = ops.upsample_cl(x.cuda(), dst, ac)
+    assert C.rel_l2(got, want) <= 1e-6
+
+
+@pytest.mark.parametrize("cin,cout,stride,double", [(192, 48, 4, True), (96, 48, 2, False)])
+def test_projection_upsample_fast_path(cin, cout, stride, double):
+    """learnable_up4 / learnable_up3 (wave_helper.py:33-81) on the HIP path (channel-last
+    upsample + depthwise conv + folded GroupNorm + GEMMs, residual 1x1 conv before its
+    upsample) vs the PyTorch modules on the CPU.  fp32 throughout: rel-L2 <= 1e-5."""
+    from waveformer_amd.network_models.wave_helper import ProjectionUpsample
+    torch.manual_seed(2)
+    m = ProjectionUpsample(cin, cout, stride=stride, residual=True, use_double_conv=double).eval()
+    with torch.no_grad():
+        for p in m.parameters():   # non-trivial GroupNorm affine
+            p.add_(0.05 * torch.randn_like(p))
+    x = seeded_randn((2, cin, 6, 5, 7), 11)
+    with torch.no_grad():
+        want = m(x)
+        got = m.cuda()(x.cuda())
+    assert tuple(got.shape) == tuple(want.shape)
+    assert C.rel_l2(got, want) <= 1e-5

@@ -1,0 +1,83 @@
+// upsample.hip -- channel-last trilinear resampling for the decoder's ProjectionUpsample
+// (network_models/wave_helper.py:33-81: nn.Upsample(scale_factor=stride, mode='trilinear',
+// align_corners=True) in front of its depthwise conv and of its 1x1 residual conv).
+//
+// Index arithmetic is PyTorch's upsample_trilinear3d (area_pixel_compute_scale /
+// area_pixel_compute_source_index, fp32): align_corners=True: src = dst * (in-1)/(out-1);
+// False: src = max((dst + 0.5) * in/out - 0.5, 0).  i0 = (int)src, i1 = i0 + (i0 < in-1),
+// l1 = src - i0, l0 = 1 - l1, combined in PyTorch's order t0 * (h0 * (w0 a + w1 b) + h1 * (..))
+// + t1 * (..).  One thread per (output position, 4 channels): the 8 source rows are L2-resident
+// (the source is 8-64x smaller than the output), the output is written once (HBM roofline).
+#include "wf_common.hpp"
+
+namespace wf {
+
+struct Src1 {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ Src1 src_index(int dst, int in, int out, bool ac) {
+  Src1 s;
+  float r;
+  if (ac) {
+    const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+    r = scale * (float)dst;
+  } else {
+    const float scale = (float)in / (float)out;
+    r = fmaxf(scale * ((float)dst + 0.5f) - 0.5f, 0.f);
+  }
+  s.i0 = (int)r;
+  s.i1 = s.i0 + (s.i0 < in - 1 ? 1 : 0);
+  s.l1 = r - (float)s.i0;
+  s.l0 = 1.f - s.l1;
+  return s;
+}
+
+__global__ __launch_bounds__(256) void upsample_cl_kernel(const float* __restrict__ in,
+                                                          float* __restrict__ out, int C, int d,
+                                                          int h, int w, int D, int H, int W,
+                                                          int64_t total, int ac) {
+  const int C4 = C >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = 4 * (int)(i % C4);
+    int64_t t = i / C4;
+    const int x = (int)(t % W);
+    t /= W;
+    const int y = (int)(t % H);
+    t /= H;
+    const int z = (int)(t % D);
+    const int64_t b = t / D;
+    const Src1 sz = src_index(z, d, D, ac), sy = src_index(y, h, H, ac), sx = src_index(x, w, W, ac);
+    const float* base = in + b * ((int64_t)d * h * w * C) + c;
+    auto at = [&](int zz, int yy, int xx) {
+      return *reinterpret_cast<const f32x4*>(base + (((int64_t)zz * h + yy) * w + xx) * C);
+    };
+    const f32x4 v0 = sy.l0 * (sx.l0 * at(sz.i0, sy.i0, sx.i0) + sx.l1 * at(sz.i0, sy.i0, sx.i1)) +
+                     sy.l1 * (sx.l0 * at(sz.i0, sy.i1, sx.i0) + sx.l1 * at(sz.i0, sy.i1, sx.i1));
+    const f32x4 v1 = sy.l0 * (sx.l0 * at(sz.i1, sy.i0, sx.i0) + sx.l1 * at(sz.i1, sy.i0, sx.i1)) +
+                     sy.l1 * (sx.l0 * at(sz.i1, sy.i1, sx.i0) + sx.l1 * at(sz.i1, sy.i1, sx.i1));
+    *reinterpret_cast<f32x4*>(out + i * 4) = sz.l0 * v0 + sz.l1 * v1;
+  }
+}
+
+}  // namespace wf
+
+using namespace wf;
+
+extern "C" int wf_upsample_trilinear_cl(const float* in, float* out, int64_t B, int64_t C,
+                                        int64_t d, int64_t h, int64_t w, int64_t D, int64_t H,
+                                        int64_t W, int align_corners, void* stream) {
+  WF_REQUIRE(B >= 1 && d >= 1 && h >= 1 && w >= 1 && D >= 1 && H >= 1 && W >= 1, "empty tensor");
+  WF_REQUIRE(C >= 4 && C % 4 == 0, "C must be a positive multiple of 4");
+  WF_REQUIRE_PTR(in);
+  WF_REQUIRE_PTR(out);
+  const int64_t total = B * D * H * W * (C / 4);
+  int64_t blocks = cdiv(total, 256);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(upsample_cl_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     in, out, (int)C, (int)d, (int)h, (int)w, (int)D, (int)H, (int)W, total,
+                     align_corners);
+  return check_launch("wf_upsample_trilinear_cl");
+}

@@ -88,9 +88,57 @@ class ProjectionUpsample(nn.Module):
                 nn.Conv3d(in_channels, out_channels, kernel_size=1))
         self.act = nn.GELU()
 
+    def _fast(self, x) -> bool:
+        dw = self.conv1[1]
+        return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 5
+                and not (torch.is_grad_enabled() and (
+                    x.requires_grad or any(p.requires_grad for p in self.parameters())))
+                and x.shape[1] % 4 == 0 and dw.kernel_size == (3, 3, 3) and dw.padding == (1, 1, 1)
+                and self.norm.num_groups == self.norm.num_channels and self.norm.affine
+                and type(self.act) is nn.GELU and self.act.approximate == "none")
+
     def forward(self, x):
+        if self._fast(x):
+            return self._forward_hip(x)
         y = self.conv3(self.act(self.conv2(self.norm(self.conv1(x)))))
         return y + self.res_conv(x) if self.do_res else y
+
+    def _forward_hip(self, x):
+        """Inference path, channel-last: HIP trilinear upsample (align_corners=True) + HIP
+        depthwise conv + HIP per-channel GroupNorm statistics; GroupNorm's normalisation and
+        affine are folded into conv2's weights per sample, so conv2 / conv3 are plain fp32
+        GEMMs over the position rows (hipBLASLt).  The residual's 1x1 conv runs BEFORE the
+        upsample (both are linear and the trilinear weights sum to 1, so W.Up(x) + b =
+        Up(W.x + b)): the GEMM is 8x / 64x smaller and only Cout channels are resampled."""
+        B, C, d, h, w = x.shape
+        size = (d * self.stride, h * self.stride, w * self.stride)
+        P = size[0] * size[1] * size[2]
+        xc = ops.to_cl(x)
+        dw = self.conv1[1]
+        y = ops.dwconv3d_cl(ops.upsample_cl(xc, size, True), dw.weight, dw.bias)
+        st = ops.instnorm_stats(y, self.norm.eps)                       # (B, 2, C)
+        scale = st[:, 1] * self.norm.weight                              # (B, C)
+        shift = self.norm.bias - st[:, 0] * scale
+        w2 = self.conv2.weight.reshape(2 * C, C)
+        w2s = w2.unsqueeze(0) * scale.unsqueeze(1)                       # (B, 2C, C)
+        b2s = torch.addmm(self.conv2.bias.unsqueeze(0), shift, w2.t())   # (B, 2C)
+        rows = y.permute(0, 2, 3, 4, 1).reshape(B, P, C)
+        hid = F.gelu(torch.baddbmm(b2s.unsqueeze(1), rows, w2s.transpose(1, 2)))
+        hid = hid.reshape(B * P, 2 * C)
+        if self.use_double_conv:
+            c3a, c3b = self.conv3[0], self.conv3[2]
+            hid = F.gelu(torch.addmm(c3a.bias, hid, c3a.weight.reshape(c3a.out_channels, -1).t()))
+            out = torch.addmm(c3b.bias, hid, c3b.weight.reshape(c3b.out_channels, -1).t())
+        else:
+            c3 = self.conv3
+            out = torch.addmm(c3.bias, hid, c3.weight.reshape(c3.out_channels, -1).t())
+        Cout = out.shape[1]
+        out = out.view(B, size[0], size[1], size[2], Cout).permute(0, 4, 1, 2, 3)
+        if self.do_res:
+            rc = self.res_conv[1]
+            r = ops.conv1x1_cl(xc, rc.weight, rc.bias)
+            out = out + ops.upsample_cl(r, size, True)
+        return out
 
 
 class DWConv(nn.Module):

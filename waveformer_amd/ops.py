@@ -411,6 +411,33 @@ def conv1x1_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tenso
     return y.view(B, D, H, W, Cout).permute(0, 4, 1, 2, 3)
 
 
+def upsample_cl(x: torch.Tensor, size: Sequence[int], align_corners: bool) -> torch.Tensor:
+    """F.interpolate(x, size, mode='trilinear', align_corners) of a channel-last tensor
+    (wf_upsample_trilinear_cl); the result is channels_last_3d."""
+    x = x if (cl_ld(x) == x.shape[1]) else x.contiguous(memory_format=torch.channels_last_3d)
+    B, C, d, h, w = x.shape
+    D, H, W = size
+    out = empty_cl(B, C, D, H, W, x.device)
+    _lib.call("wf_upsample_trilinear_cl", x.data_ptr(), out.data_ptr(), B, C, d, h, w, D, H, W,
+              int(bool(align_corners)), _stream())
+    return out
+
+
+def dwconv3d_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """Depthwise Conv3d(C, C, 3, padding=1, groups=C) of a dense channel-last tensor."""
+    x = x if (cl_ld(x) == x.shape[1]) else x.contiguous(memory_format=torch.channels_last_3d)
+    B, C, D, H, W = x.shape
+    if tuple(weight.shape) != (C, 1, 3, 3, 3):
+        raise ValueError(f"dwconv3d_cl: weight {tuple(weight.shape)} is not ({C},1,3,3,3)")
+    _check(weight, "weight")
+    if bias is not None:
+        _check(bias, "bias")
+    out = empty_cl(B, C, D, H, W, x.device)
+    _lib.call("wf_dwconv3d_cl", x.data_ptr(), weight.data_ptr(), _ptr(bias), 0, out.data_ptr(),
+              B, C, D, H, W, _stream())
+    return out
+
+
 def instnorm_stats(x: torch.Tensor, eps: float) -> torch.Tensor:
     """(B, 2, C) {mean, rstd} of InstanceNorm3d(affine=False) over a channel-last tensor."""
     ld = cl_ld(x)
