@@ -136,3 +136,18 @@ def test_projection_upsample_fast_path(cin, cout, stride, double):
         got = m.cuda()(x.cuda())
     assert tuple(got.shape) == tuple(want.shape)
     assert C.rel_l2(got, want) <= 1e-5
+
+
+def test_unetr_up_block_fast_path():
+    """decoder1 (monai UnetrUpBlock, unetr_block.py:22-86): ConvTranspose3d(k2, s2) as a GEMM
+    scattered into the channel-last concatenation buffer, then the UnetResBlock, vs the CPU
+    modules."""
+    from waveformer_amd.blocks import UnetrUpBlock
+    torch.manual_seed(3)
+    m = UnetrUpBlock(3, 144, 48, 3, 2, "instance", res_block=True).eval()
+    x = seeded_randn((2, 144, 5, 6, 7), 12)
+    skip = seeded_randn((2, 48, 10, 12, 14), 13)
+    with torch.no_grad():
+        want = m(x, skip)
+        got = m.cuda()(x.cuda(), skip.cuda())
+    assert C.rel_l2(got, want) <= 2e-5

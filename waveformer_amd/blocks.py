@@ -204,8 +204,34 @@ class UnetrUpBlock(nn.Module):
                               norm_name)
 
     def forward(self, inp, skip):
+        tc = self.transp_conv.conv
+        if (_fast_ok(inp, self) and type(tc) is nn.ConvTranspose3d and tc.kernel_size == (2, 2, 2)
+                and tc.stride == (2, 2, 2) and tc.padding == (0, 0, 0)
+                and tc.output_padding == (0, 0, 0) and tc.groups == 1 and tc.dilation == (1, 1, 1)):
+            return self.conv_block(self._upsample_cat(inp, skip, tc))
         out = self.transp_conv(inp)
         return self.conv_block(torch.cat((out, skip), dim=1))
+
+    @staticmethod
+    def _upsample_cat(inp, skip, tc):
+        """ConvTranspose3d(k=2, s=2) + torch.cat((out, skip), 1) into one channel-last buffer:
+        the transposed conv is one fp32 GEMM (positions x Cin) . (Cin x 8 Cout) whose columns
+        are the 8 sub-voxels, scattered straight into the buffer's first Cout channels."""
+        B, Cin, d, h, w = inp.shape
+        Cout = tc.out_channels
+        if tuple(skip.shape) != (B, skip.shape[1], 2 * d, 2 * h, 2 * w):
+            raise ValueError(f"skip {tuple(skip.shape)} does not match the up-sampled input")
+        buf = ops.empty_cl(B, Cout + skip.shape[1], 2 * d, 2 * h, 2 * w, inp.device)
+        rows = ops.to_cl(inp).permute(0, 2, 3, 4, 1).reshape(-1, Cin)
+        wr = tc.weight.permute(0, 2, 3, 4, 1).reshape(Cin, 8 * Cout)
+        g = rows @ wr
+        if tc.bias is not None:
+            g = g + tc.bias.repeat(8)
+        dst = buf.permute(0, 2, 3, 4, 1)[..., :Cout]
+        dst = dst.unflatten(3, (w, 2)).unflatten(2, (h, 2)).unflatten(1, (d, 2))
+        dst.permute(0, 1, 3, 5, 2, 4, 6, 7).copy_(g.view(B, d, h, w, 2, 2, 2, Cout))
+        buf[:, Cout:].copy_(skip)
+        return buf
 
 
 class PatchEmbed(nn.Module):

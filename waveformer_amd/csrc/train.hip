@@ -983,6 +983,11 @@ extern "C" int wf_dwconv3d_cl(const float* in, const float* w, const float* bias
   WF_REQUIRE_PTR(in);
   WF_REQUIRE_PTR(w);
   WF_REQUIRE_PTR(out);
+  // the forward orientation with a bias and 32-channel groups: the z-streaming LDS-tiled
+  // kernel of CCF_FFN (ffn.hip); the flipped (input-gradient) form keeps the simple one
+  if (!flip && bias && C % 32 == 0)
+    return launch_dwconv3d(in, w, bias, out, nullptr, (int)B, (int)C, (int)D, (int)H, (int)W,
+                           PREC_SPLIT, (hipStream_t)stream);
   const int64_t n = B * D * H * W * (C / 4);
   hipLaunchKernelGGL(dwconv_cl_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, in, w,
                      bias, flip, out, (int)B, (int)C, (int)D, (int)H, (int)W);
