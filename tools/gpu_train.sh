@@ -12,5 +12,5 @@ timeout -k 10 600 python -u -m pytest tests/test_train_grads.py -x -v --timeout 
 rc=$?
 tail -25 gpurun_out/${TAG}_pytest.txt
 if [ $rc -gt 1 ]; then echo "pytest rc=$rc"; exit $rc; fi
-timeout -k 10 400 python -u bench.py --workload train --steps 3 --warmup 2 --batch $BATCH > gpurun_out/${TAG}_train.json 2> gpurun_out/${TAG}_train.err || { tail -30 gpurun_out/${TAG}_train.err; exit 1; }
+timeout -k 10 900 python -u bench.py --workload train --steps 3 --warmup 2 --batch $BATCH > gpurun_out/${TAG}_train.json 2> gpurun_out/${TAG}_train.err || { tail -30 gpurun_out/${TAG}_train.err; exit 1; }
 cat gpurun_out/${TAG}_train.json

@@ -23,6 +23,8 @@
 // Precision as everywhere (include/waveformer_hip.h): SPLIT = hi*hi + lo*hi + hi*lo (fp32-
 // faithful), else plain bf16 operands; accumulation fp32.
 // Roofline: MFMA (2 * 27 * Cin * Cout flops per position; 432 flop/B at Cin 96, Cout 48).
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace wf {
@@ -39,6 +41,8 @@ struct Conv3Args {
   int B, D, H, W, Cin, Cout, nch;
   int tiles_x, tiles_y;
   int64_t nblocks;
+  int ksplit;         // > 1: blockIdx.z takes chunks [z*nch/ksplit, (z+1)*nch/ksplit) and the
+                      // epilogue atomically adds into a zeroed output (small grids only)
 };
 
 template <int CO_T, int NT, bool SPLIT>
@@ -72,7 +76,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
     for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0, 0, 0, 0};
 
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int nsteps = a.nch * kConvKS;
+  const int ch_begin = (int)(((int64_t)blockIdx.z * a.nch) / a.ksplit);
+  const int ch_end = (int)(((int64_t)(blockIdx.z + 1) * a.nch) / a.ksplit);
+  const int nsteps = ch_end * kConvKS;
   // A fragment of step s for channel tile m: W[s][co0 + 16m + l15][8 g4 .. 8 g4 + 7]
   auto wptr = [&](int s, int m) {
     return a.w + ((int64_t)s * a.Cout + co0 + 16 * m + l15) * 32 + 8 * g4;
@@ -80,11 +86,12 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   bf16x8 wh[CO_T], wl[CO_T];
 #pragma unroll
   for (int m = 0; m < CO_T; ++m) {
-    wh[m] = *reinterpret_cast<const bf16x8*>(wptr(0, m));
-    wl[m] = SPLIT ? *reinterpret_cast<const bf16x8*>(wptr(0, m) + a.wplane) : zero8;
+    wh[m] = *reinterpret_cast<const bf16x8*>(wptr(ch_begin * kConvKS, m));
+    wl[m] = SPLIT ? *reinterpret_cast<const bf16x8*>(wptr(ch_begin * kConvKS, m) + a.wplane)
+                  : zero8;
   }
 
-  for (int ch = 0; ch < a.nch; ++ch) {
+  for (int ch = ch_begin; ch < ch_end; ++ch) {
     __syncthreads();  // the previous chunk's fragment reads are done
     // ---- stage the halo tile of channels [16 ch, 16 ch + 16): NPOS x 4 float4
     for (int i = tid; i < NPOS * 4; i += 256) {
@@ -162,9 +169,24 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
     for (int m = 0; m < CO_T; ++m) {
       const int co = co0 + 16 * m + 4 * g4;
       f32x4 v = acc[m][n];
-      if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + co);
-      *reinterpret_cast<f32x4*>(o + co) = v;
+      if (a.bias && blockIdx.z == 0) v += *reinterpret_cast<const f32x4*>(a.bias + co);
+      if (a.ksplit > 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) atomicAdd(o + co + j, v[j]);
+      } else {
+        *reinterpret_cast<f32x4*>(o + co) = v;
+      }
     }
+  }
+}
+
+// zero channels [0, C) of P channel-last positions (the split-K output)
+__global__ void zero_cl_kernel(float* __restrict__ out, int64_t ldo, int C, int64_t total) {
+  const int C4 = C >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / C4;
+    *reinterpret_cast<f32x4*>(out + p * ldo + 4 * (i - p * C4)) = f32x4{0, 0, 0, 0};
   }
 }
 
@@ -177,7 +199,17 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   a.nblocks = (int64_t)a.B * a.D * a.tiles_y * a.tiles_x;
   if (a.nblocks >= ((int64_t)1 << 31)) return fail(WF_E_SHAPE, "wf_conv3d_k3_fwd: too many tiles");
   const size_t lds = (size_t)2 * 3 * 6 * (TX + 2) * kConvCC * sizeof(uint16_t);
-  dim3 grid((unsigned)a.nblocks, (unsigned)(a.Cout / (16 * CO_T)));
+  // small grids (the 8^3 / 16^3 decoder convs): split the Cin chunks over blockIdx.z so the
+  // launch covers the 256 CUs; partial sums meet in the zeroed output through fp32 atomics
+  const int64_t wgs = a.nblocks * (a.Cout / (16 * CO_T));
+  a.ksplit = 1;
+  if (wgs < 512 && a.nch > 1) {
+    a.ksplit = (int)std::min<int64_t>(a.nch, cdiv(1024, wgs));
+    const int64_t total = (int64_t)a.B * a.D * a.H * a.W * (a.Cout / 4);
+    hipLaunchKernelGGL(zero_cl_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 4096)),
+                       dim3(256), 0, stream, a.out, a.ldo, a.Cout, total);
+  }
+  dim3 grid((unsigned)a.nblocks, (unsigned)(a.Cout / (16 * CO_T)), (unsigned)a.ksplit);
   if (prec == PREC_SPLIT) {
     auto kern = conv3d_k3_kernel<CO_T, NT, true>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
