@@ -5,18 +5,20 @@
 //
 //   out[p, co] = bias[co] + sum_{tap, ci} W[co, ci, tap] * x[p + off(tap), ci]
 //
-// GEMM view: rows = output positions, columns = Cout, K = 27 * Cin ordered per 16-channel
-// chunk as (tap, ci) -- 27 * 16 = 432 values, padded with zero weights to 14 K-steps of 32.
+// GEMM view: rows = output positions, columns = Cout, K = 27 * Cin ordered per 8-channel
+// chunk as (tap, ci) -- 27 * 8 = 216 values, padded with zero weights to 7 K-steps of 32.
 // A workgroup owns one output z-plane tile of 4 rows (y) x 16*NT columns (x) and 16*CO_T
 // output channels; wave w computes row y0 + w: NT position tiles x CO_T channel tiles.
-//   * per 16-channel chunk the 3 x (4+2) x (16NT+2) halo of input positions is read ONCE
+//   * per 8-channel chunk the 3 x (4+2) x (16NT+2) halo of input positions is read ONCE
 //     (coalesced 64-B channel runs), split into bf16 hi / lo and parked in LDS as
-//     [position][16 ch] planes; each of the 27 taps then reads its B fragments (8 channels of
+//     [position][8 ch] planes; each of the 27 taps then reads its B fragments (8 channels of
 //     one position, one ds_read_b128 per plane) at a shifted position -- the 27x reuse of
 //     every input value is served from LDS, not L2;
-//   * the weights are pre-packed [2][chunk*14 + step][Cout][32] bf16 (hi plane, lo plane) so
-//     a lane's A fragment (8 consecutive K of one output channel) is one 16-B load; the next
-//     K-step's fragments are prefetched into registers while the current step's MFMAs run;
+//   * the weights are pre-packed fragment-major, [chunk*7 + step][hi, lo][Cout/16][64 lanes][8]
+//     bf16, and staged into LDS with the activations, so the K loop is LDS reads + MFMAs only;
+//   * the NEXT chunk's activations and weights are loaded into registers right after the
+//     current chunk is committed to LDS, so their HBM / L2 latency hides behind 7 K-steps of
+//     MFMAs (one register set, written after the barrier: the T14 staging pipeline);
 //   * "transposed" product as in gemm_rows: the weight fragment is MFMA operand A (rows =
 //     output channels), the activation fragment operand B (columns = positions), so each lane
 //     ends with 4 consecutive output channels of one position -> one f32x4 store.
@@ -29,15 +31,15 @@
 
 namespace wf {
 
-constexpr int kConvCC = 16;                          // input channels per LDS chunk
-constexpr int kConvKS = (27 * kConvCC + 31) / 32;    // 14 K-steps of 32 per chunk
+constexpr int kConvCC = 8;                           // input channels per LDS chunk
+constexpr int kConvKS = (27 * kConvCC + 31) / 32;    // K-steps of 32 per chunk (7)
 
 struct Conv3Args {
   const float* x;     // (B, D, H, W) positions, ldx floats apart; channels [0, Cin)
-  const uint16_t* w;  // [2][nch * kConvKS][Cout][32] bf16 (hi plane, then lo plane)
+  const uint16_t* w;  // [nch * kConvKS][2 (hi, lo)][Cout / 16][64 lanes][8] bf16
   const float* bias;  // (Cout) or nullptr
   float* out;         // (B, D, H, W) positions, ldo floats apart; channels [0, Cout)
-  int64_t ldx, ldo, wplane;
+  int64_t ldx, ldo;
   int B, D, H, W, Cin, Cout, nch;
   int tiles_x, tiles_y;
   int64_t nblocks;
@@ -49,10 +51,17 @@ template <int CO_T, int NT, bool SPLIT>
 __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   constexpr int TX = 16 * NT, TY = 4, HX = TX + 2, HY = TY + 2;
   constexpr int NPOS = 3 * HY * HX;
-  constexpr int PS = kConvCC;  // bf16 per position per plane
-  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];  // [2][NPOS][PS]
+  constexpr int PS = kConvCC;                       // bf16 per position per plane
+  constexpr int NFRAG = kConvKS * 2 * CO_T;          // weight fragments (1 KB each) per chunk
+  constexpr int NW = (NFRAG * 64 + 255) / 256;       // 16-B weight pieces per thread
+  constexpr int QN = kConvCC / 4, PSTEP = 256 / QN;  // float4 per position, positions per pass
+  constexpr int NJ = (NPOS * QN + 255) / 256;        // input float4 per thread
+  // LDS: activations [hi | lo][NPOS][PS] bf16, then the chunk's weight fragments
+  // [step][plane][m][lane][8] bf16 in MFMA operand order (a wave reads 1 KB contiguous)
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* s_hi = lds;
   uint16_t* s_lo = lds + NPOS * PS;
+  uint16_t* s_w = lds + 2 * NPOS * PS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l15 = lane & 15, g4 = lane >> 4;
 
@@ -78,82 +87,131 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   const int ch_begin = (int)(((int64_t)blockIdx.z * a.nch) / a.ksplit);
   const int ch_end = (int)(((int64_t)(blockIdx.z + 1) * a.nch) / a.ksplit);
-  const int nsteps = ch_end * kConvKS;
-  // A fragment of step s for channel tile m: W[s][co0 + 16m + l15][8 g4 .. 8 g4 + 7]
-  auto wptr = [&](int s, int m) {
-    return a.w + ((int64_t)s * a.Cout + co0 + 16 * m + l15) * 32 + 8 * g4;
-  };
-  bf16x8 wh[CO_T], wl[CO_T];
-#pragma unroll
-  for (int m = 0; m < CO_T; ++m) {
-    wh[m] = *reinterpret_cast<const bf16x8*>(wptr(ch_begin * kConvKS, m));
-    wl[m] = SPLIT ? *reinterpret_cast<const bf16x8*>(wptr(ch_begin * kConvKS, m) + a.wplane)
-                  : zero8;
-  }
 
-  for (int ch = ch_begin; ch < ch_end; ++ch) {
-    __syncthreads();  // the previous chunk's fragment reads are done
-    // ---- stage the halo tile of channels [16 ch, 16 ch + 16): NPOS x 4 float4
-    for (int i = tid; i < NPOS * 4; i += 256) {
-      const int q = i & 3, pos = i >> 2;
+  // ---- per-lane constants, computed once (the K loop below is LDS reads and MFMAs only)
+  // B fragment of K-step s: k = 32 s + 8 g4 -> tap k / CC, channels k % CC .. +7 of the halo
+  // position (tap's z, wid + tap's y, l15 + tap's x); padded taps (>= 27) carry zero
+  // weights, so any finite B is fine -- they read tap 26
+  uint32_t boff[kConvKS];
+#pragma unroll
+  for (int s = 0; s < kConvKS; ++s) {
+    const int k = 32 * s + 8 * g4;
+    const int tap = min(k / kConvCC, 26);
+    const int tz = tap / 9, tyy = (tap / 3) % 3, txx = tap % 3;
+    boff[s] = (uint32_t)((((tz * HY + wid + tyy) * HX + txx + l15) * PS + k % kConvCC) * 2);
+  }
+  // input items j: halo position p0 + PSTEP j, channels 4 q .. +3 of the chunk; source
+  // offsets relative to the chunk's channel base, clamped in range (masked to zero)
+  const int q = tid % QN, p0 = tid / QN;
+  uint32_t goff[NJ];
+  uint32_t gmask = 0;
+  {
+    const int64_t plane = (int64_t)a.H * a.W;
+    const int64_t sample = (int64_t)b * a.D * plane;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int pos = min(p0 + PSTEP * j, NPOS - 1);
       const int hx = pos % HX, r = pos / HX;
       const int hy = r % HY, hz = r / HY;
       const int gz = z + hz - 1, gy = y0 + hy - 1, gx = x0 + hx - 1;
-      const int c = ch * kConvCC + 4 * q;
-      f32x4 v = {0, 0, 0, 0};
-      if (gz >= 0 && gz < a.D && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W && c < a.Cin)
-        v = *reinterpret_cast<const f32x4*>(
-            a.x + (((int64_t)(b * a.D + gz) * a.H + gy) * a.W + gx) * a.ldx + c);
+      const bool ok = p0 + PSTEP * j < NPOS && gz >= 0 && gz < a.D && gy >= 0 && gy < a.H &&
+                      gx >= 0 && gx < a.W;
+      const int cz = min(max(gz, 0), a.D - 1), cy = min(max(gy, 0), a.H - 1),
+                cx = min(max(gx, 0), a.W - 1);
+      goff[j] = (uint32_t)((sample + cz * plane + (int64_t)cy * a.W + cx) * a.ldx);
+      gmask |= ok ? (1u << j) : 0u;
+    }
+  }
+  // weight pieces i = tid + 256 w: fragment f = i / 64 = (step, plane, m), lane i % 64; the
+  // packed global layout is fragment-major too: [step][plane][Cout/16][64][8]
+  const int64_t cblk = a.Cout / 16;
+
+  f32x4 sa[NJ];
+  bf16x8 sw[NW];
+  auto fetch = [&](int ch) {
+    // channels past Cin (the last chunk when Cin % 8 != 0) read channel 0 instead: the
+    // address stays inside the tensor, commit() zeroes the value
+    const int c = ch * kConvCC + 4 * q;
+    const float* xs = a.x + (c < a.Cin ? c : 0);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) sa[j] = *reinterpret_cast<const f32x4*>(xs + goff[j]);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int i = min(tid + 256 * w, NFRAG * 64 - 1);
+      const int f = i >> 6, ln = i & 63;
+      const int m = f % CO_T, sp = f / CO_T;  // sp = step * 2 + plane
+      const int st = sp >> 1, pl = sp & 1;
+      const int64_t frag = ((int64_t)(ch * kConvKS + st) * 2 + pl) * cblk + co0 / 16 + m;
+      sw[w] = (SPLIT || pl == 0)
+                  ? *reinterpret_cast<const bf16x8*>(a.w + (frag * 64 + ln) * 8)
+                  : zero8;
+    }
+  };
+  auto commit = [&](int ch) {
+    const bool cok = ch * kConvCC + 4 * q < a.Cin;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int pos = p0 + PSTEP * j;
+      if (j == NJ - 1 && pos >= NPOS) break;
+      f32x4 v = sa[j];
+      if (!cok || !((gmask >> j) & 1u)) v = f32x4{0, 0, 0, 0};
       bf16x4 h, l;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint16_t hb = f2bf(v[j]);
-        h[j] = (short)hb;
-        l[j] = SPLIT ? (short)f2bf(v[j] - bf2f(hb)) : (short)0;
+      for (int e = 0; e < 4; ++e) {
+        const uint16_t hb = f2bf(v[e]);
+        h[e] = (short)hb;
+        l[e] = SPLIT ? (short)f2bf(v[e] - bf2f(hb)) : (short)0;
       }
       *reinterpret_cast<bf16x4*>(s_hi + pos * PS + 4 * q) = h;
       if (SPLIT) *reinterpret_cast<bf16x4*>(s_lo + pos * PS + 4 * q) = l;
     }
-    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int i = tid + 256 * w;
+      if (w == NW - 1 && i >= NFRAG * 64) break;
+      *reinterpret_cast<bf16x8*>(s_w + i * 8) = sw[w];
+    }
+  };
+  const char* lb = reinterpret_cast<const char*>(lds);
+  const char* lw = reinterpret_cast<const char*>(s_w) + lane * 16;
 
-#pragma unroll 1
+  fetch(ch_begin);
+  for (int ch = ch_begin; ch < ch_end; ++ch) {
+    __syncthreads();  // every wave is done with the previous chunk's LDS
+    commit(ch);
+    __syncthreads();
+    // the next chunk's global reads fly during this chunk's MFMAs: no vmcnt wait below
+    if (ch + 1 < ch_end) fetch(ch + 1);
+#pragma unroll
     for (int s = 0; s < kConvKS; ++s) {
-      const int gs = ch * kConvKS + s;
-      // prefetch the next step's weight fragments
-      bf16x8 nh[CO_T], nl[CO_T];
-      const int ns = min(gs + 1, nsteps - 1);
+      bf16x8 bh[NT], bl[NT], wh[CO_T], wl[CO_T];
 #pragma unroll
       for (int m = 0; m < CO_T; ++m) {
-        nh[m] = *reinterpret_cast<const bf16x8*>(wptr(ns, m));
-        nl[m] = SPLIT ? *reinterpret_cast<const bf16x8*>(wptr(ns, m) + a.wplane) : zero8;
+        wh[m] = *reinterpret_cast<const bf16x8*>(lw + ((s * 2 + 0) * CO_T + m) * 1024);
+        wl[m] = SPLIT ? *reinterpret_cast<const bf16x8*>(lw + ((s * 2 + 1) * CO_T + m) * 1024)
+                      : zero8;
       }
-      // this lane's K slice: k = 32 s + 8 g4 -> tap k / 16, channels (k % 16) .. +7; the
-      // padded taps 27.. carry zero weights, their B fragment just has to be finite
-      const int k = 32 * s + 8 * g4;
-      const int tap = min(k >> 4, 26), ci0 = k & 15;
-      const int tz = tap / 9, tyy = (tap / 3) % 3, txx = tap % 3;
-      const int base = ((tz * HY + wid + tyy) * HX + txx + l15) * PS + ci0;
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        const int off = base + 16 * n * PS;
-        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(s_hi + off);
-        if (SPLIT) {
-          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(s_lo + off);
+        bh[n] = *reinterpret_cast<const bf16x8*>(lb + boff[s] + 16 * n * PS * 2);
+        bl[n] = SPLIT ? *reinterpret_cast<const bf16x8*>(lb + boff[s] + 16 * n * PS * 2 +
+                                                           NPOS * PS * 2)
+                      : zero8;
+      }
 #pragma unroll
-          for (int m = 0; m < CO_T; ++m) {
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[m], bl, acc[m][n], 0, 0, 0);
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[m], bh, acc[m][n], 0, 0, 0);
+      for (int n = 0; n < NT; ++n) {
+#pragma unroll
+        for (int m = 0; m < CO_T; ++m) {
+          if (SPLIT) {
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[m], bl[n], acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[m], bh[n], acc[m][n], 0, 0, 0);
           }
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[m], bh[n], acc[m][n], 0, 0, 0);
         }
-#pragma unroll
-        for (int m = 0; m < CO_T; ++m)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[m], bh, acc[m][n], 0, 0, 0);
       }
-#pragma unroll
-      for (int m = 0; m < CO_T; ++m) {
-        wh[m] = nh[m];
-        wl[m] = nl[m];
-      }
+      // keep the next step's fragment reads from being hoisted over these MFMAs (VGPRs: the
+      // next chunk's prefetch registers are live across the whole loop)
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
@@ -198,7 +256,8 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   a.tiles_y = (int)cdiv(a.H, 4);
   a.nblocks = (int64_t)a.B * a.D * a.tiles_y * a.tiles_x;
   if (a.nblocks >= ((int64_t)1 << 31)) return fail(WF_E_SHAPE, "wf_conv3d_k3_fwd: too many tiles");
-  const size_t lds = (size_t)2 * 3 * 6 * (TX + 2) * kConvCC * sizeof(uint16_t);
+  const size_t lds = ((size_t)2 * 3 * 6 * (TX + 2) * kConvCC + (size_t)kConvKS * 2 * CO_T * 512) *
+                     sizeof(uint16_t);
   // small grids (the 8^3 / 16^3 decoder convs): split the Cin chunks over blockIdx.z so the
   // launch covers the 256 CUs; partial sums meet in the zeroed output through fp32 atomics
   const int64_t wgs = a.nblocks * (a.Cout / (16 * CO_T));
@@ -233,33 +292,38 @@ extern "C" int64_t wf_conv3d_k3_packed_elems(int64_t Cin, int64_t Cout) {
 }
 
 namespace wf {
-// packed[plane][ch * 14 + ss][co][j]: K index kk = 32 ss + j -> tap kk / 16, ci 16 ch + kk % 16
+// packed[(gs * 2 + plane) * (Cout / 16) + co / 16][lane][e], lane = co % 16 + 16 (j / 8),
+// e = j % 8 for K index kk = 32 ss + j of K-step gs = ch * KS + ss: tap kk / CC, input channel
+// CC ch + kk % CC -- each 16 x 32 MFMA A fragment is 1 KB contiguous, in lane order
 __global__ void conv3d_k3_pack_kernel(const float* __restrict__ w, uint16_t* __restrict__ packed,
-                                      int Cin, int Cout, int64_t plane) {
+                                      int Cin, int Cout, int64_t total) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= plane) return;
-  const int j = (int)(i & 31);
-  int64_t r = i >> 5;
-  const int co = (int)(r % Cout);
-  const int s = (int)(r / Cout);
-  const int ch = s / kConvKS, ss = s - ch * kConvKS;
+  if (i >= total) return;
+  const int e = (int)(i & 7), ln = (int)((i >> 3) & 63);
+  int64_t r = i >> 9;
+  const int cb = (int)(r % (Cout / 16));
+  r /= (Cout / 16);
+  const int plane = (int)(r & 1);
+  const int gs = (int)(r >> 1);
+  const int co = cb * 16 + (ln & 15);
+  const int j = 8 * (ln >> 4) + e;
+  const int ch = gs / kConvKS, ss = gs - ch * kConvKS;
   const int kk = 32 * ss + j;
-  const int tap = kk >> 4, ci = ch * kConvCC + (kk & 15);
+  const int tap = kk / kConvCC, ci = ch * kConvCC + kk % kConvCC;
   const float v = (tap < 27 && ci < Cin) ? w[((int64_t)co * Cin + ci) * 27 + tap] : 0.f;
   const uint16_t h = f2bf(v);
-  packed[i] = h;
-  packed[plane + i] = f2bf(v - bf2f(h));
+  packed[i] = plane ? f2bf(v - bf2f(h)) : h;
 }
 }  // namespace wf
 
 extern "C" int wf_conv3d_k3_pack(const float* w, uint16_t* packed, int64_t Cin, int64_t Cout,
                                  void* stream) {
-  WF_REQUIRE(Cin >= 1 && Cout >= 1, "empty weight");
+  WF_REQUIRE(Cin >= 1 && Cout >= 16 && Cout % 16 == 0, "Cout must be a multiple of 16");
   WF_REQUIRE_PTR(w);
   WF_REQUIRE_PTR(packed);
-  const int64_t plane = wf_conv3d_k3_packed_elems(Cin, Cout) / 2;
-  hipLaunchKernelGGL(conv3d_k3_pack_kernel, dim3((unsigned)cdiv(plane, 256)), dim3(256), 0,
-                     (hipStream_t)stream, w, packed, (int)Cin, (int)Cout, plane);
+  const int64_t total = wf_conv3d_k3_packed_elems(Cin, Cout);
+  hipLaunchKernelGGL(conv3d_k3_pack_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, w, packed, (int)Cin, (int)Cout, total);
   return check_launch("wf_conv3d_k3_pack");
 }
 
@@ -272,7 +336,8 @@ extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_p
              "Cin must be a positive multiple of 4 with ldx >= Cin, ldx % 4 == 0");
   WF_REQUIRE(Cout >= 16 && Cout % 16 == 0 && ldo >= Cout && ldo % 4 == 0,
              "Cout must be a positive multiple of 16 with ldo >= Cout, ldo % 4 == 0");
-  WF_REQUIRE(B * D * H * W < ((int64_t)1 << 31), "too many positions");
+  WF_REQUIRE(B * D * H * W < ((int64_t)1 << 31) && B * D * H * W * ldx < ((int64_t)1 << 32),
+             "input too large (32-bit element offsets)");
   WF_REQUIRE(precision == PREC_BF16 || precision == PREC_SPLIT, "unknown precision");
   WF_REQUIRE_PTR(x);
   WF_REQUIRE_PTR(w_packed);
@@ -288,7 +353,6 @@ extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_p
   a.Cin = (int)Cin;
   a.Cout = (int)Cout;
   a.nch = (int)cdiv(Cin, kConvCC);
-  a.wplane = (int64_t)a.nch * kConvKS * Cout * 32;
   hipStream_t s = (hipStream_t)stream;
   const bool co3 = Cout % 48 == 0;
   if (W > 32) return co3 ? launch_conv3<3, 4>(a, precision, s) : launch_conv3<1, 4>(a, precision, s);
