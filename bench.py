@@ -44,6 +44,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 # bench op name -> kernel-name substring in the PMC summary (profiles/*pmc*.json)
 PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_dwfc_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
+              "window_attention": "attn_core_kernel",
               "msfuse": "msfuse", "proj_out": "proj_out"}
 
 
