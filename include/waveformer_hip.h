@@ -150,6 +150,13 @@ int wf_upsample_trilinear_cl(const float* in, float* out, int64_t B, int64_t C, 
                              int64_t h, int64_t w, int64_t D, int64_t H, int64_t W,
                              int align_corners, void* stream);
 
+/* out (M, N) = bias + act(x) (M, K) . W^T, act = GELU(erf) if gelu_in else identity; fp32
+ * rows, W as [2][N][K] bf16 hi / lo planes (wf_split_f32_to_bf16x2).  The 1x1x1 convolutions
+ * of the decoder's ProjectionUpsample (network_models/wave_helper.py:33-81), GELU fused into
+ * the next GEMM's operand loader.  K % 8 == 0, N % 4 == 0.                                    */
+int wf_linear_fwd(const float* x, const uint16_t* w_bf16x2, const float* bias, float* out,
+                  int64_t M, int64_t K, int64_t N, int gelu_in, int precision, void* stream);
+
 /* ---- a2: relative-position bias ------------------------------------------------------ */
 /* bias[h][i][j] = table[index[i][j]][h]  (attention.py:94-97), index is the int64
  * relative_position_index buffer (N, N), table (T, heads).                                */

@@ -179,10 +179,10 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
           const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * wv[j] + bv[j];
-          if (g.a_gelu) {
+        }
+        if (g.a_gelu) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
-          }
+          for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {

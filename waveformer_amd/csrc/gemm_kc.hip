@@ -200,10 +200,10 @@ __global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
         if (g.a_ln != LN_NONE) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[rt][j] = (v[rt][j] - mean[rt]) * rstd[rt] * wv[j] + bv[j];
-          if (g.a_gelu) {
+        }
+        if (g.a_gelu) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[rt][j] = gelu_erf(v[rt][j]);
-          }
+          for (int j = 0; j < 8; ++j) v[rt][j] = gelu_erf(v[rt][j]);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {

@@ -37,7 +37,7 @@ struct GemmArgs {
   const float* a_ln_w;
   const float* a_ln_b;
   float a_eps;
-  int a_gelu;            // 1: GELU(erf) after the loader's LayerNorm (CCF_FFN norm -> act)
+  int a_gelu;            // 1: GELU(erf) on the loaded A values (after the LayerNorm, if any)
   // ---- B
   const uint16_t* w;     // [2][N][K] bf16 (hi plane; lo plane read only for PREC_SPLIT)
   // ---- problem

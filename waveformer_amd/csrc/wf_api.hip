@@ -1,5 +1,5 @@
 // wf_api.hip -- error plumbing and small utilities of the C-ABI (include/waveformer_hip.h).
-#include "wf_common.hpp"
+#include "kernels.hpp"
 
 namespace wf {
 
@@ -68,4 +68,40 @@ extern "C" int wf_split_f32_to_bf16x2(const float* in, uint16_t* out, int64_t n,
   hipLaunchKernelGGL(wf::split_f32_bf16x2_kernel, dim3((unsigned)blocks), dim3(256), 0,
                      (hipStream_t)stream, in, out, n);
   return wf::check_launch("wf_split_f32_to_bf16x2");
+}
+
+using wf::GemmArgs;
+using namespace wf;
+
+// out[m, n] = bias[n] + sum_k act(x[m, k]) * W[n, k] over fp32 rows (act = GELU(erf) or
+// identity): the decoder's 1x1x1 convolutions of ProjectionUpsample on the MFMA GEMM family
+// (gemm_rows / gemm_kc / gemm_ares, bf16x3 or bf16 operands, fp32 accumulation).
+extern "C" int wf_linear_fwd(const float* x, const uint16_t* w_bf16x2, const float* bias,
+                             float* out, int64_t M, int64_t K, int64_t N, int gelu_in,
+                             int precision, void* stream) {
+  WF_REQUIRE(M >= 0 && K >= 8 && K % 8 == 0 && N >= 4 && N % 4 == 0,
+             "need K a multiple of 8 and N a multiple of 4");
+  WF_REQUIRE(precision == PREC_BF16 || precision == PREC_SPLIT, "unknown precision");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(w_bf16x2);
+  WF_REQUIRE_PTR(out);
+  GemmArgs g{};
+  g.prec = precision;
+  g.a_src = x;
+  g.a_bf16 = 0;
+  g.a_C = (int)K;
+  g.a_nseg = 1;
+  g.a_map = MAP_IDENTITY;
+  g.a_ln = LN_NONE;
+  g.a_gelu = gelu_in ? 1 : 0;
+  g.w = w_bf16x2;
+  g.M = M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.epi = EPI_STORE;
+  g.bias = bias;
+  g.out = out;
+  g.out_bf16 = 0;
+  g.ldo = N;
+  return launch_gemm(g, (hipStream_t)stream, "wf_linear_fwd");
 }

@@ -106,8 +106,8 @@ class ProjectionUpsample(nn.Module):
     def _forward_hip(self, x):
         """Inference path, channel-last: HIP trilinear upsample (align_corners=True) + HIP
         depthwise conv + HIP per-channel GroupNorm statistics; GroupNorm's normalisation and
-        affine are folded into conv2's weights per sample, so conv2 / conv3 are plain fp32
-        GEMMs over the position rows (hipBLASLt).  The residual's 1x1 conv runs BEFORE the
+        affine are folded into conv2's weights per sample, so conv2 / conv3 are MFMA GEMMs
+        over the position rows (bf16x3) with each GELU fused into the next GEMM's loader.  The residual's 1x1 conv runs BEFORE the
         upsample (both are linear and the trilinear weights sum to 1, so W.Up(x) + b =
         Up(W.x + b)): the GEMM is 8x / 64x smaller and only Cout channels are resampled."""
         B, C, d, h, w = x.shape
@@ -123,15 +123,18 @@ class ProjectionUpsample(nn.Module):
         w2s = w2.unsqueeze(0) * scale.unsqueeze(1)                       # (B, 2C, C)
         b2s = torch.addmm(self.conv2.bias.unsqueeze(0), shift, w2.t())   # (B, 2C)
         rows = y.permute(0, 2, 3, 4, 1).reshape(B, P, C)
-        hid = F.gelu(torch.baddbmm(b2s.unsqueeze(1), rows, w2s.transpose(1, 2)))
-        hid = hid.reshape(B * P, 2 * C)
+        # the 1x1 convs are MFMA GEMMs (wf_linear_fwd); each GELU is applied in the NEXT
+        # GEMM's operand loader, so no activation tensor is written twice
+        hid = torch.cat([ops.linear_rows(rows[i], w2s[i], b2s[i].contiguous(), cache=False)
+                         for i in range(B)]) if B > 1 else \
+            ops.linear_rows(rows[0], w2s[0], b2s[0].contiguous(), cache=False)
         if self.use_double_conv:
             c3a, c3b = self.conv3[0], self.conv3[2]
-            hid = F.gelu(torch.addmm(c3a.bias, hid, c3a.weight.reshape(c3a.out_channels, -1).t()))
-            out = torch.addmm(c3b.bias, hid, c3b.weight.reshape(c3b.out_channels, -1).t())
+            hid = ops.linear_rows(hid, c3a.weight, c3a.bias, gelu_in=True)
+            out = ops.linear_rows(hid, c3b.weight, c3b.bias, gelu_in=True)
         else:
             c3 = self.conv3
-            out = torch.addmm(c3.bias, hid, c3.weight.reshape(c3.out_channels, -1).t())
+            out = ops.linear_rows(hid, c3.weight, c3.bias, gelu_in=True)
         Cout = out.shape[1]
         out = out.view(B, size[0], size[1], size[2], Cout).permute(0, 4, 1, 2, 3)
         if self.do_res:

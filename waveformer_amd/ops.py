@@ -438,6 +438,29 @@ def dwconv3d_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tens
     return out
 
 
+def linear_rows(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                gelu_in: bool = False, cache: bool = True) -> torch.Tensor:
+    """bias + act(x2d) . W^T on the MFMA GEMM family (wf_linear_fwd), act = GELU(erf) when
+    gelu_in.  weight (N, K) or (N, K, 1, 1, 1); `cache=False` for per-call weights (no split
+    cache on the tensor)."""
+    _check(x2d, "x")
+    M, K = x2d.shape
+    N = weight.shape[0]
+    w2 = weight.reshape(N, K)
+    if cache:
+        wb = split_weight(weight, (N, K))
+    else:
+        w2 = w2.contiguous()
+        wb = torch.empty((2, N, K), dtype=torch.bfloat16, device=x2d.device)
+        _lib.call("wf_split_f32_to_bf16x2", w2.data_ptr(), wb.data_ptr(), w2.numel(), _stream())
+    if bias is not None:
+        _check(bias, "bias")
+    out = torch.empty((M, N), dtype=torch.float32, device=x2d.device)
+    _lib.call("wf_linear_fwd", x2d.data_ptr(), wb.data_ptr(), _ptr(bias), out.data_ptr(), M, K, N,
+              int(bool(gelu_in)), _prec(), _stream())
+    return out
+
+
 def instnorm_stats(x: torch.Tensor, eps: float) -> torch.Tensor:
     """(B, 2, C) {mean, rstd} of InstanceNorm3d(affine=False) over a channel-last tensor."""
     ld = cl_ld(x)
