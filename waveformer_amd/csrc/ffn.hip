@@ -479,7 +479,25 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   g.out_bf16 = hbf;
   g.ldo = hidden;
   int rc = 0;
-  if (stage == 0 || stage == 1) rc = launch_gemm(g, s, "wf_ccf_ffn_fwd(pwconv)");
+  // wide hidden rows (stages 3 / 4: 4C = 768, 1536): a LayerNorm epilogue needs the whole
+  // row in one workgroup, which only the A-resident gemm_ares can hold -- it then re-streams
+  // the full weight per 16 rows (measured 107 / 145 us per launch at B = 4).  Instead: the
+  // K-chunked GEMM with a plain bias epilogue, then one in-place LayerNorm + GELU row pass.
+  static const bool no_split_ln1 = getenv("WF_FFN_NO_SPLIT_LN1") != nullptr;
+  const bool split_ln1 = !no_split_ln1 && precision == PREC_SPLIT && hidden >= 768 &&
+                         hidden <= 1536;
+  if (stage == 0 || stage == 1) {
+    if (split_ln1) {
+      GemmArgs g2 = g;
+      g2.epi = EPI_STORE;
+      rc = launch_gemm(g2, s, "wf_ccf_ffn_fwd(pwconv)");
+      if (!rc)
+        rc = wf_ln_act_fwd(reinterpret_cast<const float*>(h1), ln1_w, ln1_b, eps1, 1,
+                           reinterpret_cast<float*>(h1), M, hidden, stream);
+    } else {
+      rc = launch_gemm(g, s, "wf_ccf_ffn_fwd(pwconv)");
+    }
+  }
   if (rc) return rc;
   // dwconv + LN2 + GELU (+ fc + residual): the stage-1 shape runs the fused back half
   // (ffn_dwfc.hip, h2 stays on chip); other shapes either fuse dwconv + LN over the full 4C row
