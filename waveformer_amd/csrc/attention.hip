@@ -205,6 +205,202 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
   }
 }
 
+// Whole-window variant (N <= 512, the 8^3 windows of the default config): all N keys' K rows
+// and V^T are staged into LDS ONCE per workgroup (one barrier), then each wave runs the flash
+// loop over 64-key tiles with no barriers, prefetching the next tile's relative-position bias
+// rows into registers while the current tile's MFMAs and softmax run (the per-tile staging +
+// 2 barriers + exposed bias loads of attn_core_kernel left the waves waiting on memory 57% of
+// their cycles).  V is stored [key/4][hd][4 keys], so the staging writes 4 keys per
+// ds_write_b64 and the PV A fragment (4 consecutive keys of one hd) is one ds_read_b64.
+template <int HD, bool SPLIT>
+__global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict__ qkv,
+                                                          const float* __restrict__ bias,
+                                                          void* __restrict__ out,
+                                                          float* __restrict__ lse, int N,
+                                                          int heads, float scale_log2) {
+  constexpr int NC = HD / 16;
+  constexpr int KT = 64, NKT = KT / 16;
+  constexpr int KS = HD + 4;
+  constexpr int NB = SPLIT ? 2 : 1;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds_attn[];
+  const int NP = (N + KT - 1) / KT * KT;  // keys padded to whole tiles (zero K / V rows)
+  uint16_t* Ks = lds_attn;                           // [NB][NP][KS]
+  uint16_t* Vq = lds_attn + (size_t)NB * NP * KS;    // [NB][NP/4][HD][4]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int qb = blockIdx.x, h = blockIdx.y;
+  const int64_t bw = blockIdx.z;
+  const int C = heads * HD;
+  const int64_t row0 = bw * N;
+  const int ld = 3 * C;
+  const int q = qb * kQB + wid * 16 + (lane & 15);
+  const bool qv = q < N;
+  const int g4 = 4 * (lane >> 4);
+
+  // ---- stage K [key][hd] and V [key/4][hd][4] for all keys (zero past N)
+  for (int it = tid; it < NP * (HD / 8); it += 256) {
+    const int kr = it / (HD / 8), ch = it % (HD / 8);
+    bf16x8 kh = {0, 0, 0, 0, 0, 0, 0, 0}, kl = kh;
+    if (kr < N) load8_split<SPLIT>(qkv, (row0 + kr) * ld + C + h * HD + ch * 8, kh, kl);
+    *reinterpret_cast<bf16x8*>(Ks + (size_t)kr * KS + ch * 8) = kh;
+    if (SPLIT) *reinterpret_cast<bf16x8*>(Ks + (size_t)(NP + kr) * KS + ch * 8) = kl;
+  }
+  for (int it = tid; it < (NP / 4) * (HD / 8); it += 256) {
+    const int k4 = it / (HD / 8), ch = it % (HD / 8);
+    bf16x8 vh[4], vl[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      vh[r] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      vl[r] = vh[r];
+      const int key = 4 * k4 + r;
+      if (key < N) load8_split<SPLIT>(qkv, (row0 + key) * ld + 2 * C + h * HD + ch * 8, vh[r], vl[r]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const size_t o = ((size_t)k4 * HD + ch * 8 + j) * 4;
+      *reinterpret_cast<bf16x4*>(Vq + o) = bf16x4{vh[0][j], vh[1][j], vh[2][j], vh[3][j]};
+      if (SPLIT)
+        *reinterpret_cast<bf16x4*>(Vq + (size_t)NP * HD + o) =
+            bf16x4{vl[0][j], vl[1][j], vl[2][j], vl[3][j]};
+    }
+  }
+
+  // Q^T fragments (B operand): lane holds Q[q][c*16 + g4 + j], j < 4
+  bf16x4 qf[NC], qfl[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    qf[c] = bf16x4{0, 0, 0, 0};
+    qfl[c] = bf16x4{0, 0, 0, 0};
+    if (!qv) continue;
+    const int64_t off = (row0 + q) * ld + h * HD + c * 16 + g4;
+    if (SPLIT) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(qkv) + off);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint16_t hh = f2bf(v[j]);
+        qf[c][j] = (short)hh;
+        qfl[c][j] = (short)f2bf(v[j] - bf2f(hh));
+      }
+    } else {
+      qf[c] = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const uint16_t*>(qkv) + off);
+    }
+  }
+  f32x4 o[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) o[c] = f32x4{0, 0, 0, 0};
+  float mrun = -INFINITY, lrun = 0.f;
+  const float* brow = bias + ((int64_t)h * N + (qv ? q : 0)) * N;
+  // bias of key kb .. kb+3 (zero past N; kb is a multiple of 4 and N of 4 or not -- guarded)
+  auto load_bias = [&](int kb) -> f32x4 {
+    if (kb + 3 < N) return *reinterpret_cast<const f32x4*>(brow + kb);
+    f32x4 r;
+    r.x = kb + 0 < N ? brow[kb + 0] : 0.f;
+    r.y = kb + 1 < N ? brow[kb + 1] : 0.f;
+    r.z = kb + 2 < N ? brow[kb + 2] : 0.f;
+    r.w = kb + 3 < N ? brow[kb + 3] : 0.f;
+    return r;
+  };
+  f32x4 bnext[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) bnext[kt] = load_bias(kt * 16 + g4);
+  __syncthreads();
+
+  for (int k0 = 0; k0 < N; k0 += KT) {
+    f32x4 bv[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) bv[kt] = bnext[kt];
+    if (k0 + KT < N) {
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) bnext[kt] = load_bias(k0 + KT + kt * 16 + g4);
+    }
+    f32x4 s[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      s[kt] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ko = (k0 + kt * 16 + (lane & 15)) * KS + c * 16 + g4;
+        const bf16x4 a = *reinterpret_cast<const bf16x4*>(Ks + ko);
+        if (SPLIT) {
+          const bf16x4 al = *reinterpret_cast<const bf16x4*>(Ks + (size_t)NP * KS + ko);
+          s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, qf[c], s[kt], 0, 0, 0);
+          s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, qfl[c], s[kt], 0, 0, 0);
+        }
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, qf[c], s[kt], 0, 0, 0);
+      }
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const int kb = k0 + kt * 16 + g4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float t = s[kt][i] * scale_log2 + bv[kt][i] * 1.4426950408889634f;
+        t = (kb + i < N) ? t : -INFINITY;
+        s[kt][i] = t;
+        tmax = fmaxf(tmax, t);
+      }
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mnew = fmaxf(mrun, tmax);
+    const float alpha = exp2f(mrun - mnew);
+    mrun = mnew;
+    float psum = 0.f;
+    bf16x4 pf[NKT], pfl[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = exp2f(s[kt][i] - mnew);
+        psum += p;
+        const uint16_t ph = f2bf(p);
+        pf[kt][i] = (short)ph;
+        pfl[kt][i] = SPLIT ? (short)f2bf(p - bf2f(ph)) : (short)0;
+      }
+    }
+    lrun = lrun * alpha + psum;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      o[c] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const size_t vo = ((size_t)((k0 + kt * 16 + g4) >> 2) * HD + c * 16 + (lane & 15)) * 4;
+        const bf16x4 a = *reinterpret_cast<const bf16x4*>(Vq + vo);
+        if (SPLIT) {
+          const bf16x4 al = *reinterpret_cast<const bf16x4*>(Vq + (size_t)NP * HD + vo);
+          o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, pf[kt], o[c], 0, 0, 0);
+          o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pfl[kt], o[c], 0, 0, 0);
+        }
+        o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pf[kt], o[c], 0, 0, 0);
+      }
+    }
+  }
+  lrun += __shfl_xor(lrun, 16, 64);
+  lrun += __shfl_xor(lrun, 32, 64);
+  if (lse && qv && lane < 16) lse[(bw * heads + h) * N + q] = mrun + __log2f(lrun);
+  if (qv) {
+    const float inv = 1.f / lrun;
+    const int64_t off = (row0 + q) * C + h * HD + g4;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (SPLIT) {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off + c * 16) = o[c] * inv;
+      } else {
+        bf16x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = (short)f2bf(o[c][i] * inv);
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(out) + off + c * 16) = r;
+      }
+    }
+  }
+}
+
+static size_t attn_win_lds(int N, int hd, bool split) {
+  const size_t NP = (size_t)(N + 63) / 64 * 64;
+  return (split ? 2 : 1) * (NP * (hd + 4) + NP * hd) * sizeof(uint16_t);
+}
+
 int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, int64_t Bw,
                      int N, int heads, int hd, float scale, int prec, hipStream_t s) {
   if (Bw <= 0) return WF_OK;
@@ -212,6 +408,25 @@ int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, 
   dim3 grid((unsigned)cdiv(N, kQB), (unsigned)heads, (unsigned)Bw);
   const float sl2 = scale * 1.4426950408889634f;
   const bool split = prec == PREC_SPLIT;
+  // the window-resident variant measured slower (236 vs 186 us on the stage-1 launch: its
+  // 74 KB of LDS leaves 2 workgroups per CU, the tiled kernel's occupancy hides more latency;
+  // hoisting the tiled kernel's bias loads over its staging cost occupancy too: 206 us); opt-in
+  static const bool use_win = getenv("WF_ATTN_WIN") != nullptr;
+  if (use_win && hd == 16 && attn_win_lds(N, hd, split) <= 80 * 1024) {
+    const size_t lds = attn_win_lds(N, hd, split);
+    if (split) {
+      auto k = attn_win_kernel<16, true>;
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, qkv, bias, out, lse, N, heads, sl2);
+    } else {
+      auto k = attn_win_kernel<16, false>;
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, qkv, bias, out, lse, N, heads, sl2);
+    }
+    return check_launch("attention core (window-resident)");
+  }
 #define WF_ATTN_CASE(HDV)                                                                  \
   case HDV:                                                                                \
     if (split)                                                                             \
