@@ -157,6 +157,18 @@ int wf_upsample_trilinear_cl(const float* in, float* out, int64_t B, int64_t C, 
 int wf_linear_fwd(const float* x, const uint16_t* w_bf16x2, const float* bias, float* out,
                   int64_t M, int64_t K, int64_t N, int gelu_in, int precision, void* stream);
 
+/* wf_window_attention_fwd with the bias taken from the (T, heads) relative_position_bias_table
+ * directly: the index is the reference's formula (attention.py:40-56, Q2 depth stride 3ws-1)
+ * computed from the token coordinates, the table column staged in LDS -- valid when the
+ * module's relative_position_index buffer equals that formula (the caller checks).  ws = 8,
+ * head_dim = 16.                                                                             */
+int wf_window_attention_fwd_table(const float* x, const float* ln_w, const float* ln_b,
+                                  float ln_eps, const uint16_t* wqkv_bf16x2, const float* bqkv,
+                                  const float* table, const uint16_t* wproj_bf16x2,
+                                  const float* bproj, float* out, void* workspace, int64_t B,
+                                  int64_t C, int64_t D1, int64_t H1, int64_t W1, int64_t ws,
+                                  int64_t heads, float scale, int precision, void* stream);
+
 /* ---- a2: relative-position bias ------------------------------------------------------ */
 /* bias[h][i][j] = table[index[i][j]][h]  (attention.py:94-97), index is the int64
  * relative_position_index buffer (N, N), table (T, heads).                                */

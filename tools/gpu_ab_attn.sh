@@ -1,5 +1,5 @@
 #!/bin/bash
-# parity (encoder + attention + training grads) and an A/B of the window-resident attention
+# parity (encoder + attention + training grads) and the encoder bench's attention timing
 set -o pipefail
 TAG=${1:-aa}
 export TMPDIR=/tmp
@@ -7,8 +7,4 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_train_grads.py -x -q --timeout 200 --timeout-method thread -m gpu > gpurun_out/${TAG}_pytest.txt 2>&1 || { tail -30 gpurun_out/${TAG}_pytest.txt; exit 1; }
 tail -2 gpurun_out/${TAG}_pytest.txt
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --parity 0 > gpurun_out/${TAG}_new.json 2>/dev/null || exit 1
-WF_ATTN_WIN=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --parity 0 > gpurun_out/${TAG}_old.json 2>/dev/null || exit 1
-python -c "
-import json
-for n in ("new","old"):
-    d=json.load(open('gpurun_out/${TAG}_'+n+'.json')); r=d['rooflines']['window_attention']; print(n, round(d['value'],1), round(d['ms_per_step'],3), 'attn us', r['avg_launch_us'], 'frac', r['frac'])"
+python tools/bench_line.py gpurun_out/${TAG}_new.json

@@ -43,6 +43,9 @@ SIGNATURES = {
     "wf_upsample_trilinear_cl": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64,
                                       _I, _P]),
     "wf_linear_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I, _I, _P]),
+    "wf_window_attention_fwd_table": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P,
+                                           _I64, _I64, _I64, _I64, _I64, _I64, _I64, _F, _I,
+                                           _P]),
     "wf_rel_pos_bias": (_I, [_P, _P, _P, _I64, _I64, _I64, _P]),
     "wf_window_attention_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I]),
     "wf_window_attention_fwd": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P,

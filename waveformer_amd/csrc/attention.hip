@@ -38,12 +38,22 @@ __device__ __forceinline__ void load8_split(const void* base, int64_t off, bf16x
   }
 }
 
-template <int HD, int KT, bool SPLIT>
+// WS == 0: `bias` is the dense (heads, N, N) relative-position bias.  WS == 8 (ws % 4 == 0
+// in general): `bias` is the (T, heads) relative_position_bias_table itself; its column h is
+// staged in LDS (pre-scaled by log2 e) and each score's row is the reference's index formula
+// (attention.py:40-56, with the Q2 depth stride 3 ws - 1) evaluated from the query / key
+// coordinates -- the (heads, N, N) tensor (805 MB of L2 reads per stage-1 launch) is never
+// touched.  The 4 keys a lane holds share (z, y) and have consecutive x, so their indices are
+// i0, i0 - 1, i0 - 2, i0 - 3.
+template <int HD, int KT, bool SPLIT, int WS = 0>
 __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__ qkv,
                                                         const float* __restrict__ bias,
                                                         void* __restrict__ out,
                                                         float* __restrict__ lse, int N,
                                                         int heads, float scale_log2) {
+  constexpr int TBLN = WS ? (2 * WS - 2) * (3 * WS - 1) + (2 * WS - 2) * (2 * WS - 1) + 2 * WS - 1
+                          : 1;  // reachable table rows (Q2 collapses the (2ws-1)^3 table)
+  __shared__ float tb[TBLN];
   constexpr int NC = HD / 16;  // 16-wide head_dim chunks
   constexpr int NKT = KT / 16; // 16-key sub-tiles per tile
   constexpr int KS = HD + 4, VS = KT + 4;
@@ -85,7 +95,14 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
 #pragma unroll
   for (int c = 0; c < NC; ++c) o[c] = f32x4{0, 0, 0, 0};
   float mrun = -INFINITY, lrun = 0.f;
-  const float* brow = bias + ((int64_t)h * N + (qv ? q : 0)) * N;
+  const float* brow = bias + ((int64_t)h * N + (qv ? q : 0)) * (WS ? 0 : N);
+  int qbase = 0;
+  if (WS) {
+    for (int i = tid; i < TBLN; i += 256) tb[i] = bias[(int64_t)i * heads + h] * 1.4426950408889634f;
+    const int qq = qv ? q : 0;
+    const int qz = qq / (WS * WS), qy = (qq / WS) % WS, qx = qq % WS;
+    qbase = (qz + WS - 1) * (3 * WS - 1) + (qy + WS - 1) * (2 * WS - 1) + (qx + WS - 1);
+  }
 
   for (int k0 = 0; k0 < N; k0 += KT) {
     __syncthreads();
@@ -132,17 +149,22 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
     for (int kt = 0; kt < NKT; ++kt) {
       const int kb = k0 + kt * 16 + g4;
       f32x4 bv;
-      if (kb + 3 < N) {
-        bv = *reinterpret_cast<const f32x4*>(brow + kb);
+      if (WS) {  // already scaled by log2 e
+        const int kz = kb / (WS * WS), ky = (kb / WS) % WS, kx = kb % WS;
+        const int i0 = min(max(qbase - (kz * (3 * WS - 1) + ky * (2 * WS - 1) + kx), 3), TBLN - 1);
+        bv = f32x4{tb[i0], tb[i0 - 1], tb[i0 - 2], tb[i0 - 3]};
+      } else if (kb + 3 < N) {
+        bv = *reinterpret_cast<const f32x4*>(brow + kb) * 1.4426950408889634f;
       } else {
         bv.x = kb + 0 < N ? brow[kb + 0] : 0.f;
         bv.y = kb + 1 < N ? brow[kb + 1] : 0.f;
         bv.z = kb + 2 < N ? brow[kb + 2] : 0.f;
         bv.w = kb + 3 < N ? brow[kb + 3] : 0.f;
+        bv *= 1.4426950408889634f;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float t = s[kt][i] * scale_log2 + bv[i] * 1.4426950408889634f;
+        float t = s[kt][i] * scale_log2 + bv[i];
         t = (kb + i < N) ? t : -INFINITY;
         s[kt][i] = t;
         tmax = fmaxf(tmax, t);
@@ -402,12 +424,24 @@ static size_t attn_win_lds(int N, int hd, bool split) {
 }
 
 int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, int64_t Bw,
-                     int N, int heads, int hd, float scale, int prec, hipStream_t s) {
+                     int N, int heads, int hd, float scale, int prec, hipStream_t s,
+                     int table_ws) {
   if (Bw <= 0) return WF_OK;
   if (Bw > 65535) return fail(WF_E_SHAPE, "attention: more than 65535 windows per call");
   dim3 grid((unsigned)cdiv(N, kQB), (unsigned)heads, (unsigned)Bw);
   const float sl2 = scale * 1.4426950408889634f;
   const bool split = prec == PREC_SPLIT;
+  if (table_ws) {  // bias = the (T, heads) table; index from the coordinates
+    if (table_ws != 8 || hd != 16 || N != 512)
+      return fail(WF_E_SHAPE, "attention (table bias): implemented for ws = 8, head_dim = 16");
+    if (split)
+      hipLaunchKernelGGL((attn_core_kernel<16, 64, true, 8>), grid, dim3(256), 0, s, qkv, bias,
+                         out, lse, N, heads, sl2);
+    else
+      hipLaunchKernelGGL((attn_core_kernel<16, 64, false, 8>), grid, dim3(256), 0, s, qkv, bias,
+                         out, lse, N, heads, sl2);
+    return check_launch("attention core (table bias)");
+  }
   // the window-resident variant measured slower (236 vs 186 us on the stage-1 launch: its
   // 74 KB of LDS leaves 2 workgroups per CU, the tiled kernel's occupancy hides more latency;
   // hoisting the tiled kernel's bias loads over its staging cost occupancy too: 206 us); opt-in
@@ -487,14 +521,13 @@ extern "C" int64_t wf_window_attention_workspace_bytes(int64_t B, int64_t C, int
   return qkv + ao;
 }
 
-extern "C" int wf_window_attention_fwd_train(const float* x, const float* ln_w,
-                                             const float* ln_b, float ln_eps,
-                                             const uint16_t* wqkv_bf16x2, const float* bqkv,
-                                             const float* bias, const uint16_t* wproj_bf16x2,
-                                             const float* bproj, float* out, void* workspace,
-                                             float* lse, int64_t B, int64_t C, int64_t D1,
-                                             int64_t H1, int64_t W1, int64_t ws, int64_t heads,
-                                             float scale, int precision, void* stream) {
+static int window_attention_impl(const float* x, const float* ln_w, const float* ln_b,
+                                 float ln_eps, const uint16_t* wqkv_bf16x2, const float* bqkv,
+                                 const float* bias, int table_ws,
+                                 const uint16_t* wproj_bf16x2, const float* bproj, float* out,
+                                 void* workspace, float* lse, int64_t B, int64_t C, int64_t D1,
+                                 int64_t H1, int64_t W1, int64_t ws, int64_t heads, float scale,
+                                 int precision, void* stream) {
   WF_REQUIRE(B >= 1 && C >= 8 && C % 8 == 0, "C must be a positive multiple of 8");
   WF_REQUIRE(ws >= 1 && D1 % ws == 0 && H1 % ws == 0 && W1 % ws == 0,
              "the raster must tile into ws^3 windows (window_partition, wave_helper.py:459)");
@@ -545,7 +578,7 @@ extern "C" int wf_window_attention_fwd_train(const float* x, const float* ln_w,
   if (rc) return rc;
   // 2. softmax(q k^T * scale + bias) v
   rc = launch_attn_core(qkv, bias, ao, lse, Bw, (int)N, (int)heads, (int)(C / heads), scale,
-                        precision, s);
+                        precision, s, table_ws);
   if (rc) return rc;
   // 3. proj; window-major rows == the reshaped raster (Q1)
   GemmArgs p{};
@@ -566,6 +599,34 @@ extern "C" int wf_window_attention_fwd_train(const float* x, const float* ln_w,
   p.out_bf16 = 0;
   p.ldo = C;
   return launch_gemm(p, s, "wf_window_attention_fwd(proj)");
+}
+
+extern "C" int wf_window_attention_fwd_train(const float* x, const float* ln_w,
+                                             const float* ln_b, float ln_eps,
+                                             const uint16_t* wqkv_bf16x2, const float* bqkv,
+                                             const float* bias, const uint16_t* wproj_bf16x2,
+                                             const float* bproj, float* out, void* workspace,
+                                             float* lse, int64_t B, int64_t C, int64_t D1,
+                                             int64_t H1, int64_t W1, int64_t ws, int64_t heads,
+                                             float scale, int precision, void* stream) {
+  return window_attention_impl(x, ln_w, ln_b, ln_eps, wqkv_bf16x2, bqkv, bias, 0, wproj_bf16x2,
+                               bproj, out, workspace, lse, B, C, D1, H1, W1, ws, heads, scale,
+                               precision, stream);
+}
+
+extern "C" int wf_window_attention_fwd_table(const float* x, const float* ln_w,
+                                             const float* ln_b, float ln_eps,
+                                             const uint16_t* wqkv_bf16x2, const float* bqkv,
+                                             const float* table, const uint16_t* wproj_bf16x2,
+                                             const float* bproj, float* out, void* workspace,
+                                             int64_t B, int64_t C, int64_t D1, int64_t H1,
+                                             int64_t W1, int64_t ws, int64_t heads, float scale,
+                                             int precision, void* stream) {
+  WF_REQUIRE(ws == 8 && C == 16 * heads,
+             "table-bias attention is implemented for window 8 and head_dim 16");
+  return window_attention_impl(x, ln_w, ln_b, ln_eps, wqkv_bf16x2, bqkv, table, (int)ws,
+                               wproj_bf16x2, bproj, out, workspace, nullptr, B, C, D1, H1, W1,
+                               ws, heads, scale, precision, stream);
 }
 
 extern "C" int wf_window_attention_fwd(const float* x, const float* ln_w, const float* ln_b,

@@ -65,8 +65,11 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);
 int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_only);
 
 // ---- windowed attention core over a (B_, N, 3C) qkv buffer (bf16, or fp32 when SPLIT) ----
+// table_ws != 0: `bias` is the (T, heads) relative_position_bias_table and the index is the
+// reference's formula for window table_ws (8 with head_dim 16 implemented)
 int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, int64_t Bw,
-                     int N, int heads, int hd, float scale, int prec, hipStream_t s);
+                     int N, int heads, int hd, float scale, int prec, hipStream_t s,
+                     int table_ws = 0);
 
 // ---- depthwise 3^3 conv + bias + LayerNorm + GELU over a channel-last volume ------------
 // (bf16 storage for PREC_BF16, fp32 for PREC_SPLIT)

@@ -71,9 +71,22 @@ class Attention(nn.Module):
         self._check_train()
         if wfa.needs_grad(x_cl, *self.parameters(), *(ln[:2] if ln is not None else ())):
             return wfa.window_attention(self, x_cl, ln)
+        bias = self.relative_position_bias_table.detach() if self._table_ok() else self.dense_bias()
         return ops.window_attention(
-            x_cl, self.qkv.weight, self.qkv.bias, self.dense_bias(), self.proj.weight,
+            x_cl, self.qkv.weight, self.qkv.bias, bias, self.proj.weight,
             self.proj.bias, self.window_size, self.num_heads, self.scale, ln)
+
+    def _table_ok(self) -> bool:
+        """The table-bias kernel (ws 8, head_dim 16) computes the index from the reference's
+        formula; use it only while the relative_position_index buffer still equals it."""
+        if self.window_size != 8 or self.head_dim != 16:
+            return False
+        i = self.relative_position_index
+        key = (i.data_ptr(), i._version, i.device)
+        if getattr(self, "_tbl_key", None) != key:
+            self._tbl_ok = bool(torch.equal(i, relative_position_index(8).to(i.device)))
+            self._tbl_key = key
+        return self._tbl_ok
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x: (B_, N, C) token batches, N = window_size^3 (attention.py:83-104)."""

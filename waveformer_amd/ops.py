@@ -522,7 +522,9 @@ def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torc
                      ws: int, heads: int, scale: float,
                      ln: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None) -> torch.Tensor:
     """window_partition + Attention.forward + reshape-reverse (Q1) over a channel-last raster.
-    Returns (B, D1, H1, W1, C) whose rows are the window-major attention outputs."""
+    Returns (B, D1, H1, W1, C) whose rows are the window-major attention outputs.  `bias` is
+    the dense (heads, N, N) bias, or the ((2ws-1)^3, heads) table itself when the index is the
+    reference's formula (wf_window_attention_fwd_table, ws 8 / head_dim 16)."""
     _check(x_cl, "x")
     B, D1, H1, W1, C = x_cl.shape
     wq = split_weight(wqkv)
@@ -533,8 +535,10 @@ def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torc
         _check(bproj, "proj.bias")
     _check(bias, "bias")
     N = ws ** 3
-    if tuple(bias.shape) != (heads, N, N):
-        raise ValueError(f"window_attention: bias {tuple(bias.shape)} != ({heads},{N},{N})")
+    table = tuple(bias.shape) == ((2 * ws - 1) ** 3, heads)
+    if not table and tuple(bias.shape) != (heads, N, N):
+        raise ValueError(f"window_attention: bias {tuple(bias.shape)} is neither ({heads},{N},{N}) "
+                         f"nor the ({(2 * ws - 1) ** 3},{heads}) table")
     lw = lb = None
     eps = 0.0
     if ln is not None:
@@ -543,7 +547,8 @@ def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torc
     prec = _prec()
     wsb = _lib.query("wf_window_attention_workspace_bytes", B, C, D1, H1, W1, prec)
     work = torch.empty(wsb, dtype=torch.uint8, device=x_cl.device)
-    _lib.call("wf_window_attention_fwd", x_cl.data_ptr(), _ptr(lw), _ptr(lb), float(eps),
+    _lib.call("wf_window_attention_fwd_table" if table else "wf_window_attention_fwd",
+              x_cl.data_ptr(), _ptr(lw), _ptr(lb), float(eps),
               wq.data_ptr(), _ptr(bqkv), bias.data_ptr(), wp.data_ptr(), _ptr(bproj),
               out.data_ptr(), work.data_ptr(), B, C, D1, H1, W1, ws, heads, float(scale),
               prec, _stream())
