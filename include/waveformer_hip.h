@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 6
+#define WF_ABI_VERSION 7
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1 };
 
@@ -125,9 +125,12 @@ int wf_idwt3d_level(const float* const* coef, const int64_t* coef_strides, int64
  * fp32 (Cout, Cin, 3, 3, 3) weight ([2] hi / lo planes, K-step-major).  precision WF_PREC_*. */
 int64_t wf_conv3d_k3_packed_elems(int64_t Cin, int64_t Cout);
 int wf_conv3d_k3_pack(const float* w, uint16_t* packed, int64_t Cin, int64_t Cout, void* stream);
+/* stats_acc: NULL, or a ZEROED (B, Cout, 2) fp64 buffer that receives each output channel's
+ * sum and sum of squares per sample (InstanceNorm statistics fused into the epilogue; finish
+ * with wf_instnorm_finalize).                                                                 */
 int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed, const float* bias,
-                     float* out, int64_t ldo, int64_t B, int64_t Cin, int64_t Cout, int64_t D,
-                     int64_t H, int64_t W, int precision, void* stream);
+                     float* out, int64_t ldo, double* stats_acc, int64_t B, int64_t Cin,
+                     int64_t Cout, int64_t D, int64_t H, int64_t W, int precision, void* stream);
 
 /* InstanceNorm3d(affine=False) statistics of a channel-last tensor: P positions per sample,
  * element (b, p, c) at x[(b*P + p)*ldx + c].  stats: (B, 2, C) fp32 {mean row, rstd row},
@@ -139,6 +142,9 @@ int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed, cons
 int64_t wf_instnorm_workspace_bytes(int64_t B, int64_t C);
 int wf_instnorm_stats_cl(const float* x, int64_t ldx, int64_t B, int64_t C, int64_t P, float eps,
                          float* stats, void* workspace, void* stream);
+/* (B, C, 2) {sum, sum of squares} fp64 over P positions -> (B, 2, C) {mean, rstd} fp32. */
+int wf_instnorm_finalize(const double* acc, float* stats, int64_t B, int64_t C, int64_t P,
+                         float eps, void* stream);
 int wf_norm_act_cl(const float* a, int64_t lda, const float* stats_a, const float* r, int64_t ldr,
                    const float* stats_r, float* out, int64_t ldo, int64_t B, int64_t C, int64_t P,
                    float slope, void* stream);

@@ -151,3 +151,20 @@ def test_unetr_up_block_fast_path():
         want = m(x, skip)
         got = m.cuda()(x.cuda(), skip.cuda())
     assert C.rel_l2(got, want) <= 2e-5
+
+
+@pytest.mark.parametrize("B,Cin,Cout,S", [(2, 48, 48, (12, 9, 70)), (1, 384, 192, (8, 8, 8)),
+                                          (1, 20, 32, (5, 6, 19))])
+def test_conv3d_k3_fused_instnorm_stats(B, Cin, Cout, S):
+    """The InstanceNorm statistics accumulated in the conv epilogue (and, for split-K small
+    grids, by the follow-up pass) equal mean / rstd of the conv output: rel err <= 1e-5."""
+    from waveformer_amd import ops
+    x = (seeded_randn((B, Cin) + S, 14) + 0.5).cuda()
+    w = (seeded_randn((Cout, Cin, 3, 3, 3), 15) * (Cin * 27) ** -0.5).cuda()
+    b = seeded_randn((Cout,), 16).cuda()
+    out, st = ops.conv3d_k3(x, w, b, norm_eps=1e-5)
+    o = out.double().cpu()
+    mean = o.mean(dim=(2, 3, 4))
+    rstd = 1.0 / torch.sqrt(o.var(dim=(2, 3, 4), unbiased=False) + 1e-5)
+    assert C.rel_l2(st[:, 0], mean) <= 1e-5
+    assert C.rel_l2(st[:, 1], rstd) <= 1e-5

@@ -35,8 +35,9 @@ SIGNATURES = {
                              _P]),
     "wf_conv3d_k3_packed_elems": (_I64, [_I64, _I64]),
     "wf_conv3d_k3_pack": (_I, [_P, _P, _I64, _I64, _P]),
-    "wf_conv3d_k3_fwd": (_I, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64,
-                              _I, _P]),
+    "wf_conv3d_k3_fwd": (_I, [_P, _I64, _P, _P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I64,
+                              _I64, _I, _P]),
+    "wf_instnorm_finalize": (_I, [_P, _P, _I64, _I64, _I64, _F, _P]),
     "wf_instnorm_workspace_bytes": (_I64, [_I64, _I64]),
     "wf_instnorm_stats_cl": (_I, [_P, _I64, _I64, _I64, _I64, _F, _P, _P, _P]),
     "wf_norm_act_cl": (_I, [_P, _I64, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),
@@ -88,7 +89,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 _lock = threading.Lock()
 _lib = None
 _err = None

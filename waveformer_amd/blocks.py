@@ -125,10 +125,11 @@ class UnetResBlock(nn.Module):
         if self._fast(inp):
             slope = self.lrelu.negative_slope
             x = ops.to_cl(inp)
-            h = ops.conv3d_k3(x, self.conv1.conv.weight, self.conv1.conv.bias)
-            ops.norm_act(h, ops.instnorm_stats(h, self.norm1.eps), slope=slope, out=h)
-            out = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias)
-            s2 = ops.instnorm_stats(out, self.norm2.eps)
+            h, s1 = ops.conv3d_k3(x, self.conv1.conv.weight, self.conv1.conv.bias,
+                                  norm_eps=self.norm1.eps)
+            ops.norm_act(h, s1, slope=slope, out=h)
+            out, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
+                                    norm_eps=self.norm2.eps)
             if self.downsample:
                 c3 = self.conv3.conv
                 res = ops.conv1x1_cl(x, c3.weight, c3.bias)
@@ -158,10 +159,12 @@ class UnetBasicBlock(nn.Module):
                 and _k3_ok(self.conv2.conv, self.conv2.conv.in_channels)
                 and _in_ok(self.norm1) and _in_ok(self.norm2)):
             slope = self.lrelu.negative_slope
-            h = ops.conv3d_k3(inp, self.conv1.conv.weight, self.conv1.conv.bias)
-            ops.norm_act(h, ops.instnorm_stats(h, self.norm1.eps), slope=slope, out=h)
-            out = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias)
-            return ops.norm_act(out, ops.instnorm_stats(out, self.norm2.eps), slope=slope, out=out)
+            h, s1 = ops.conv3d_k3(inp, self.conv1.conv.weight, self.conv1.conv.bias,
+                                  norm_eps=self.norm1.eps)
+            ops.norm_act(h, s1, slope=slope, out=h)
+            out, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
+                                    norm_eps=self.norm2.eps)
+            return ops.norm_act(out, s2, slope=slope, out=out)
         out = self.lrelu(self.norm1(self.conv1(inp)))
         return self.lrelu(self.norm2(self.conv2(out)))
 

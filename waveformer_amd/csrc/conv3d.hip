@@ -45,6 +45,8 @@ struct Conv3Args {
   int64_t nblocks;
   int ksplit;         // > 1: blockIdx.z takes chunks [z*nch/ksplit, (z+1)*nch/ksplit) and the
                       // epilogue atomically adds into a zeroed output (small grids only)
+  double* stats;      // (B, Cout, 2) fp64 {sum, sum of squares} accumulator or nullptr: the
+                      // InstanceNorm statistics of the output, fused into the epilogue
 };
 
 template <int CO_T, int NT, bool SPLIT>
@@ -215,6 +217,54 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
     }
   }
 
+  // ---- InstanceNorm statistics of this tile's outputs (ksplit == 1 only): per channel, the
+  // lane's NT positions, then the 16 lanes of its row (DPP), then the 4 waves (LDS), then one
+  // fp64 atomic per (channel, moment) per workgroup
+  if (a.stats && a.ksplit == 1) {
+    const bool rowok = y0 + wid < a.H;
+    f32x4 ps[CO_T], pq[CO_T];
+#pragma unroll
+    for (int m = 0; m < CO_T; ++m) {
+      ps[m] = f32x4{0, 0, 0, 0};
+      pq[m] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const bool ok = rowok && x0 + 16 * n + l15 < a.W;
+        f32x4 v = acc[m][n];
+        if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + co0 + 16 * m + 4 * g4);
+        if (ok) {
+          ps[m] += v;
+          pq[m] += v * v;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ps[m][i] = group_sum<16>(ps[m][i]);
+        pq[m][i] = group_sum<16>(pq[m][i]);
+      }
+    }
+    __syncthreads();  // every wave is done reading the chunk tiles: reuse the LDS
+    float* red = reinterpret_cast<float*>(lds);  // [4 waves][CO_T * 16][2]
+    if (l15 == 0) {
+#pragma unroll
+      for (int m = 0; m < CO_T; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 16 * m + 4 * g4 + i;
+          red[(wid * CO_T * 16 + c) * 2 + 0] = ps[m][i];
+          red[(wid * CO_T * 16 + c) * 2 + 1] = pq[m][i];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < CO_T * 16 * 2; i += 256) {
+      const int c = i >> 1, mom = i & 1;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) t += red[(w * CO_T * 16 + c) * 2 + mom];
+      atomicAdd(a.stats + ((int64_t)b * a.Cout + co0 + c) * 2 + mom, (double)t);
+    }
+  }
+
   // ---- epilogue: acc[m][n][i] = out[(z, y0 + wid, x0 + 16 n + l15)][co0 + 16 m + 4 g4 + i]
   const int gy = y0 + wid;
   if (gy >= a.H) return;
@@ -269,6 +319,7 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
                        dim3(256), 0, stream, a.out, a.ldo, a.Cout, total);
   }
   dim3 grid((unsigned)a.nblocks, (unsigned)(a.Cout / (16 * CO_T)), (unsigned)a.ksplit);
+  const bool post_stats = a.stats && a.ksplit > 1;  // partial outputs: a separate pass below
   if (prec == PREC_SPLIT) {
     auto kern = conv3d_k3_kernel<CO_T, NT, true>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -280,7 +331,10 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
   }
-  return check_launch("wf_conv3d_k3_fwd");
+  int rc = check_launch("wf_conv3d_k3_fwd");
+  if (rc || !post_stats) return rc;
+  return launch_instnorm_partial(a.out, a.ldo, a.B, a.Cout, (int64_t)a.D * a.H * a.W, a.stats,
+                                 stream);
 }
 
 }  // namespace wf
@@ -328,9 +382,9 @@ extern "C" int wf_conv3d_k3_pack(const float* w, uint16_t* packed, int64_t Cin, 
 }
 
 extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed,
-                                const float* bias, float* out, int64_t ldo, int64_t B,
-                                int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W,
-                                int precision, void* stream) {
+                                const float* bias, float* out, int64_t ldo, double* stats_acc,
+                                int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H,
+                                int64_t W, int precision, void* stream) {
   WF_REQUIRE(B >= 1 && D >= 1 && H >= 1 && W >= 1, "empty tensor");
   WF_REQUIRE(Cin >= 4 && Cin % 4 == 0 && ldx >= Cin && ldx % 4 == 0,
              "Cin must be a positive multiple of 4 with ldx >= Cin, ldx % 4 == 0");
@@ -353,6 +407,7 @@ extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_p
   a.Cin = (int)Cin;
   a.Cout = (int)Cout;
   a.nch = (int)cdiv(Cin, kConvCC);
+  a.stats = stats_acc;
   hipStream_t s = (hipStream_t)stream;
   const bool co3 = Cout % 48 == 0;
   if (W > 32) return co3 ? launch_conv3<3, 4>(a, precision, s) : launch_conv3<1, 4>(a, precision, s);

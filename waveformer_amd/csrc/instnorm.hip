@@ -10,7 +10,7 @@
 //   apply:  out = act((a - mean_a) * rstd_a + r'), r' = (r - mean_r) * rstd_r (norm3 of the
 //           1x1 residual), r itself, or 0; act = LeakyReLU(slope) (slope 1 = identity).
 // Both are one streaming pass over the tensor (HBM roofline).
-#include "wf_common.hpp"
+#include "kernels.hpp"
 
 namespace wf {
 
@@ -105,6 +105,31 @@ using namespace wf;
 
 extern "C" int64_t wf_instnorm_workspace_bytes(int64_t B, int64_t C) {
   return B * C * 2 * (int64_t)sizeof(double);
+}
+
+// partial sums into a zeroed (B, C, 2) fp64 accumulator (shared with conv3d.hip's split-K path)
+int wf::launch_instnorm_partial(const float* x, int64_t ldx, int64_t B, int64_t C, int64_t P,
+                            double* acc, hipStream_t s) {
+  const int C4 = (int)(C / 4);
+  const int R = 256 / C4;
+  int64_t chunks = cdiv(1024, B);
+  int64_t chunk = cdiv(P, chunks);
+  if (chunk < 4 * R) chunk = 4 * R;
+  chunks = cdiv(P, chunk);
+  const size_t lds = (size_t)R * C4 * 8 * sizeof(double);
+  hipLaunchKernelGGL(instnorm_partial_kernel, dim3((unsigned)chunks, (unsigned)B), dim3(256), lds,
+                     s, x, ldx, (int)C, P, chunk, acc);
+  return check_launch("instnorm partial sums");
+}
+
+extern "C" int wf_instnorm_finalize(const double* acc, float* stats, int64_t B, int64_t C,
+                                    int64_t P, float eps, void* stream) {
+  WF_REQUIRE(B >= 1 && C >= 1 && P >= 1, "empty tensor");
+  WF_REQUIRE_PTR(acc);
+  WF_REQUIRE_PTR(stats);
+  hipLaunchKernelGGL(instnorm_finalize_kernel, dim3((unsigned)cdiv(B * C, 256)), dim3(256), 0,
+                     (hipStream_t)stream, acc, stats, (int)B, (int)C, P, eps);
+  return check_launch("wf_instnorm_finalize");
 }
 
 extern "C" int wf_instnorm_stats_cl(const float* x, int64_t ldx, int64_t B, int64_t C,

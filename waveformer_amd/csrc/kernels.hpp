@@ -61,6 +61,10 @@ struct GemmArgs {
 };
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);
+// InstanceNorm partial sums (sum, sum of squares per (b, c)) of a channel-last tensor into a
+// zeroed (B, C, 2) fp64 accumulator (instnorm.hip)
+int launch_instnorm_partial(const float* x, int64_t ldx, int64_t B, int64_t C, int64_t P,
+                            double* acc, hipStream_t s);
 // streaming variant (gemm_rows.hip); returns 1 if it took the shape, 0 to fall back
 int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_only);
 

@@ -378,9 +378,11 @@ def conv3d_k3_packed(weight: torch.Tensor) -> torch.Tensor:
 
 
 def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, norm_eps: Optional[float] = None):
     """Conv3d(k=3, stride 1, padding 1) of an NCDHW-shaped fp32 tensor on the MFMA implicit-GEMM
-    kernel; the result is channels_last_3d (or written into `out`, a channel-last view)."""
+    kernel; the result is channels_last_3d (or written into `out`, a channel-last view).
+    With `norm_eps` it returns (out, stats): the InstanceNorm (B, 2, C) {mean, rstd} of the
+    output, accumulated in the conv's epilogue."""
     _check(x, "x", contiguous=False)
     x = to_cl(x)
     B, Cin, D, H, W = x.shape
@@ -394,9 +396,18 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor
     ldo = cl_ld(out)
     if ldo is None or tuple(out.shape) != (B, Cout, D, H, W):
         raise ValueError("conv3d_k3: out must be a channel-last (B, Cout, D, H, W) tensor")
+    acc = None
+    if norm_eps is not None:
+        acc = torch.zeros((B, Cout, 2), dtype=torch.float64, device=x.device)
     _lib.call("wf_conv3d_k3_fwd", x.data_ptr(), cl_ld(x), conv3d_k3_packed(weight).data_ptr(),
-              _ptr(bias), out.data_ptr(), ldo, B, Cin, Cout, D, H, W, _prec(), _stream())
-    return out
+              _ptr(bias), out.data_ptr(), ldo, _ptr(acc), B, Cin, Cout, D, H, W, _prec(),
+              _stream())
+    if acc is None:
+        return out
+    stats = torch.empty((B, 2, Cout), dtype=torch.float32, device=x.device)
+    _lib.call("wf_instnorm_finalize", acc.data_ptr(), stats.data_ptr(), B, Cout, D * H * W,
+              float(norm_eps), _stream())
+    return out, stats
 
 
 def conv1x1_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None
