@@ -378,6 +378,10 @@ int wf_haar_analysis_ncdhw(const float* in, int64_t in_bstride, int64_t in_cstri
 /* Adjoint of F.interpolate(trilinear, align_corners=False) along one axis
  * (wave_helper.py:500): in (outer, Lout, inner) -> out (outer, Lin, inner), optionally times
  * outer_scale[o / outer_per_scale] (the DropPath factor of the attention branch).           */
+/* The same for align_corners=True (ProjectionUpsample's nn.Upsample, wave_helper.py:33-81):
+ * three calls (x, y, z axes of a channel-last tensor) give the backward of upsample_cl.     */
+int wf_interp_adjoint_axis_ac(const float* in, float* out, int64_t outer, int64_t Lout,
+                              int64_t Lin, int64_t inner, void* stream);
 int wf_interp_adjoint_axis(const float* in, float* out, int64_t outer, int64_t Lout,
                            int64_t Lin, int64_t inner, const float* outer_scale,
                            int64_t outer_per_scale, void* stream);

@@ -168,3 +168,21 @@ def test_conv3d_k3_fused_instnorm_stats(B, Cin, Cout, S):
     rstd = 1.0 / torch.sqrt(o.var(dim=(2, 3, 4), unbiased=False) + 1e-5)
     assert C.rel_l2(st[:, 0], mean) <= 1e-5
     assert C.rel_l2(st[:, 1], rstd) <= 1e-5
+
+
+@pytest.mark.parametrize("src,s", [((4, 5, 6), 4), ((8, 7, 3), 2)])
+def test_upsample_cl_autograd_adjoint(src, s):
+    """Training path of ProjectionUpsample's nn.Upsample(align_corners=True): the HIP adjoint
+    (three separable gather passes) vs PyTorch's autograd of F.interpolate on the CPU."""
+    from waveformer_amd import autograd as wfa
+    x = seeded_randn((2, 8) + src, 17)
+    size = tuple(v * s for v in src)
+    g = seeded_randn((2, 8) + size, 18)
+    xc = x.clone().requires_grad_(True)
+    F.interpolate(xc, size=size, mode="trilinear", align_corners=True).backward(g)
+    xg = x.cuda().requires_grad_(True)
+    y = wfa.upsample_cl(xg, size)
+    want_y = F.interpolate(x, size=size, mode="trilinear", align_corners=True)
+    assert C.rel_l2(y, want_y) <= 1e-6
+    y.backward(g.cuda())
+    assert C.rel_l2(xg.grad, xc.grad) <= 1e-6

@@ -80,6 +80,7 @@ SIGNATURES = {
     "wf_haar_analysis_ncdhw": (_I, [_P, _I64, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _I64,
                                     _P]),
     "wf_interp_adjoint_axis": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _I64, _P]),
+    "wf_interp_adjoint_axis_ac": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P]),
     "wf_dwconv3d_cl": (_I, [_P, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwconv_wgrad_ws_floats": (_I64, [_I64, _I64]),
     "wf_dwconv3d_wgrad": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P]),

@@ -508,3 +508,38 @@ class ProjOutFn(torch.autograd.Function):
             dx, _, _ = ln_bwd(x.view(-1, C), None, None, ctx.eps, False, dcl.view(-1, C))
             dcl = dx.view_as(x)
         return dcl, None, None
+
+
+# ------------------------------------------------------------------------------------------
+# trilinear up-sampling (align_corners=True) of ProjectionUpsample, channel-last
+# ------------------------------------------------------------------------------------------
+class UpsampleCL(torch.autograd.Function):
+    """nn.Upsample(size, 'trilinear', align_corners=True) (wave_helper.py:33-81): forward =
+    wf_upsample_trilinear_cl, backward = its exact adjoint as three separable gather passes
+    (x, then y, then z; wf_interp_adjoint_axis_ac) -- no atomics, unlike the framework's
+    scatter-add backward (measured 13.7 ms per call at 64^3 x 192)."""
+
+    @staticmethod
+    def forward(ctx, x, size):
+        ctx.src = tuple(x.shape[2:])
+        return ops.upsample_cl(x, size, True)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, C, D, H, W = g.shape
+        d, h, w = ctx.src
+        g = g.contiguous(memory_format=torch.channels_last_3d)   # (B, D, H, W, C) storage
+        t1 = torch.empty((B, D, H, w, C), dtype=torch.float32, device=g.device)
+        _lib.call("wf_interp_adjoint_axis_ac", g.data_ptr(), t1.data_ptr(), B * D * H, W, w, C,
+                  _s())
+        t2 = torch.empty((B, D, h, w, C), dtype=torch.float32, device=g.device)
+        _lib.call("wf_interp_adjoint_axis_ac", t1.data_ptr(), t2.data_ptr(), B * D, H, h, w * C,
+                  _s())
+        t3 = torch.empty((B, d, h, w, C), dtype=torch.float32, device=g.device)
+        _lib.call("wf_interp_adjoint_axis_ac", t2.data_ptr(), t3.data_ptr(), B, D, d, h * w * C,
+                  _s())
+        return t3.permute(0, 4, 1, 2, 3), None
+
+
+def upsample_cl(x: torch.Tensor, size) -> torch.Tensor:
+    return UpsampleCL.apply(x, tuple(size))

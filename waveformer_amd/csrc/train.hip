@@ -533,11 +533,24 @@ __device__ __forceinline__ void lin_src(int p, int in, int out, int& i0, int& i1
   l0 = 1.f - l1;
 }
 
+// align_corners=True: src = p * (in - 1) / (out - 1) (PyTorch's area_pixel_compute_scale)
+__device__ __forceinline__ void lin_src_ac(int p, int in, int out, int& i0, int& i1, float& l0,
+                                           float& l1) {
+  const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  const float s = scale * (float)p;
+  i0 = min((int)s, in - 1);
+  l1 = fminf(fmaxf(s - (float)i0, 0.f), 1.f);
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l0 = 1.f - l1;
+}
+
+template <bool AC>
 __global__ __launch_bounds__(256) void interp_adjoint_kernel(
     const float* __restrict__ in, float* __restrict__ out, int64_t outer, int Lout, int Lin,
     int64_t inner, const float* __restrict__ oscale, int64_t outer_per_scale) {
   const int64_t n = outer * Lin * inner;
-  const float r = (float)Lout / (float)Lin;
+  const float r = AC ? (Lin > 1 ? (float)(Lout - 1) / (float)(Lin - 1) : (float)Lout)
+                     : (float)Lout / (float)Lin;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = idx % inner;
@@ -553,7 +566,8 @@ __global__ __launch_bounds__(256) void interp_adjoint_kernel(
     for (int p = pmin; p <= pmax; ++p) {
       int i0, i1;
       float l0, l1;
-      lin_src(p, Lin, Lout, i0, i1, l0, l1);
+      if (AC) lin_src_ac(p, Lin, Lout, i0, i1, l0, l1);
+      else lin_src(p, Lin, Lout, i0, i1, l0, l1);
       float wgt = (i0 == i ? l0 : 0.f) + (i1 == i ? l1 : 0.f);
       if (wgt != 0.f) acc = fmaf(wgt, src[(int64_t)p * inner], acc);
     }
@@ -970,10 +984,23 @@ extern "C" int wf_interp_adjoint_axis(const float* in, float* out, int64_t outer
   WF_REQUIRE_PTR(in);
   WF_REQUIRE_PTR(out);
   const int64_t n = outer * Lin * inner;
-  hipLaunchKernelGGL(interp_adjoint_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
-                     in, out, outer, (int)Lout, (int)Lin, inner, outer_scale,
+  hipLaunchKernelGGL(interp_adjoint_kernel<false>, dim3(grid_for(n)), dim3(256), 0,
+                     (hipStream_t)stream, in, out, outer, (int)Lout, (int)Lin, inner, outer_scale,
                      outer_per_scale > 0 ? outer_per_scale : outer);
   return check_launch("wf_interp_adjoint_axis");
+}
+
+extern "C" int wf_interp_adjoint_axis_ac(const float* in, float* out, int64_t outer,
+                                         int64_t Lout, int64_t Lin, int64_t inner,
+                                         void* stream) {
+  WF_REQUIRE(outer >= 1 && Lout >= 1 && Lin >= 1 && inner >= 1, "empty interpolation axis");
+  WF_REQUIRE_PTR(in);
+  WF_REQUIRE_PTR(out);
+  const int64_t n = outer * Lin * inner;
+  hipLaunchKernelGGL(interp_adjoint_kernel<true>, dim3(grid_for(n)), dim3(256), 0,
+                     (hipStream_t)stream, in, out, outer, (int)Lout, (int)Lin, inner, nullptr,
+                     outer);
+  return check_launch("wf_interp_adjoint_axis_ac");
 }
 
 extern "C" int wf_dwconv3d_cl(const float* in, const float* w, const float* bias, int flip,
