@@ -209,7 +209,7 @@ extern "C" int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float*
   const bool ln = ln_w != nullptr;
   if (ln) WF_REQUIRE_PTR(ln_b);
   const int64_t total = B * (D / 2) * (H / 2) * (W / 2);
-  return dispatch_gv(C / 4, [&](auto G_, auto V_) -> int {
+  auto go = [&](auto G_, auto V_) -> int {
     constexpr int G = decltype(G_)::value, V = decltype(V_)::value;
     const int gpb = 256 / G;
     int64_t blocks = cdiv(total, gpb);
@@ -223,7 +223,12 @@ extern "C" int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float*
                          0, (hipStream_t)stream, x, ln_w, ln_b, ln_eps, bands, (int)B, (int)C,
                          (int)D, (int)H, (int)W);
     return check_launch("wf_dwt3d_haar_fwd");
-  });
+  };
+  // C = 48 (stage 1, the 400 MB launch): 16 lanes x 1 float4 per position instead of 4 x 3
+  // (4 idle lanes) -- 32 data VGPRs instead of 96, so the whole grid is resident at once
+  static const bool wide = getenv("WF_DWT_G4") == nullptr;
+  if (wide && C == 48) return go(ic<16>{}, ic<1>{});
+  return dispatch_gv(C / 4, go);
 }
 
 extern "C" int wf_idwt3d_haar(const float* ll, int64_t ll_bstride, const float* const* det,
