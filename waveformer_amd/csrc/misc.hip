@@ -206,6 +206,17 @@ __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
   const int z = r % a.D;
   const int b = r / a.D;
   const int tid = threadIdx.x;
+  // the shortcut row of this thread's first output position, issued before the source
+  // staging so its latency overlaps it (a group owns one position when W <= 256 / G)
+  const int lane0 = tid & 63, gl0 = lane0 & (G - 1);
+  const int64_t rowbase0 = (((int64_t)b * a.D + z) * a.H + y) * a.W;
+  const int xf = tid / G;
+  f32x4 scp[V];
+  if (xf < a.W) {
+    const f32x4* sc0 = reinterpret_cast<const f32x4*>(a.shortcut + (rowbase0 + xf) * C);
+#pragma unroll
+    for (int j = 0; j < V; ++j) scp[j] = sc0[min(gl0 + j * G, C4 - 1)];
+  }
   int roff[4];
   int ro = 0;
   for (int s = 0; s < a.nsrc; ++s) {
@@ -257,7 +268,7 @@ __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const int c4 = min(gl + j * G, C4 - 1);
-      const f32x4 o = sc[c4] + acc[j] * bs;
+      const f32x4 o = (x == xf ? scp[j] : sc[c4]) + acc[j] * bs;
       v[j] = live[j] ? o : f32x4{0, 0, 0, 0};
       if (live[j]) dst[c4] = o;
     }
