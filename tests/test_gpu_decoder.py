@@ -186,3 +186,24 @@ def test_upsample_cl_autograd_adjoint(src, s):
     assert C.rel_l2(y, want_y) <= 1e-6
     y.backward(g.cuda())
     assert C.rel_l2(xg.grad, xc.grad) <= 1e-6
+
+
+@pytest.mark.parametrize("cin,cout,S", [(48, 48, (6, 7, 20)), (4, 48, (5, 5, 9)), (96, 16, (4, 6, 5))])
+def test_conv3d_k3_autograd(cin, cout, S):
+    """Training path of the decoder conv (wfa.Conv3dK3): forward on the MFMA kernel, input
+    gradient on the same kernel with flipped / transposed weights (or the framework's when
+    Cin % 16 != 0), weight / bias gradients from the framework; vs CPU autograd, rel-L2 1e-5."""
+    from waveformer_amd import autograd as wfa
+    x = seeded_randn((2, cin) + S, 19)
+    w = seeded_randn((cout, cin, 3, 3, 3), 20) * (cin * 27) ** -0.5
+    b = seeded_randn((cout,), 21)
+    g = seeded_randn((2, cout) + S, 22)
+    xc, wc, bc = (t.clone().requires_grad_(True) for t in (x, w, b))
+    F.conv3d(xc, wc, bc, padding=1).backward(g)
+    xg, wg, bg = (t.cuda().requires_grad_(True) for t in (x, w, b))
+    y = wfa.conv3d_k3(xg, wg, bg)
+    y.backward(g.cuda())
+    assert C.rel_l2(y, F.conv3d(x, w, b, padding=1)) <= 1e-5
+    assert C.rel_l2(xg.grad, xc.grad) <= 1e-5
+    assert C.rel_l2(wg.grad, wc.grad) <= 1e-5
+    assert C.rel_l2(bg.grad, bc.grad) <= 1e-5

@@ -543,3 +543,41 @@ class UpsampleCL(torch.autograd.Function):
 
 def upsample_cl(x: torch.Tensor, size) -> torch.Tensor:
     return UpsampleCL.apply(x, tuple(size))
+
+
+# ------------------------------------------------------------------------------------------
+# decoder 3x3x3 convolution (MONAI Convolution / UnetResBlock conv1, conv2) for training
+# ------------------------------------------------------------------------------------------
+class Conv3dK3(torch.autograd.Function):
+    """Conv3d(k=3, stride 1, padding 1) on the implicit-GEMM MFMA kernel (bf16x3) with its
+    input gradient on the same kernel: dx = conv(dy, W~), W~[ci, co, k] = W[co, ci, 26 - k]
+    (flipped taps, swapped channels).  The weight gradient is the framework's conv3d_weight
+    (MIOpen), as in the reference's training."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xc = ops.to_cl(x)
+        ctx.save_for_backward(xc, w)
+        ctx.has_bias = b is not None
+        return ops.conv3d_k3(xc, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, w = ctx.saved_tensors
+        g = ops.to_cl(g)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if w.shape[1] % 16 == 0 and w.shape[0] % 4 == 0:
+                wt = w.detach().flip(2, 3, 4).transpose(0, 1).contiguous()
+                dx = ops.conv3d_k3(g, wt)
+            else:
+                dx = torch.nn.grad.conv3d_input(xc.shape, w, g, padding=1)
+        if ctx.needs_input_grad[1]:
+            dw = torch.nn.grad.conv3d_weight(xc, w.shape, g, padding=1)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = g.sum(dim=(0, 2, 3, 4))
+        return dx, dw, db
+
+
+def conv3d_k3(x, w, b=None):
+    return Conv3dK3.apply(x, w, b)

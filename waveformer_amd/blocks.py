@@ -17,6 +17,7 @@ from typing import Sequence, Tuple, Union
 import torch
 import torch.nn as nn
 
+from . import autograd as wfa
 from . import ops
 
 
@@ -74,6 +75,10 @@ class Convolution(nn.Sequential):
         conv = self.conv
         if _fast_ok(x, self) and _k3_ok(conv, x.shape[1]):
             return ops.conv3d_k3(x, conv.weight, conv.bias)
+        if x.is_cuda and x.dtype == torch.float32 and x.dim() == 5 and _k3_ok(conv, x.shape[1]):
+            # training (autograd recording): the MFMA conv forward and input gradient
+            # (wfa.Conv3dK3, channel-last), MIOpen for the weight gradient
+            return wfa.conv3d_k3(x, conv.weight, conv.bias)
         return conv(x)
 
 
