@@ -368,7 +368,8 @@ def conv3d_k3_packed(weight: torch.Tensor) -> torch.Tensor:
     if ent is not None and ent[0] == ver and ent[1] == weight.data_ptr():
         return ent[2]
     w = weight.detach()
-    _check(w, "conv weight")
+    _check(w, "conv weight", contiguous=False)
+    w = w.contiguous()  # a channels_last_3d model keeps its 5-D weights channel-last
     Cout, Cin = w.shape[:2]
     n = _lib.query("wf_conv3d_k3_packed_elems", Cin, Cout)
     out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
