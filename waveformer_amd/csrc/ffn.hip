@@ -201,14 +201,38 @@ struct Vec16<uint16_t> {
   }
 };
 
-constexpr int DW_CH = 32, DW_TX = 8, DW_TY = 8;
+constexpr int DW_CH = 32, DW_TX = 16, DW_TY = 8;
 
+template <typename T>
+struct Store2;
+template <>
+struct Store2<float> {
+  static __device__ __forceinline__ void put(float* p, f32x2 v) {
+    *reinterpret_cast<f32x2*>(p) = v;
+  }
+  static __device__ __forceinline__ f32x2 round(f32x2 v) { return v; }
+};
+template <>
+struct Store2<uint16_t> {
+  static __device__ __forceinline__ void put(uint16_t* p, f32x2 v) {
+    *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+  }
+  static __device__ __forceinline__ f32x2 round(f32x2 v) {  // statistics of the stored values
+    return f32x2{bf2f(f2bf(v.x)), bf2f(f2bf(v.y))};
+  }
+};
+
+// 256 threads = DW_TX columns x 16 channel PAIRS: each thread owns two adjacent channels of
+// one x column and the TY outputs of that column, so the 27-tap accumulation runs as packed
+// v_pk_fma_f32 on the pair (half the VALU instructions of one-channel-per-thread), and the
+// per-position 32-channel statistics reduce over 16 lanes.
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv3d_kernel(
     const T* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias,
     T* __restrict__ out, float* __restrict__ pstats, int B, int Hd, int D, int H, int W, int ZS) {
   constexpr int CH = DW_CH, TX = DW_TX, TY = DW_TY;
   static_assert(CH == DW_STAT_GROUP, "one statistics group per workgroup channel chunk");
+  static_assert(TX * (CH / 2) == 256, "one thread per (column, channel pair)");
   constexpr int PY = TY + 2, PX = TX + 2;
   typedef Vec16<T> V;
   constexpr int NV = CH / V::N;                  // 16-byte vectors per tile position
@@ -234,12 +258,13 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
   const int x0 = xt * TX, y0 = yt * TY, z0 = zt * ZS, z1 = min(z0 + ZS, D);
   const int c0 = cc * CH;
   const int tid = threadIdx.x;
-  const int ch = tid % CH, xi = tid / CH;
+  const int cp = tid % (CH / 2), xi = tid / (CH / 2);
 
-  float wt[27];
+  f32x2 w2[27];
 #pragma unroll
-  for (int k = 0; k < 27; ++k) wt[k] = w[(c0 + ch) * 27 + k];
-  const float bv = bias[c0 + ch];
+  for (int k = 0; k < 27; ++k)
+    w2[k] = f32x2{w[(c0 + 2 * cp) * 27 + k], w[(c0 + 2 * cp + 1) * 27 + k]};
+  const f32x2 bv = f32x2{bias[c0 + 2 * cp], bias[c0 + 2 * cp + 1]};
 
   // staging of one input plane: item i -> (tile position i / NV, vector i % NV)
   typename V::raw stg[NLD];
@@ -267,9 +292,9 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
     }
   };
 
-  float accA[TY], accB[TY], accC[TY];
+  f32x2 accA[TY], accB[TY], accC[TY];
 #pragma unroll
-  for (int o = 0; o < TY; ++o) accA[o] = accB[o] = accC[o] = 0.f;
+  for (int o = 0; o < TY; ++o) accA[o] = accB[o] = accC[o] = f32x2{0.f, 0.f};
   const int xo = x0 + xi;
   fetch(z0 - 1);
   commit(0);
@@ -277,37 +302,38 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
   int buf = 0;
   for (int p = z0 - 1; p <= z1; ++p) {
     fetch(p + 1);  // next plane in flight during this plane's arithmetic (past z1: unused)
-    const float* P = pl[buf] + xi * CH + ch;
+    const float* P = pl[buf] + xi * CH + 2 * cp;
     // plane p feeds output p+1 (kz = 0), p (kz = 1) and p-1 (kz = 2)
 #pragma unroll
     for (int r = 0; r < PY; ++r) {
-      const float v0 = P[(r * PX + 0) * CH], v1 = P[(r * PX + 1) * CH], v2 = P[(r * PX + 2) * CH];
+      const f32x2 v0 = *reinterpret_cast<const f32x2*>(P + (r * PX + 0) * CH);
+      const f32x2 v1 = *reinterpret_cast<const f32x2*>(P + (r * PX + 1) * CH);
+      const f32x2 v2 = *reinterpret_cast<const f32x2*>(P + (r * PX + 2) * CH);
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky) {
         const int o = r - ky;  // output row fed by input row r through tap ky
         if (o < 0 || o >= TY) continue;
-        const float* w0 = wt + ky * 3;
-        accC[o] += w0[0] * v0 + w0[1] * v1 + w0[2] * v2;
-        accB[o] += w0[9] * v0 + w0[10] * v1 + w0[11] * v2;
-        accA[o] += w0[18] * v0 + w0[19] * v1 + w0[20] * v2;
+        const f32x2* w0 = w2 + ky * 3;
+        // one packed FMA per tap into the running sum
+        accC[o] = w0[2] * v2 + (w0[1] * v1 + (w0[0] * v0 + accC[o]));
+        accB[o] = w0[11] * v2 + (w0[10] * v1 + (w0[9] * v0 + accB[o]));
+        accA[o] = w0[20] * v2 + (w0[19] * v1 + (w0[18] * v0 + accA[o]));
       }
     }
     // output plane p-1 is complete
     const int zo = p - 1;
     if (zo >= z0) {
-      float r1[TY], mu[TY], m2[TY];
+      f32x2 r1[TY];
 #pragma unroll
-      for (int o = 0; o < TY; ++o) {
-        r1[o] = accA[o] + bv;
-        if (sizeof(T) == 2) r1[o] = bf2f(f2bf(r1[o]));  // statistics of the stored values
-      }
-      if (pstats) {  // {mean, M2} of this 32-channel group (32 consecutive lanes) per position
+      for (int o = 0; o < TY; ++o) r1[o] = Store2<T>::round(accA[o] + bv);
+      float mu[TY], m2[TY];
+      if (pstats) {  // {mean, M2} of this 32-channel group (16 consecutive lanes) per position
 #pragma unroll
-        for (int o = 0; o < TY; ++o) mu[o] = group_sum<32>(r1[o]) * (1.f / 32.f);
+        for (int o = 0; o < TY; ++o) mu[o] = group_sum<16>(r1[o].x + r1[o].y) * (1.f / 32.f);
 #pragma unroll
         for (int o = 0; o < TY; ++o) {
-          const float d = r1[o] - mu[o];
-          m2[o] = group_sum<32>(d * d);
+          const float dx = r1[o].x - mu[o], dy = r1[o].y - mu[o];
+          m2[o] = group_sum<16>(dx * dx + dy * dy);
         }
       }
       if (xo < W) {
@@ -316,10 +342,8 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
           const int yo = y0 + o;
           if (yo < H) {
             const int64_t pos = (((int64_t)b * D + zo) * H + yo) * W + xo;
-            T* dst = out + pos * Hd + c0 + ch;
-            if (sizeof(T) == 4) *reinterpret_cast<float*>(dst) = r1[o];
-            else *reinterpret_cast<uint16_t*>(dst) = f2bf(r1[o]);
-            if (pstats && ch == 0)
+            Store2<T>::put(out + pos * Hd + c0 + 2 * cp, r1[o]);
+            if (pstats && cp == 0)
               *reinterpret_cast<float2*>(pstats + (pos * ncc + cc) * 2) = float2{mu[o], m2[o]};
           }
         }
@@ -329,7 +353,7 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
     for (int o = 0; o < TY; ++o) {
       accA[o] = accB[o];
       accB[o] = accC[o];
-      accC[o] = 0.f;
+      accC[o] = f32x2{0.f, 0.f};
     }
     commit(buf ^ 1);
     __syncthreads();
