@@ -195,9 +195,11 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
         for (int ky = 0; ky < 3; ++ky) {
           const int o = r - ky;
           if (o < 0 || o >= TY) continue;
-          accC[o] += w2[ky * 3 + 0] * v0 + w2[ky * 3 + 1] * v1 + w2[ky * 3 + 2] * v2;
-          accB[o] += w2[9 + ky * 3 + 0] * v0 + w2[9 + ky * 3 + 1] * v1 + w2[9 + ky * 3 + 2] * v2;
-          accA[o] += w2[18 + ky * 3 + 0] * v0 + w2[18 + ky * 3 + 1] * v1 + w2[18 + ky * 3 + 2] * v2;
+          // one packed FMA per tap into the running sum
+          const f32x2* w0 = w2 + ky * 3;
+          accC[o] = w0[2] * v2 + (w0[1] * v1 + (w0[0] * v0 + accC[o]));
+          accB[o] = w0[11] * v2 + (w0[10] * v1 + (w0[9] * v0 + accB[o]));
+          accA[o] = w0[20] * v2 + (w0[19] * v1 + (w0[18] * v0 + accA[o]));
         }
         __builtin_amdgcn_sched_barrier(0);  // one input row in flight at a time (VGPRs)
       }
