@@ -87,8 +87,7 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
   float* fcb = lnb + HID;                                         // [C]
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
-  const int l15 = lane & 15, g4 = lane >> 4;
+  const int wid = tid >> 6;
   const int D = a.D, H = a.H, W = a.W;
 
   // ---- tile of this workgroup (XCD-contiguous order: neighbouring tiles, which share halo
@@ -169,8 +168,6 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
 #pragma unroll
   for (int o = 0; o < TY; ++o) accA[o] = accB[o] = accC[o] = f32x2{0.f, 0.f};
 
-  // fc role of this wave: position tile rt, output-channel tile ct
-  const int rt = wid / K::CT, ct = wid % K::CT;
   const int64_t plane_sz = (int64_t)H * W;
 
   // Schedule per input plane p (3 barriers): scatter(p) | C | commit(p+1) into the other plane
@@ -224,8 +221,14 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
     __syncthreads();  // A: h2 tile and plane p+1 visible
     if (zo >= z0) {
       // ---- LN2 + GELU per position, rewritten in place as bf16 {hi[HID], lo[HID]}
-      if (tid < K::NPOS * K::LN_LANES) {
-        const int pos = tid / K::LN_LANES, g = tid % K::LN_LANES;
+      // Loop-invariant per-lane values of the LN2 and epilogue phases are recomputed from a
+      // laundered thread index every plane: hoisted out of the z loop they exceed the
+      // 168-VGPR budget and spill, and each scratch reload's vmcnt(0) would also wait out the
+      // in-flight fetch(p + 2), exposing its HBM latency once per plane.
+      int ltid = tid;
+      asm volatile("" : "+v"(ltid));
+      if (ltid < K::NPOS * K::LN_LANES) {
+        const int pos = ltid / K::LN_LANES, g = ltid % K::LN_LANES;
         float* row = h2t + pos * K::HS;
         float v[K::LN_CH];
 #pragma unroll
@@ -270,7 +273,9 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
         }
       }
       // residual inputs of this lane's epilogue row, in flight during the barrier + GEMM
-      const int lp = rt * 16 + l15;                 // tile position of this lane's row
+      const int lln = ltid & 63, lwid = ltid >> 6;
+      const int ct = lwid % K::CT, l15 = lln & 15, g4 = lln >> 4;  // fc tile of this wave
+      const int lp = (lwid / K::CT) * 16 + l15;  // tile position of this lane's row
       const int yo = y0 + lp / TX, xo = x0 + lp % TX;
       const bool rv = yo < H && xo < W;
       const int64_t gpos = (int64_t)b * D * plane_sz + (int64_t)zo * plane_sz +
