@@ -159,10 +159,7 @@ __global__ __launch_bounds__(512) void dwconv_ln_gelu_kernel(
     f32x4 v = (reinterpret_cast<const f32x4*>(rb + (size_t)p * HP)[c] - st[2 * p]) * st[2 * p + 1] *
                   lw + lb;
     T* dst = out + ((((int64_t)b * D + z) * H + yy) * W + xx) * Hd + 4 * c;
-    v.x = gelu_erf(v.x);
-    v.y = gelu_erf(v.y);
-    v.z = gelu_erf(v.z);
-    v.w = gelu_erf(v.w);
+    v = gelu_erf4(v);
     S::store4(dst, v);
   }
 }

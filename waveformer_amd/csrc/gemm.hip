@@ -181,8 +181,7 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
           for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * wv[j] + bv[j];
         }
         if (g.a_gelu) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+          gelu_erf8(v);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -278,10 +277,7 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
       const f32x4 lw = reinterpret_cast<const f32x4*>(g.e_ln_w)[c4];
       const f32x4 lb = reinterpret_cast<const f32x4*>(g.e_ln_b)[c4];
       v = (v - st[2 * r]) * st[2 * r + 1] * lw + lb;
-      v.x = gelu_erf(v.x);
-      v.y = gelu_erf(v.y);
-      v.z = gelu_erf(v.z);
-      v.w = gelu_erf(v.w);
+      v = gelu_erf4(v);
     } else if (g.epi == EPI_RESID) {
       const f32x4 xr = reinterpret_cast<const f32x4*>(g.r_x + m * (int64_t)N)[c4];
       const float bs = g.r_scale ? g.r_scale[m / g.rows_per_sample] : 1.f;

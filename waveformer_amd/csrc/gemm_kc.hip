@@ -202,8 +202,7 @@ __global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
           for (int j = 0; j < 8; ++j) v[rt][j] = (v[rt][j] - mean[rt]) * rstd[rt] * wv[j] + bv[j];
         }
         if (g.a_gelu) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[rt][j] = gelu_erf(v[rt][j]);
+          gelu_erf8(v[rt]);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -281,10 +280,7 @@ __global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
         const f32x4 lw = *reinterpret_cast<const f32x4*>(g.e_ln_w + colc);
         const f32x4 lb = *reinterpret_cast<const f32x4*>(g.e_ln_b + colc);
         v = (v - rm_) * rs_ * lw + lb;
-        v.x = gelu_erf(v.x);
-        v.y = gelu_erf(v.y);
-        v.z = gelu_erf(v.z);
-        v.w = gelu_erf(v.w);
+        v = gelu_erf4(v);
       } else if (EPI == EPI_RESID) {
         const f32x4 xr = *reinterpret_cast<const f32x4*>(g.r_x + (int64_t)rowc * N + colc);
         if (g.r_stats) {

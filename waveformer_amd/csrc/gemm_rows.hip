@@ -160,8 +160,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
         for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * wv[j] + bv[j];
       }
       if (g.a_gelu) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+        gelu_erf8(v);
       }
       bf16x8 ah, al;
 #pragma unroll
@@ -234,10 +233,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
         const f32x4 lw = *reinterpret_cast<const f32x4*>(elw + t * 16 + 4 * g4);
         const f32x4 lb = *reinterpret_cast<const f32x4*>(elb + t * 16 + 4 * g4);
         v = (v - rm_) * rs_ * lw + lb;
-        v.x = gelu_erf(v.x);
-        v.y = gelu_erf(v.y);
-        v.z = gelu_erf(v.z);
-        v.w = gelu_erf(v.w);
+        v = gelu_erf4(v);
       } else if (EPI == EPI_RESID) {
         const f32x4 xr = *reinterpret_cast<const f32x4*>(g.r_x + (int64_t)rowc * N + colc);
         if (g.r_stats) {

@@ -76,6 +76,21 @@ __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
   return hx * f32x2{copysignf(erfa.x, x.x), copysignf(erfa.y, x.y)} + hx;
 }
 
+// four / eight lanes' worth as packed pairs (bitwise equal to gelu_erf with FMA contraction)
+__device__ __forceinline__ f32x4 gelu_erf4(f32x4 v) {
+  const f32x2 a = gelu_erf2(f32x2{v.x, v.y});
+  const f32x2 b = gelu_erf2(f32x2{v.z, v.w});
+  return f32x4{a.x, a.y, b.x, b.y};
+}
+__device__ __forceinline__ void gelu_erf8(float* v) {
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const f32x2 r = gelu_erf2(f32x2{v[j], v[j + 1]});
+    v[j] = r.x;
+    v[j + 1] = r.y;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // sub-wave reductions: a "row group" is G consecutive lanes (G a power of two <= 64)
 // ---------------------------------------------------------------------------------------
