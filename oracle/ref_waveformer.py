@@ -14,7 +14,7 @@ Third-party arithmetic restated here:
 from __future__ import annotations
 
 import math
-from typing import Dict, List, Mapping, Sequence, Tuple
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -208,9 +208,18 @@ def patch_merging(sd: SD, p: str, x: Tensor, eps: float = 1e-6) -> Tensor:
 # ----------------------------------------------------------------------------------------
 # Block (network_models/wave_helper.py:357-549)
 # ----------------------------------------------------------------------------------------
+def _dp(t: Tensor, s: Optional[Tensor]) -> Tensor:
+    """DropPath with given per-sample factors (timm drop_path: x * mask / keep, the
+    `self.drop_path(...)` calls at wave_helper.py:507-508 / :546-547); None = identity."""
+    return t if s is None else t * s.view((-1,) + (1,) * (t.dim() - 1))
+
+
 def block(sd: SD, p: str, x: Tensor, heads: int, level: int, img_size: Sequence[int],
-          ms_attention: bool = True, eps: float = 1e-6):
-    """Block.forward -> multi_scale_forward (:470-512) or single_scale_forward (:515-549)."""
+          ms_attention: bool = True, eps: float = 1e-6,
+          drop_scales: Optional[Tuple[Tensor, Tensor]] = None):
+    """Block.forward -> multi_scale_forward (:470-512) or single_scale_forward (:515-549).
+    drop_scales = (attention-branch, FFN-branch) per-sample DropPath factors (training)."""
+    s_attn, s_mlp = drop_scales if drop_scales is not None else (None, None)
     D, H, W = img_size
     ws = img_size[0] // (2 ** level)
     B, _, _, _, C = x.shape
@@ -235,9 +244,9 @@ def block(sd: SD, p: str, x: Tensor, heads: int, level: int, img_size: Sequence[
                 hfs.append(det)
             else:
                 fused = fused + a
-        fused = shortcut + fused.permute(0, 2, 3, 4, 1)
+        fused = shortcut + _dp(fused.permute(0, 2, 3, 4, 1), s_attn)
         n2 = F.layer_norm(fused, [C], sd[p + "norm2.weight"], sd[p + "norm2.bias"], eps)
-        out = fused + ccf_ffn(sd, p + "mlp.", n2)  # quirk Q4: CCF_FFN already adds n2
+        out = fused + _dp(ccf_ffn(sd, p + "mlp.", n2), s_mlp)  # Q4: CCF_FFN already adds n2
         if level > 0:
             return out, tuple(reversed(hfs))
         return out
@@ -252,9 +261,9 @@ def block(sd: SD, p: str, x: Tensor, heads: int, level: int, img_size: Sequence[
     if level > 0:
         a = F.interpolate(a.permute(0, 4, 1, 2, 3), size=(D, H, W), mode="trilinear")
         a = a.permute(0, 2, 3, 4, 1)
-    x = shortcut + a
+    x = shortcut + _dp(a, s_attn)
     n2 = F.layer_norm(x, [C], sd[p + "norm2.weight"], sd[p + "norm2.bias"], eps)
-    x = x + ccf_ffn(sd, p + "mlp.", n2)
+    x = x + _dp(ccf_ffn(sd, p + "mlp.", n2), s_mlp)
     if level > 0:
         return x, x_h
     return x

@@ -559,7 +559,8 @@ class Conv3dK3(torch.autograd.Function):
         xc = ops.to_cl(x)
         ctx.save_for_backward(xc, w)
         ctx.has_bias = b is not None
-        return ops.conv3d_k3(xc, w, b)
+        with ops.precision("bf16x3"):  # training is fp32-faithful whatever the global mode
+            return ops.conv3d_k3(xc, w, b)
 
     @staticmethod
     def backward(ctx, g):
@@ -569,7 +570,8 @@ class Conv3dK3(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if w.shape[1] % 16 == 0 and w.shape[0] % 4 == 0:
                 wt = w.detach().flip(2, 3, 4).transpose(0, 1).contiguous()
-                dx = ops.conv3d_k3(g, wt)
+                with ops.precision("bf16x3"):
+                    dx = ops.conv3d_k3(g, wt)
             else:
                 dx = torch.nn.grad.conv3d_input(xc.shape, w, g, padding=1)
         if ctx.needs_input_grad[1]:
