@@ -43,7 +43,8 @@ METRIC = "128³×4 volumes/sec fwd (1/2/4/8 MI355X) + Dice Δ vs reference"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 # bench op name -> kernel-name substring in the PMC summary (profiles/*pmc*.json)
-PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_dwfc_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
+PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_fused_kernel" if os.environ.get("WF_FFN_FUSED")
+              else "ffn_dwfc_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
               "window_attention": "attn_core_kernel",
               "msfuse": "msfuse", "proj_out": "proj_out"}
 
@@ -60,6 +61,9 @@ def parse():
     ap.add_argument("--roofline-op", default="auto")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--parity", type=int, default=1)
+    ap.add_argument("--op-timers", type=int, default=1,
+                    help="0: skip the per-op roofline timing after the timed region (a rocprof "
+                         "trace then holds the warm-up and the graph replays only)")
     ap.add_argument("--img", type=int, default=128)
     ap.add_argument("--workload", default="encoder", choices=["encoder", "sliding", "train"],
                     help="encoder: config 2 (the driver's line); sliding: config 3, one "
@@ -81,22 +85,25 @@ def parse():
 # ------------------------------------------------------------------------------------------
 # per-launch timing of one op with HIP events on its stream
 # ------------------------------------------------------------------------------------------
-def _dwfc_fused(a):
-    """ops.ccf_ffn_dwconv(args, positions, hidden): stage 2 runs the fused back half of the FFN
-    (ffn_dwfc.hip) for C = 48, hidden = 192 (args[20] = C)."""
+def _stage1(a):
+    """ops.ccf_ffn_dwconv(args, positions, hidden) of the stage-1 shape (args[20] = C = 48,
+    hidden 192): stage 2 is ffn_dwfc.hip (dwconv + LN2 + GELU + fc + residual), or with
+    WF_FFN_FUSED=1 the whole CCF_FFN in one kernel (ffn_fused.hip)."""
     return a[0][20] == 48 and a[2] == 192
 
 
 def _dw_bytes(a, kw, out):
-    """CCF_FFN stage 2.  Fused (C 48 / hidden 192): read h1 (positions x hidden, fp32 for
-    bf16x3, bf16 for bf16) + the residual rows x and their norm2 stats, write out.  Unfused:
-    read h1 + write h2 + the (mean, M2) partial per 32 channels of every position."""
+    """CCF_FFN stage 2.  Stage 1 (C 48 / hidden 192): ffn_dwfc reads h1 (fp32 for bf16x3, bf16
+    for bf16) + the residual rows x and their norm2 stats, writes out; the whole-FFN kernel
+    reads x + stats and writes out (h1 / h2 stay on chip).  Other stages: read h1 + write h2 +
+    the (mean, M2) partial per 32 channels of every position."""
     from waveformer_amd import ops
     P, Hd = a[1], a[2]
     e = 4 if ops.get_precision() == "bf16x3" else 2
-    if _dwfc_fused(a):
+    if _stage1(a):
         C = a[0][20]
-        return P * Hd * e + 2 * P * C * 4 + (P * 8 if a[0][1] else 0)
+        io = 2 * P * C * 4 + (P * 8 if a[0][1] else 0)
+        return io if os.environ.get("WF_FFN_FUSED") else io + P * Hd * e
     return 2 * P * Hd * e + P * (Hd // 32) * 8
 
 
@@ -499,14 +506,16 @@ def main():
 
     # per-launch roofline timing of the dominant streaming kernel (eager launches, so the HIP
     # events sit on the launch stream around each launch)
-    for t in timers.values():
-        t.active = True
-    with torch.no_grad():
-        for _ in range(max(2, min(args.steps, 10))):
-            model(x)
-    for t in timers.values():
-        t.active = False
-    roofs = {n: t.summary() for n, t in timers.items()}
+    roofs = {}
+    if args.op_timers:
+        for t in timers.values():
+            t.active = True
+        with torch.no_grad():
+            for _ in range(max(2, min(args.steps, 10))):
+                model(x)
+        for t in timers.values():
+            t.active = False
+        roofs = {n: t.summary() for n, t in timers.items()}
 
     if rank == 0:
         vols = args.batch * args.steps * world

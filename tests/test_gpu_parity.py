@@ -192,6 +192,16 @@ def test_ccf_ffn_stage1_fused_vs_oracle(shape, block):
         assert C.rel_l2(out, ref) <= tol, prec
 
 
+@pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (1, 16, 16, 16), (1, 3, 12, 9)])
+@pytest.mark.parametrize("block", [False, True])
+def test_ccf_ffn_stage1_whole_kernel_vs_oracle(shape, block, monkeypatch):
+    """The opt-in whole-FFN kernel (WF_FFN_FUSED=1, ffn_fused.hip: pw + LN1 + GELU recomputed
+    on chip per haloed plane, dwconv, LN2, GELU, fc, Q4 residual) on the same cases and bars as
+    the staged path above, ragged tiles and volume edges included."""
+    monkeypatch.setenv("WF_FFN_FUSED", "1")
+    test_ccf_ffn_stage1_fused_vs_oracle(shape, block)
+
+
 def test_window_attention_q1_layout_on_raster():
     """Raster attention == window_partition -> Attention -> plain reshape (quirk Q1)."""
     import waveformer_amd.network_models as NM

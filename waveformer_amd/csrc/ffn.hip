@@ -507,6 +507,38 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   static const bool no_split_ln1 = getenv("WF_FFN_NO_SPLIT_LN1") != nullptr;
   const bool split_ln1 = !no_split_ln1 && precision == PREC_SPLIT && hidden >= 768 &&
                          hidden <= 1536;
+  // C = 48 / hidden = 192 (stage 1), opt-in (WF_FFN_FUSED=1): the whole FFN in one kernel
+  // (ffn_fused.hip), h1 and h2 stay on chip; stage 2 is that kernel, stages 1 and 3 are part
+  // of it.  Off by default: recomputing the 4 x 8 tile's haloed h1 plane (1.875x the pw GEMM,
+  // LN1 and GELU) costs more VALU time than the h1 round trip through HBM it saves
+  const bool whole = getenv("WF_FFN_FUSED") != nullptr;  // per call: tests switch it
+  if (!keep && whole && C == 48 && hidden == 192) {
+    if (stage == 1 || stage == 3) return 0;
+    DwFcArgs d{};
+    d.dw_w = dw_w;
+    d.dw_b = dw_b;
+    d.ln2_w = ln2_w;
+    d.ln2_b = ln2_b;
+    d.eps2 = eps2;
+    d.fc = fc_bf16x2;
+    d.fc_b = fc_b;
+    d.x = xh;
+    d.stats = stats;
+    d.n2_w = n2_w;
+    d.n2_b = n2_b;
+    d.bscale = branch_scale;
+    d.out = out;
+    d.B = (int)B;
+    d.D = (int)D;
+    d.H = (int)H;
+    d.W = (int)W;
+    d.pw = pw_bf16x2;
+    d.pw_b = pw_b;
+    d.ln1_w = ln1_w;
+    d.ln1_b = ln1_b;
+    d.eps1 = eps1;
+    return launch_ffn_fused(d, precision, s);
+  }
   if (stage == 0 || stage == 1) {
     if (split_ln1) {
       GemmArgs g2 = g;

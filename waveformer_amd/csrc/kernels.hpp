@@ -104,8 +104,18 @@ struct DwFcArgs {
   const float* bscale;   // (B) or NULL
   float* out;            // (B, D, H, W, C)
   int B, D, H, W, ZS;
+  // whole-FFN kernel (ffn_fused.hip) only: the front half, recomputed on chip from x
+  const uint16_t* pw;    // [2][HID][C] bf16 {hi, lo}
+  const float* pw_b;     // (HID) or NULL
+  const float* ln1_w;    // (HID)
+  const float* ln1_b;
+  float eps1;
+  int dbg;               // timing experiments only (WF_FFN_DBG): bit mask of phases skipped
 };
 int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s);
+// ---- the whole CCF_FFN + norm2 + Q4 residual in one kernel for C = 48, hidden = 192: the
+// haloed h1 plane is computed in LDS from the x rows (pw MFMA + LN1 + GELU), never stored
+int launch_ffn_fused(const DwFcArgs& a, int prec, hipStream_t s);
 // K-chunked MFMA GEMM (gemm_kc.hip) for the shapes whose weight does not fit gemm_rows' LDS
 // in one column chunk; returns 1 if it took the shape
 int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s);

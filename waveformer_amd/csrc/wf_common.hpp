@@ -59,24 +59,33 @@ __device__ __forceinline__ float gelu_erf(float x) {
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-// gelu_erf on a pair: the same arithmetic, the FMA-class steps as packed v_pk_*_f32 ops
-__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
-  const f32x2 u = f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752f;
-  const f32x2 d = u * 0.3275911f + 1.0f;
+// GELU on a pair given HALF its input, hx = x / 2:  GELU(x) = x Phi(x) = hx + |hx| erf(sqrt2 |hx|)
+// (no sign restore: x erf(x / sqrt2) = |x| erf(|x| / sqrt2)).  erf by Abramowitz & Stegun 7.1.26
+// as in gelu_erf, with the polynomial's coefficients negated so 1 - p e is one FMA, and the
+// sqrt2 folded into its constants; the FMA-class steps are packed v_pk_*_f32 ops.  A caller
+// whose input comes out of an affine step (LayerNorm) folds the 1/2 into that step for free.
+__device__ __forceinline__ f32x2 gelu_half2(f32x2 hx) {
+  const f32x2 a = f32x2{fabsf(hx.x), fabsf(hx.y)};
+  const f32x2 d = a * 0.46328425f + 1.0f;                  // 1 + p |x| / sqrt2
   const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  f32x2 p = t * 1.061405429f + -1.453152027f;
-  p = t * p + 1.421413741f;
-  p = t * p + -0.284496736f;
-  p = t * p + 0.254829592f;
+  f32x2 p = t * -1.061405429f + 1.453152027f;              // -(a1 t + ... + a5 t^5)
+  p = t * p + -1.421413741f;
+  p = t * p + 0.284496736f;
+  p = t * p + -0.254829592f;
   p = p * t;
-  const f32x2 q = (x * x) * -0.72134752044448170f;
+  const f32x2 q = (a * a) * -2.88539008177792681f;          // -(x^2 / 2) log2 e
   const f32x2 e = f32x2{__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
-  const f32x2 erfa = 1.0f - p * e;
-  const f32x2 hx = 0.5f * x;
-  return hx * f32x2{copysignf(erfa.x, x.x), copysignf(erfa.y, x.y)} + hx;
+  return a * (p * e + 1.0f) + hx;
 }
+// gelu_erf on a pair
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) { return gelu_half2(x * 0.5f); }
 
-// four / eight lanes' worth as packed pairs (bitwise equal to gelu_erf with FMA contraction)
+// four / eight lanes' worth as packed pairs
+__device__ __forceinline__ f32x4 gelu_half4(f32x4 h) {
+  const f32x2 a = gelu_half2(f32x2{h.x, h.y});
+  const f32x2 b = gelu_half2(f32x2{h.z, h.w});
+  return f32x4{a.x, a.y, b.x, b.y};
+}
 __device__ __forceinline__ f32x4 gelu_erf4(f32x4 v) {
   const f32x2 a = gelu_erf2(f32x2{v.x, v.y});
   const f32x2 b = gelu_erf2(f32x2{v.z, v.w});
