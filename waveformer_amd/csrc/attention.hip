@@ -20,6 +20,21 @@ namespace wf {
 
 constexpr int kQB = 64;  // queries per workgroup (16 per wave)
 
+// XCD-aware decode of the 1-D grid.  Workgroups are dealt round-robin over the 8 XCDs (linear
+// id L runs on XCD L % 8), so the query tiles of one (window, head) -- which all stage the same
+// K / V rows -- would land on 8 different XCDs and each XCD's L2 would fetch those rows again.
+// Logical id t = the L-th slot of XCD L % 8 in a contiguous split keeps consecutive t (the
+// query tiles of one (window, head)) on one XCD.
+__device__ __forceinline__ void attn_block(int gx, int heads, int& qb, int& h, int64_t& bw) {
+  const int64_t L = blockIdx.x, nb = gridDim.x;
+  const int64_t xcd = L & 7, q8 = nb >> 3, r8 = nb & 7;
+  int64_t t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+  qb = (int)(t % gx);
+  t /= gx;
+  h = (int)(t % heads);
+  bw = t / heads;
+}
+
 template <bool SPLIT>
 __device__ __forceinline__ void load8_split(const void* base, int64_t off, bf16x8& hi,
                                             bf16x8& lo) {
@@ -62,8 +77,9 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
   __shared__ __attribute__((aligned(16))) uint16_t Vt[NB][HD * VS];  // [hd][key]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int qb = blockIdx.x, h = blockIdx.y;
-  const int64_t bw = blockIdx.z;
+  int qb, h;
+  int64_t bw;
+  attn_block((N + kQB - 1) / kQB, heads, qb, h, bw);
   const int C = heads * HD;
   const int64_t row0 = bw * N;  // first token row of this window
   const int ld = 3 * C;
@@ -250,8 +266,9 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
   uint16_t* Vq = lds_attn + (size_t)NB * NP * KS;    // [NB][NP/4][HD][4]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int qb = blockIdx.x, h = blockIdx.y;
-  const int64_t bw = blockIdx.z;
+  int qb, h;
+  int64_t bw;
+  attn_block((N + kQB - 1) / kQB, heads, qb, h, bw);
   const int C = heads * HD;
   const int64_t row0 = bw * N;
   const int ld = 3 * C;
@@ -418,6 +435,156 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
   }
 }
 
+// Table-bias attention for the default window (ws 8: N = 512 tokens, head_dim 16), one
+// workgroup per (window, head) -- or per 1/2 or 1/4 of its queries when there are too few
+// windows to fill the chip.  K and V are split into bf16 hi / lo ONCE per (window, head) and
+// staged in LDS (76 KB: two workgroups per CU), instead of once per 64-query workgroup.  Every
+// product runs on v_mfma_f32_16x16x32_bf16:
+//   S^T = K Q^T : the K = 32 reduction packs [Kh | Kl] against [Qh | Qh] (Kh Qh + Kl Qh in one
+//                 MFMA), a second MFMA adds Kh Ql ([Kh | Kl] against [Ql | 0]);
+//   O^T = V^T P^T : 32 keys per MFMA, the B operand is the lane's two 4-key score quads of two
+//                 16-key sub-tiles as they come out of the S MFMAs (the K-slot order is matched
+//                 by reading V at the same keys), x3 for the split.
+// The bias index is the reference's formula (attention.py:40-56, Q2 depth stride 3 ws - 1)
+// with the key part reduced to per-tile constants: a 64-key tile is one z slice of the window.
+template <bool SPLIT>
+__global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict__ qkv,
+                                                          const float* __restrict__ table,
+                                                          void* __restrict__ out, int heads,
+                                                          int qsplit, float scale_log2) {
+  constexpr int N = 512, HD = 16;
+  constexpr int TBLN = 547;      // reachable rows of the (15^3, heads) table under Q2
+  constexpr int KS = 40;         // K row: hi[16] | lo[16] | pad (80 B: conflict-free b128)
+  constexpr int VQ = (N / 4) * HD * 4;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[N * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vq[2 * VQ];  // [hi, lo][key/4][hd][4 keys]
+  __shared__ float tb[TBLN];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int qs, h;
+  int64_t bw;
+  attn_block(qsplit, heads, qs, h, bw);
+  const int C = heads * HD, ld = 3 * C;
+  const int64_t row0 = bw * N;
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  for (int i = tid; i < TBLN; i += 512) tb[i] = table[(int64_t)i * heads + h] * 1.4426950408889634f;
+  for (int it = tid; it < N * 2; it += 512) {  // K: (key, 8-value chunk)
+    const int key = it >> 1, ch = it & 1;
+    bf16x8 hi = z8, lo = z8;
+    load8_split<SPLIT>(qkv, (row0 + key) * ld + C + h * HD + ch * 8, hi, lo);
+    *reinterpret_cast<bf16x8*>(&Ks[key * KS + ch * 8]) = hi;
+    *reinterpret_cast<bf16x8*>(&Ks[key * KS + 16 + ch * 8]) = SPLIT ? lo : z8;
+  }
+  for (int it = tid; it < (N / 4) * 2; it += 512) {  // V: (key quad, 8-value chunk)
+    const int k4 = it >> 1, ch = it & 1;
+    bf16x8 vh[4], vl[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      vh[r] = z8;
+      vl[r] = z8;
+      load8_split<SPLIT>(qkv, (row0 + 4 * k4 + r) * ld + 2 * C + h * HD + ch * 8, vh[r], vl[r]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = ((k4 * HD) + ch * 8 + j) * 4;
+      *reinterpret_cast<bf16x4*>(&Vq[o]) = bf16x4{vh[0][j], vh[1][j], vh[2][j], vh[3][j]};
+      if (SPLIT) *reinterpret_cast<bf16x4*>(&Vq[VQ + o]) = bf16x4{vl[0][j], vl[1][j], vl[2][j], vl[3][j]};
+    }
+  }
+  __syncthreads();
+
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const int nsub = N / 16 / qsplit;  // 16-query sub-tiles of this workgroup
+  for (int st = wid; st < nsub; st += 8) {
+    const int q = qs * (N / qsplit) + st * 16 + l15;
+    // B operands of S: slots 8 g4 .. +7 <- Q[q][8 (g4 & 1) ..]: [Qh | Qh] and [Ql | 0]
+    bf16x8 b1 = z8, b2 = z8;
+    {
+      bf16x8 hi = z8, lo = z8;
+      load8_split<SPLIT>(qkv, (row0 + q) * ld + h * HD + 8 * (g4 & 1), hi, lo);
+      b1 = hi;
+      b2 = (SPLIT && g4 < 2) ? lo : z8;
+    }
+    const int qz = q >> 6, qy = (q >> 3) & 7, qx = q & 7;
+    const int ib = (qz + 7) * 23 + (qy + 7) * 15 + (qx + 7) - ((g4 >> 1) * 15 + 4 * (g4 & 1));
+    f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+    float mrun = -INFINITY, lrun = 0.f;
+#pragma unroll 2
+    for (int t = 0; t < 8; ++t) {  // 64-key tiles (one z slice of the window each)
+      f32x4 s[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ks[(t * 64 + kt * 16 + l15) * KS + 8 * g4]);
+        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        if (SPLIT) s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b2, s[kt], 0, 0, 0);
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const int i0 = ib - t * 23 - kt * 30;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s[kt][i] = s[kt][i] * scale_log2 + tb[i0 - i];
+          tmax = fmaxf(tmax, s[kt][i]);
+        }
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(mrun, tmax);
+      const float alpha = exp2f(mrun - mnew);
+      mrun = mnew;
+      float psum = 0.f;
+      bf16x4 ph[4], pl[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(s[kt][i] - mnew);
+          psum += p;
+          const uint16_t hb = f2bf(p);
+          ph[kt][i] = (short)hb;
+          pl[kt][i] = SPLIT ? (short)f2bf(p - bf2f(hb)) : (short)0;
+        }
+      }
+      lrun = lrun * alpha + psum;
+      o *= alpha;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 pb = bf16x8{ph[2 * j][0], ph[2 * j][1], ph[2 * j][2], ph[2 * j][3],
+                                 ph[2 * j + 1][0], ph[2 * j + 1][1], ph[2 * j + 1][2], ph[2 * j + 1][3]};
+        const int o1 = (((16 * t + 8 * j + g4) * HD) + l15) * 4;
+        const int o2 = (((16 * t + 8 * j + 4 + g4) * HD) + l15) * 4;
+        const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(&Vq[o1]);
+        const bf16x4 v2 = *reinterpret_cast<const bf16x4*>(&Vq[o2]);
+        const bf16x8 vh = bf16x8{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+        if (SPLIT) {
+          const bf16x8 plb = bf16x8{pl[2 * j][0], pl[2 * j][1], pl[2 * j][2], pl[2 * j][3],
+                                    pl[2 * j + 1][0], pl[2 * j + 1][1], pl[2 * j + 1][2],
+                                    pl[2 * j + 1][3]};
+          const bf16x4 w1 = *reinterpret_cast<const bf16x4*>(&Vq[VQ + o1]);
+          const bf16x4 w2 = *reinterpret_cast<const bf16x4*>(&Vq[VQ + o2]);
+          const bf16x8 vl = bf16x8{w1[0], w1[1], w1[2], w1[3], w2[0], w2[1], w2[2], w2[3]};
+          o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, pb, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, plb, o, 0, 0, 0);
+        }
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, pb, o, 0, 0, 0);
+      }
+    }
+    lrun += __shfl_xor(lrun, 16, 64);
+    lrun += __shfl_xor(lrun, 32, 64);
+    const float inv = 1.f / lrun;
+    const int64_t off = (row0 + q) * C + h * HD + 4 * g4;
+    if (SPLIT) {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off) = o * inv;
+    } else {
+      bf16x4 r;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = (short)f2bf(o[i] * inv);
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(out) + off) = r;
+    }
+  }
+}
+
 static size_t attn_win_lds(int N, int hd, bool split) {
   const size_t NP = (size_t)(N + 63) / 64 * 64;
   return (split ? 2 : 1) * (NP * (hd + 4) + NP * hd) * sizeof(uint16_t);
@@ -427,13 +594,29 @@ int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, 
                      int N, int heads, int hd, float scale, int prec, hipStream_t s,
                      int table_ws) {
   if (Bw <= 0) return WF_OK;
-  if (Bw > 65535) return fail(WF_E_SHAPE, "attention: more than 65535 windows per call");
-  dim3 grid((unsigned)cdiv(N, kQB), (unsigned)heads, (unsigned)Bw);
+  const int64_t nblk = cdiv(N, kQB) * heads * Bw;
+  if (nblk > 0x7fffffff) return fail(WF_E_SHAPE, "attention: too many (window, head) tiles");
+  dim3 grid((unsigned)nblk);  // 1-D, decoded XCD-aware by attn_block
   const float sl2 = scale * 1.4426950408889634f;
   const bool split = prec == PREC_SPLIT;
   if (table_ws) {  // bias = the (T, heads) table; index from the coordinates
     if (table_ws != 8 || hd != 16 || N != 512)
       return fail(WF_E_SHAPE, "attention (table bias): implemented for ws = 8, head_dim = 16");
+    static const bool tiled = getenv("WF_ATTN_TILED") != nullptr;  // the r1 kernel, for A/B
+    if (!lse && !tiled) {
+      // queries of one (window, head) split over 1, 2 or 4 workgroups: enough workgroups for
+      // two per CU, each staging the window's K / V once
+      const int64_t wh = Bw * heads;
+      const int qsplit = wh >= 512 ? 1 : (wh >= 256 ? 2 : 4);
+      const dim3 g1((unsigned)(wh * qsplit));
+      if (split)
+        hipLaunchKernelGGL(attn_tbl_kernel<true>, g1, dim3(512), 0, s, qkv, bias, out, heads,
+                           qsplit, sl2);
+      else
+        hipLaunchKernelGGL(attn_tbl_kernel<false>, g1, dim3(512), 0, s, qkv, bias, out, heads,
+                           qsplit, sl2);
+      return check_launch("attention core (table bias, window per workgroup)");
+    }
     if (split)
       hipLaunchKernelGGL((attn_core_kernel<16, 64, true, 8>), grid, dim3(256), 0, s, qkv, bias,
                          out, lse, N, heads, sl2);

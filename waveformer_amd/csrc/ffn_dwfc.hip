@@ -49,7 +49,7 @@ struct DwFcCfg {
   static_assert(NPOS * LN_LANES <= NTH, "LN2 lanes");
   static_assert(LN_CH % 4 == 0, "LN2 vector width");
   static constexpr size_t LDS_BYTES = (size_t)BUF_F * 4 + (size_t)2 * C * WKP * 2 +
-                                      (size_t)(2 * HID + C) * 4;
+                                      (size_t)(2 * HID + 3 * C) * 4;
 };
 
 template <typename T>
@@ -85,6 +85,8 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
   float* lnw = reinterpret_cast<float*>(wf + 2 * C * K::WKP);     // [HID]
   float* lnb = lnw + HID;                                         // [HID]
   float* fcb = lnb + HID;                                         // [C]
+  float* n2w = fcb + C;                                           // [C] norm2 (1, 0 if none)
+  float* n2b = n2w + C;
 
   const int tid = threadIdx.x;
   const int wid = tid >> 6;
@@ -114,18 +116,24 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
                          : z8;
     *reinterpret_cast<bf16x8*>(wf + ((size_t)pl * C + n) * K::WKP + 8 * k8) = v;
   }
-  for (int i = tid; i < HID; i += K::NTH) {
-    lnw[i] = a.ln2_w[i];
-    lnb[i] = a.ln2_b[i];
+  for (int i = tid; i < HID; i += K::NTH) {  // halved: GELU is evaluated from x / 2
+    lnw[i] = 0.5f * a.ln2_w[i];
+    lnb[i] = 0.5f * a.ln2_b[i];
   }
-  for (int i = tid; i < C; i += K::NTH) fcb[i] = a.fc_b ? a.fc_b[i] : 0.f;
+  // depthwise weights, coalesced into the (not yet used) plane buffer, read back per thread
+  for (int i = tid; i < HID * 27; i += K::NTH) planes[i] = a.dw_w[i];
+  __syncthreads();
+  for (int i = tid; i < C; i += K::NTH) {
+    fcb[i] = a.fc_b ? a.fc_b[i] : 0.f;
+    n2w[i] = a.stats ? a.n2_w[i] : 1.f;
+    n2b[i] = a.stats ? a.n2_b[i] : 0.f;
+  }
 
   // ---- depthwise role: channel pair cp, column xi
   const int cp = tid % (HID / 2), xi = tid / (HID / 2);
   f32x2 w2[27];
 #pragma unroll
-  for (int k = 0; k < 27; ++k)
-    w2[k] = f32x2{a.dw_w[(2 * cp) * 27 + k], a.dw_w[(2 * cp + 1) * 27 + k]};
+  for (int k = 0; k < 27; ++k) w2[k] = f32x2{planes[(2 * cp) * 27 + k], planes[(2 * cp + 1) * 27 + k]};
   const f32x2 bias2 = f32x2{a.dw_b[2 * cp], a.dw_b[2 * cp + 1]};
 
   // ---- h1 plane staging: item i -> (haloed position i / NV, 4-channel vector i % NV).  The
@@ -164,16 +172,39 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
     }
   };
 
+  const int64_t plane_sz = (int64_t)H * W;
+  // Epilogue inputs (x rows + norm2 stats of the fc lane's output row), issued right after the
+  // commit (whose wait they do not extend) and before the next plane's fetch (which the fc's
+  // wait for them therefore does not include); the LN2 phase runs while they are in flight.
+  // Every load is unconditional -- a branch join on a load in flight makes the compiler wait
+  // on the spot -- so without norm2 stats the stats pointer reads x and the values are
+  // discarded.
+  const float* sbase = a.stats ? a.stats : a.x;
+  f32x4 xr = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x2 es = f32x2{0.f, 1.f};
+  auto epi_fetch = [&](int zp) {
+    int ltid = tid;
+    asm volatile("" : "+v"(ltid));
+    const int lwid = min(ltid >> 6, K::RT * K::CT - 1);  // waves without an fc tile load tile 5
+    const int lp = (lwid / K::CT) * 16 + (ltid & 15);
+    const int col = (lwid % K::CT) * 16 + 4 * ((ltid >> 4) & 3);
+    const int yo = min(y0 + lp / TX, H - 1), xo = min(x0 + lp % TX, W - 1);
+    const int64_t gpos = (int64_t)b * D * plane_sz + (int64_t)zp * plane_sz + yo * W + xo;
+    xr = *reinterpret_cast<const f32x4*>(a.x + gpos * C + col);
+    es = *reinterpret_cast<const f32x2*>(sbase + 2 * gpos);
+  };
+  const float bs = a.bscale ? a.bscale[b] : 1.f;  // DropPath factor of this sample
+
   f32x2 accA[TY], accB[TY], accC[TY];
 #pragma unroll
   for (int o = 0; o < TY; ++o) accA[o] = accB[o] = accC[o] = f32x2{0.f, 0.f};
 
-  const int64_t plane_sz = (int64_t)H * W;
-
   // Schedule per input plane p (3 barriers): scatter(p) | C | commit(p+1) into the other plane
-  // buffer, fetch(p+2), h2 tile of output p-1 | A | LN2 + GELU in place | B | fc + store.
-  // Waves without an fc tile run ahead into the next plane's scatter while the fc runs.
+  // buffer, the epilogue rows of output p and the h1 plane p+2 fetched for later, h2 tile of
+  // output p-1 | A | LN2 + GELU in place | B | fc + store.  Waves without an fc tile run ahead
+  // into the next plane's scatter while the fc runs.
   fetch(z0 - 1);
+  __syncthreads();  // the depthwise weights are read out of the plane buffer
   commit(z0 - 1, planes);
   fetch(z0);
   __syncthreads();
@@ -204,7 +235,14 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
 
     const int zo = p - 1;  // output plane completed by this input plane
     __syncthreads();  // C: scatter(p) done everywhere (nxt is free), fc(p-2) done (h2t is free)
+    // retire the loads issued a plane ago on every path (an empty asm "reading" them): where
+    // the commit or the fc is skipped their registers would otherwise stay pending, and the
+    // compiler would then drain the loads issued just below before re-using the registers
+    asm volatile("" ::"v"(xr), "v"(es));
+#pragma unroll
+    for (int j = 0; j < K::NLD; ++j) asm volatile("" ::"v"(stg[j]));
     if (p + 1 <= z1) commit(p + 1, nxt);
+    if (zo >= z0) epi_fetch(zo);
     if (p + 2 <= z1) fetch(p + 2);  // in flight behind the next plane's work
     if (zo >= z0) {
       // ---- h2 tile (+ bias) into LDS: row = position o * TX + xi
@@ -223,8 +261,7 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
       // ---- LN2 + GELU per position, rewritten in place as bf16 {hi[HID], lo[HID]}
       // Loop-invariant per-lane values of the LN2 and epilogue phases are recomputed from a
       // laundered thread index every plane: hoisted out of the z loop they exceed the
-      // 168-VGPR budget and spill, and each scratch reload's vmcnt(0) would also wait out the
-      // in-flight fetch(p + 2), exposing its HBM latency once per plane.
+      // 168-VGPR budget and spill.
       int ltid = tid;
       asm volatile("" : "+v"(ltid));
       if (ltid < K::NPOS * K::LN_LANES) {
@@ -239,10 +276,10 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
           v[4 * j + 2] = u.z;
           v[4 * j + 3] = u.w;
         }
-        float s = 0.f;
+        float sm = 0.f;
 #pragma unroll
-        for (int j = 0; j < K::LN_CH; ++j) s += v[j];
-        const float mean = group_sum<K::LN_LANES>(s) * (1.f / HID);
+        for (int j = 0; j < K::LN_CH; ++j) sm += v[j];
+        const float mean = group_sum<K::LN_LANES>(sm) * (1.f / HID);
         float q = 0.f;
 #pragma unroll
         for (int j = 0; j < K::LN_CH; ++j) {
@@ -250,17 +287,15 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
           q += d * d;
         }
         const float rstd = rsqrtf(group_sum<K::LN_LANES>(q) * (1.f / HID) + a.eps2);
+        const float nmr = -mean * rstd;
         uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
 #pragma unroll
         for (int j = 0; j < K::LN_CH / 4; ++j) {
           const int c = g * K::LN_CH + 4 * j;
           const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + c);
           const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + c);
-          const f32x2 y0 = gelu_erf2((f32x2{v[4 * j], v[4 * j + 1]} - mean) * rstd *
-                                         f32x2{lw4.x, lw4.y} + f32x2{lb4.x, lb4.y});
-          const f32x2 y1 = gelu_erf2((f32x2{v[4 * j + 2], v[4 * j + 3]} - mean) * rstd *
-                                         f32x2{lw4.z, lw4.w} + f32x2{lb4.z, lb4.w});
-          const float y[4] = {y0.x, y0.y, y1.x, y1.y};
+          const f32x4 y = gelu_half4((f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]} *
+                                      rstd + nmr) * lw4 + lb4);
           bf16x4 hi4, lo4;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -272,7 +307,6 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
           if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + c) = lo4;
         }
       }
-      // residual inputs of this lane's epilogue row, in flight during the barrier + GEMM
       const int lln = ltid & 63, lwid = ltid >> 6;
       const int ct = lwid % K::CT, l15 = lln & 15, g4 = lln >> 4;  // fc tile of this wave
       const int lp = (lwid / K::CT) * 16 + l15;  // tile position of this lane's row
@@ -282,46 +316,36 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
                            (int64_t)min(yo, H - 1) * W + min(xo, W - 1);
       const int col = ct * 16 + 4 * g4;
       const bool fcw = wid < K::RT * K::CT;  // this wave owns an fc tile
-      f32x4 xr = f32x4{0.f, 0.f, 0.f, 0.f};
-      float smu = 0.f, srs = 1.f;
-      if (fcw) {
-        xr = *reinterpret_cast<const f32x4*>(a.x + gpos * C + col);
-        if (a.stats) {
-          smu = a.stats[2 * gpos];
-          srs = a.stats[2 * gpos + 1];
-        }
-      }
       __syncthreads();  // B: LN2 + GELU rows visible
       // ---- fc GEMM (waves 0 .. RT*CT-1): acc[i] = ffn[position lp][channel col + i]
       if (fcw) {
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)lp * (2 * K::HS);
-      const uint16_t* Wh = wf + (size_t)(ct * 16 + l15) * K::WKP;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)lp * (2 * K::HS);
+        const uint16_t* Wh = wf + (size_t)(ct * 16 + l15) * K::WKP;
 #pragma unroll
-      for (int ks = 0; ks < HID / 32; ++ks) {
-        const int k = ks * 32 + 8 * g4;
-        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bh + k);
-        const bf16x8 wh = *reinterpret_cast<const bf16x8*>(Wh + k);
-        if (SPLIT) {
-          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
-          const bf16x8 wl = *reinterpret_cast<const bf16x8*>(Wh + C * K::WKP + k);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bl, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, bh, acc, 0, 0, 0);
+        for (int ks = 0; ks < HID / 32; ++ks) {
+          const int k = ks * 32 + 8 * g4;
+          const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bh + k);
+          const bf16x8 wh = *reinterpret_cast<const bf16x8*>(Wh + k);
+          if (SPLIT) {
+            const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
+            const bf16x8 wl = *reinterpret_cast<const bf16x8*>(Wh + C * K::WKP + k);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bl, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, bh, acc, 0, 0, 0);
+          }
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bh, acc, 0, 0, 0);
         }
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bh, acc, 0, 0, 0);
-      }
-      // ---- epilogue: bias + Q4 residual, 16-byte store
-      f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
-      const float bs = a.bscale ? a.bscale[b] : 1.f;
-      if (a.stats) {
-        const f32x4 lw = *reinterpret_cast<const f32x4*>(a.n2_w + col);
-        const f32x4 lb = *reinterpret_cast<const f32x4*>(a.n2_b + col);
-        const f32x4 n2 = (xr - smu) * srs * lw + lb;
-        v = xr + (n2 + v) * bs;
-      } else {
-        v = xr + v * bs;
-      }
-      if (rv) *reinterpret_cast<f32x4*>(a.out + gpos * C + col) = v;
+        // ---- epilogue: bias + Q4 residual, 16-byte store
+        f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+        if (a.stats) {
+          const f32x4 lw = *reinterpret_cast<const f32x4*>(n2w + col);
+          const f32x4 lb = *reinterpret_cast<const f32x4*>(n2b + col);
+          const f32x4 n2 = (xr - es.x) * es.y * lw + lb;
+          v = xr + (n2 + v) * bs;
+        } else {
+          v = xr + v * bs;
+        }
+        if (rv) *reinterpret_cast<f32x4*>(a.out + gpos * C + col) = v;
       }
     }
 #pragma unroll
