@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 7
+#define WF_ABI_VERSION 8
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1 };
 
@@ -59,6 +59,13 @@ int wf_cast_f32_to_bf16(const float* in, uint16_t* out, int64_t n, void* stream)
 
 /* out[i] = hi = bf16(in[i]), out[n + i] = bf16(in[i] - hi): the [2][...] weight planes. */
 int wf_split_f32_to_bf16x2(const float* in, uint16_t* out, int64_t n, void* stream);
+
+/* wf_split_f32_to_bf16x2 of n weights in one launch (the per-forward weight arena of
+ * waveformer_amd.ops.weight_scope).  table_dev (device memory, int64): [n + 1] prefix sums of
+ * the element counts, then the n fp32 source pointers, then the n destination pointers
+ * ([2][numel] bf16 each); total = table[n].                                                */
+int wf_split_f32_to_bf16x2_multi(const int64_t* table_dev, int64_t n, int64_t total,
+                                 void* stream);
 
 /* ---- a10: PatchEmbed -------------------------------------------------------------- */
 /* Replaces monai PatchEmbed.proj = Conv3d(Cin, Cout, k=2, s=2) as called at

@@ -27,6 +27,7 @@ SIGNATURES = {
     "wf_last_error": (ctypes.c_char_p, []),
     "wf_cast_f32_to_bf16": (_I, [_P, _P, _I64, _P]),
     "wf_split_f32_to_bf16x2": (_I, [_P, _P, _I64, _P]),
+    "wf_split_f32_to_bf16x2_multi": (_I, [_P, _I64, _I64, _P]),
     "wf_patch_embed_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwt3d_haar_fwd": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
@@ -90,7 +91,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _lock = threading.Lock()
 _lib = None
 _err = None

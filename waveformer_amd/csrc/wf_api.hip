@@ -40,9 +40,43 @@ __global__ void split_f32_bf16x2_kernel(const float* __restrict__ in, uint16_t* 
   }
 }
 
+// Many weights in one launch: table = [n + 1] int64 element offsets (prefix sums), then n
+// source pointers, then n destination pointers, all in device memory.  Destination d of
+// weight s holds its [2][numel] {hi, lo} planes, as wf_split_f32_to_bf16x2 writes them.
+__global__ void split_multi_kernel(const int64_t* __restrict__ table, int n, int64_t total) {
+  const int64_t* pre = table;
+  const float* const* src = reinterpret_cast<const float* const*>(table + n + 1);
+  uint16_t* const* dst = reinterpret_cast<uint16_t* const*>(table + 2 * n + 1);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    int lo = 0, hi = n - 1;  // last segment with pre[s] <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int64_t j = i - pre[lo], m = pre[lo + 1] - pre[lo];
+    const float v = src[lo][j];
+    const uint16_t h = f2bf(v);
+    dst[lo][j] = h;
+    dst[lo][m + j] = f2bf(v - bf2f(h));
+  }
+}
+
 }  // namespace wf
 
 extern "C" int wf_abi_version(void) { return WF_ABI_VERSION; }
+
+extern "C" int wf_split_f32_to_bf16x2_multi(const int64_t* table_dev, int64_t n, int64_t total,
+                                            void* stream) {
+  WF_REQUIRE(n >= 0 && total >= 0, "negative count");
+  if (n == 0 || total == 0) return WF_OK;
+  WF_REQUIRE_PTR(table_dev);
+  int64_t blocks = wf::cdiv(total, 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(wf::split_multi_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     (hipStream_t)stream, table_dev, (int)n, total);
+  return wf::check_launch("wf_split_f32_to_bf16x2_multi");
+}
 
 extern "C" const char* wf_last_error(void) { return wf::g_last_error.c_str(); }
 

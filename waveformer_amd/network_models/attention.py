@@ -1,8 +1,8 @@
 """Window multi-head self-attention with a 3D relative-position bias.
 
 Mirrors network_models/attention.py (class Attention, :15-129): same constructor, parameters,
-buffers and state_dict keys.  The forward runs on the waveformer_amd HIP kernels
-(wf_window_attention_fwd): qkv GEMM -> flash-style QK^T + bias / softmax / PV core -> proj.
+buffers and state_dict keys.  The forward is the waveformer::window_attn op (library.py) on the HIP kernels:
+qkv GEMM -> flash-style QK^T + bias / softmax / PV core -> proj.
 """
 from __future__ import annotations
 
@@ -13,7 +13,10 @@ import torch
 import torch.nn as nn
 
 from .. import autograd as wfa
+from .. import library  # noqa: F401  (registers the torch.ops.waveformer ops)
 from .. import ops
+
+_OPS = torch.ops.waveformer
 
 
 def relative_position_index(ws: int) -> torch.Tensor:
@@ -46,47 +49,32 @@ class Attention(nn.Module):
         self.register_buffer("relative_position_index", relative_position_index(window_size))
         nn.init.trunc_normal_(self.relative_position_bias_table, std=.02)
         self.softmax = nn.Softmax(dim=-1)
-        self._bias_key = None
-        self._bias = None
-
-    # ---- dense (heads, N, N) bias, rebuilt only when the table / index change
-    def dense_bias(self) -> torch.Tensor:
-        t, i = self.relative_position_bias_table, self.relative_position_index
-        key = (t.data_ptr(), t._version, i.data_ptr(), i._version, t.device)
-        if self._bias is None or self._bias_key != key:
-            self._bias = ops.rel_pos_bias(t.detach(), i)
-            self._bias_key = key
-        return self._bias
 
     def _check_train(self):
         if self.training and (self.attn_drop.p > 0 or self.proj_drop.p > 0):
             raise NotImplementedError("waveformer_amd: attention dropout > 0 is not supported")
+
+    def _wf_split_params(self):
+        return [self.qkv.weight, self.proj.weight]
 
     def forward_raster(self, x_cl: torch.Tensor,
                        ln: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None) -> torch.Tensor:
         """Attention over the ws^3 windows of a channel-last raster (B, D, H, W, C): the
         window_partition + forward + plain-reshape "reverse" of Block (wave_helper.py:491-499,
         quirk Q1).  Row r of the result (as a (B*D*H*W, C) matrix) is token r % N of window
-        r // N; viewed as (B, D, H, W, C) it is exactly the reference's attn_windows."""
+        r // N; viewed as (B, D, H, W, C) it is exactly the reference's attn_windows.  One
+        waveformer::window_attn op: it reads the bias table itself (ws 8, head_dim 16, the
+        index buffer equal to the reference's formula) or its dense expansion."""
         self._check_train()
-        if wfa.needs_grad(x_cl, *self.parameters(), *(ln[:2] if ln is not None else ())):
-            return wfa.window_attention(self, x_cl, ln)
-        bias = self.relative_position_bias_table.detach() if self._table_ok() else self.dense_bias()
-        return ops.window_attention(
-            x_cl, self.qkv.weight, self.qkv.bias, bias, self.proj.weight,
-            self.proj.bias, self.window_size, self.num_heads, self.scale, ln)
-
-    def _table_ok(self) -> bool:
-        """The table-bias kernel (ws 8, head_dim 16) computes the index from the reference's
-        formula; use it only while the relative_position_index buffer still equals it."""
-        if self.window_size != 8 or self.head_dim != 16:
-            return False
-        i = self.relative_position_index
-        key = (i.data_ptr(), i._version, i.device)
-        if getattr(self, "_tbl_key", None) != key:
-            self._tbl_ok = bool(torch.equal(i, relative_position_index(8).to(i.device)))
-            self._tbl_key = key
-        return self._tbl_ok
+        lw, lb, eps = ln if ln is not None else (None, None, 0.0)
+        train = wfa.needs_grad(x_cl, *self.parameters(), lw, lb)
+        prec = wfa.SPLIT if train else ops.prec_id()
+        out, _, _ = _OPS.window_attn(x_cl, lw, lb, float(eps), self.qkv.weight, self.qkv.bias,
+                                     self.relative_position_bias_table,
+                                     self.relative_position_index, self.proj.weight,
+                                     self.proj.bias, self.window_size, self.num_heads,
+                                     float(self.scale), prec, train)
+        return out
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x: (B_, N, C) token batches, N = window_size^3 (attention.py:83-104)."""

@@ -15,6 +15,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 from functools import partial
 
+from .. import ops
+
 from ..blocks import UnetOutBlock, UnetrBasicBlock, UnetrUpBlock
 from .idwt_upsample import UnetrIDWTBlock
 from .wave_helper import ProjectionUpsample
@@ -141,7 +143,12 @@ class Waveformer(nn.Module):
         return layers[norm_name]
 
     def forward(self, x_in: torch.Tensor) -> torch.Tensor:
-        """network_backbone.py:380-407."""
+        """network_backbone.py:380-407.  One weight_scope per forward: the split / packed
+        forms of the weights are rebuilt once at its start (ops.weight_scope)."""
+        with ops.weight_scope(self):
+            return self._forward(x_in)
+
+    def _forward(self, x_in: torch.Tensor) -> torch.Tensor:
         outs, outs_hf = self.waveformer_encoder(x_in)
         enc0 = self.encoder1(x_in)
         enc1 = self.encoder2(outs[0])

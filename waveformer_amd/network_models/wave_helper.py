@@ -16,8 +16,11 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import autograd as wfa
+from .. import library  # noqa: F401  (registers the torch.ops.waveformer ops)
 from .. import ops
 from .attention import Attention
+
+_OPS = torch.ops.waveformer
 
 
 def _conv_fan_out_init(m: nn.Module) -> None:
@@ -87,6 +90,10 @@ class ProjectionUpsample(nn.Module):
                 nn.Upsample(scale_factor=stride, mode='trilinear', align_corners=True),
                 nn.Conv3d(in_channels, out_channels, kernel_size=1))
         self.act = nn.GELU()
+
+    def _wf_split_params(self):
+        c3 = self.conv3
+        return [c3[0].weight, c3[2].weight] if self.use_double_conv else [c3.weight]
 
     def _fast(self, x) -> bool:
         dw = self.conv1[1]
@@ -198,9 +205,12 @@ class PatchMergingV2(nn.Module):
         if d % 2 or h % 2 or w % 2:  # F.pad branch of the reference (never hit by WaveFormer)
             x = F.pad(x, (0, 0, 0, w % 2, 0, h % 2, 0, d % 2))
         x = x.contiguous()
-        if wfa.needs_grad(x, *self.parameters()):
-            return wfa.patch_merging(x, self.norm, self.reduction, self._v2)
-        return ops.patch_merging(x, self.norm, self.reduction, v2=self._v2)
+        prec = wfa.prec_for(x, *self.parameters())
+        return _OPS.patch_merging(x, self.norm.weight, self.norm.bias, float(self.norm.eps),
+                                  self.reduction.weight, self._v2, prec)
+
+    def _wf_split_params(self):
+        return [self.reduction.weight]
 
 
 class PatchMerging(PatchMergingV2):
@@ -241,14 +251,30 @@ class CCF_FFN(nn.Module):
         B, D, H, W, C = x.shape
         assert D * H * W == self.D * self.H * self.W
         x = x.contiguous()
-        if wfa.needs_grad(x, *self.parameters()):
-            return wfa.ccf_ffn(x, None, None, self)
-        return ops.ccf_ffn(x, None, None, self)
+        return ffn_op(x, None, None, self, None)
+
+    def _wf_split_params(self):
+        return [self.pwconv.weight, self.fc.weight]
 
     def flops(self):
         n = self.D * self.H * self.W
         c, h = self.fc.out_features, self.C_hid
         return n * (2 * c * h + 54 * h + 2 * h * c)
+
+
+def ffn_op(xh, stats, norm2, mlp: CCF_FFN, s_mlp):
+    """waveformer::ccf_ffn over a Block's norm2 (stats given) or a bare CCF_FFN (stats None)."""
+    n2w = n2b = None
+    n2eps = 0.0
+    if stats is not None:
+        n2w, n2b, n2eps = norm2.weight, norm2.bias, float(norm2.eps)
+    train = wfa.needs_grad(xh, *mlp.parameters(), n2w, n2b)
+    prec = wfa.SPLIT if train else ops.prec_id()
+    out, _ = _OPS.ccf_ffn(xh, stats, n2w, n2b, mlp.pwconv.weight, mlp.pwconv.bias,
+                          mlp.norm1.weight, mlp.norm1.bias, mlp.dwconv.weight, mlp.dwconv.bias,
+                          mlp.norm2.weight, mlp.norm2.bias, mlp.fc.weight, mlp.fc.bias, s_mlp,
+                          n2eps, float(mlp.norm1.eps), float(mlp.norm2.eps), prec, train)
+    return out
 
 
 class Mlp(nn.Module):
@@ -307,17 +333,14 @@ class WaveletTransform3D(nn.Module):
                     f"waveformer_amd: backward through wavelet {self.wavelet!r} not implemented")
             co = ops.wavedec3(x, self.wavelet, level)
             return co[0], co[1:]
-        if wfa.needs_grad(x):
-            self._check()
-            cur = x.permute(0, 2, 3, 4, 1).contiguous()
-            yh = []
-            for _ in range(level):
-                cur, det = wfa.dwt3d_haar(cur)
-                yh.append(det)
-            return cur.permute(0, 4, 1, 2, 3), list(reversed(yh))
-        ll, bands = self.decompose_cl(x.permute(0, 2, 3, 4, 1).contiguous(), level)
-        yh = [ops.bands_to_coeffs(b)[1] for b in reversed(bands)]
-        return ll.permute(0, 4, 1, 2, 3), yh
+        self._check()
+        cur = x.permute(0, 2, 3, 4, 1).contiguous()
+        yh = []
+        for _ in range(level):
+            bands = _OPS.dwt3d(cur, None, None, 0.0)
+            cur = bands[0]
+            yh.append(ops.bands_to_coeffs(bands)[1])
+        return cur.permute(0, 4, 1, 2, 3), list(reversed(yh))
 
 
 class Block(nn.Module):
@@ -383,50 +406,35 @@ class Block(nn.Module):
             return self.multi_scale_forward(x)
         return self.single_scale_forward(x)
 
+    def _levels(self, x, ln1, n):
+        """n one-level Haar DWTs (norm1 fused into the first): [band buffers], fine -> coarse."""
+        bands, cur = [], x
+        for i in range(n):
+            b = _OPS.dwt3d(cur, ln1[0] if i == 0 else None, ln1[1] if i == 0 else None,
+                           float(ln1[2]) if i == 0 else 0.0)
+            bands.append(b)
+            cur = b[0]
+        return bands
+
     def multi_scale_forward(self, x):
         """wave_helper.py:470-512.  norm1 is fused into the first DWT (or, at level 0, into
         the qkv loader); the interpolations, their sum, the shortcut and norm2's statistics
         are one msfuse kernel; norm2 + CCF_FFN + the double residual (Q4) are the FFN
-        kernels' loader/epilogues."""
+        kernels' loader/epilogues.  Inference and training run the same torch.ops.waveformer
+        ops (their autograd is the HIP backward)."""
         x = self._prep(x)
         s_attn, s_mlp = self._branch_scales(x.shape[0], x.device)
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
-        if wfa.needs_grad(x, *self.parameters()):
-            return self._multi_scale_train(x, ln1, s_attn, s_mlp)
+        hfs = None
         if self.level > 0:
             self.dwt_downsamples._check()
-            srcs, hfs = [], []
-            cur = x
-            for i in range(self.attn_computation_level):
-                b = ops.dwt3d_haar(cur, ln1 if i == 0 else None)
-                cur = b[0]
-                srcs.append(self.attn.forward_raster(cur))
-                hfs.append(ops.bands_to_coeffs(b)[1])
+            bands = self._levels(x, ln1, self.attn_computation_level)
+            srcs = [self.attn.forward_raster(b[0]) for b in bands]
+            hfs = [ops.bands_to_coeffs(b)[1] for b in bands]
         else:
             srcs = [self.attn.forward_raster(x, ln1)]
-            hfs = None
-        xh, stats = ops.msfuse(srcs, x, self.norm2.eps, s_attn)
-        out = ops.ccf_ffn(xh, stats, self.norm2, self.mlp, s_mlp)
-        if self.level > 0:
-            return out, tuple(reversed(hfs))
-        return out
-
-    def _multi_scale_train(self, x, ln1, s_attn, s_mlp):
-        """multi_scale_forward under autograd: the same dataflow through the differentiable
-        Functions of waveformer_amd.autograd (HIP forward + backward kernels)."""
-        if self.level > 0:
-            self.dwt_downsamples._check()
-            srcs, hfs = [], []
-            cur = x
-            for i in range(self.attn_computation_level):
-                cur, det = wfa.dwt3d_haar(cur, ln1 if i == 0 else None)
-                srcs.append(self.attn.forward_raster(cur))
-                hfs.append(det)
-        else:
-            srcs = [self.attn.forward_raster(x, ln1)]
-            hfs = None
-        xh, stats = wfa.MsFuse.apply(x, s_attn, float(self.norm2.eps), *srcs)
-        out = wfa.ccf_ffn(xh, stats, self.norm2, self.mlp, s_mlp)
+        xh, stats = _OPS.msfuse(srcs, x, s_attn, float(self.norm2.eps), True)
+        out = ffn_op(xh, stats, self.norm2, self.mlp, s_mlp)
         if self.level > 0:
             return out, tuple(reversed(hfs))
         return out
@@ -436,30 +444,16 @@ class Block(nn.Module):
         x = self._prep(x)
         s_attn, s_mlp = self._branch_scales(x.shape[0], x.device)
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
-        if wfa.needs_grad(x, *self.parameters()):
-            x_h = None
-            if self.level > 0:
-                self.dwt_downsamples._check()
-                cur, x_h = x, []
-                for i in range(self.level):
-                    cur, det = wfa.dwt3d_haar(cur, ln1 if i == 0 else None)
-                    x_h.append(det)
-                a = self.attn.forward_raster(cur)
-                x_h = list(reversed(x_h))
-            else:
-                a = self.attn.forward_raster(x, ln1)
-            xh, stats = wfa.MsFuse.apply(x, s_attn, float(self.norm2.eps), a)
-            out = wfa.ccf_ffn(xh, stats, self.norm2, self.mlp, s_mlp)
-            return (out, x_h) if self.level > 0 else out
         x_h = None
         if self.level > 0:
-            ll, bands = self.dwt_downsamples.decompose_cl(x, self.level, ln1)
-            a = self.attn.forward_raster(ll)
+            self.dwt_downsamples._check()
+            bands = self._levels(x, ln1, self.level)
+            a = self.attn.forward_raster(bands[-1][0])
             x_h = [ops.bands_to_coeffs(b)[1] for b in reversed(bands)]
         else:
             a = self.attn.forward_raster(x, ln1)
-        xh, stats = ops.msfuse([a], x, self.norm2.eps, s_attn)
-        out = ops.ccf_ffn(xh, stats, self.norm2, self.mlp, s_mlp)
+        xh, stats = _OPS.msfuse([a], x, s_attn, float(self.norm2.eps), True)
+        out = ffn_op(xh, stats, self.norm2, self.mlp, s_mlp)
         if self.level > 0:
             return out, x_h
         return out

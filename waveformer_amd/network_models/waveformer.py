@@ -137,7 +137,8 @@ class MultiscaleTransformer(nn.Module):
         return outs, outs_hf
 
     def forward(self, x_rgb: torch.Tensor):
-        return self.forward_features(x_rgb)
+        with ops.weight_scope(self):  # split weights rebuilt once per forward (one launch)
+            return self.forward_features(x_rgb)
 
     def flops(self) -> int:
         return 0

@@ -84,20 +84,132 @@ def _prec() -> int:
     return PRECISIONS[_precision]
 
 
-def split_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None) -> torch.Tensor:
-    """[2][N][K] bf16 {hi, lo} planes of an fp32 weight (wf_split_f32_to_bf16x2), cached on the
-    parameter until it changes (in-place optimizer steps / load_state_dict bump _version)."""
-    ver = p._version
-    ent = getattr(p, "_wf_bf16x2", None)
-    if ent is not None and ent[0] == ver and ent[1] == p.data_ptr():
-        return ent[2]
-    src = p.detach()
-    _check(src, "weight")
-    out = torch.empty((2,) + tuple(src.shape if shape is None else shape), dtype=torch.bfloat16,
-                      device=src.device)
-    _lib.call("wf_split_f32_to_bf16x2", src.data_ptr(), out.data_ptr(), src.numel(), _stream())
-    p._wf_bf16x2 = (ver, p.data_ptr(), out)
+def prec_id() -> int:
+    """WF_PREC_* id of the current global precision."""
+    return PRECISIONS[_precision]
+
+
+# ------------------------------------------------------------------------------------------
+# per-forward weight preparation: the bf16 hi / lo planes (and other derived forms) of the
+# fp32 parameters are rebuilt at the start of every top-level forward, never cached across
+# forwards -- a cache keyed on (data_ptr, _version) goes stale when a caller writes a weight
+# through .data (EMA, weight surgery), which bumps no version.  A model's split weights are
+# re-split together in ONE launch (WeightArena); inside a HIP graph that launch is captured
+# too, so replays always see the current weights.
+# ------------------------------------------------------------------------------------------
+class WeightArena:
+    """The [2][numel] bf16 {hi, lo} planes of a list of fp32 CUDA weights in one buffer,
+    refreshed by one wf_split_f32_to_bf16x2_multi launch."""
+
+    def __init__(self, params: Sequence[torch.Tensor]):
+        dev = params[0].device
+        self.key = tuple((p.data_ptr(), p.numel()) for p in params)
+        pre, dsts, off = [0], [], 0
+        blocks = []
+        for p in params:
+            blocks.append(off)
+            off += 2 * p.numel()            # numel % 8 == 0: every plane stays 16-B aligned
+        self.buf = torch.empty(max(off, 8), dtype=torch.bfloat16, device=dev)
+        self.views: Dict[int, torch.Tensor] = {}
+        for p, o in zip(params, blocks):
+            v = self.buf[o:o + 2 * p.numel()]
+            self.views[p.data_ptr()] = v
+            dsts.append(v.data_ptr())
+            pre.append(pre[-1] + p.numel())
+        self.n, self.total = len(params), pre[-1]
+        table = pre + [p.data_ptr() for p in params] + dsts
+        self.table = torch.tensor(table, dtype=torch.int64).to(dev)
+
+    def refresh(self) -> None:
+        _lib.call("wf_split_f32_to_bf16x2_multi", self.table.data_ptr(), self.n, self.total,
+                  _stream())
+
+
+class _Scope:
+    def __init__(self, arena: Optional[WeightArena]):
+        self.arena = arena
+        self.cache: Dict[tuple, torch.Tensor] = {}
+
+
+_scope: Optional[_Scope] = None
+
+
+def split_params(module: torch.nn.Module) -> List[torch.Tensor]:
+    """The fp32 CUDA weights `module` feeds to the MFMA kernels as split operands (each
+    module that has some lists them in `_wf_split_params()`)."""
+    seen, out = set(), []
+    for m in module.modules():
+        fn = getattr(m, "_wf_split_params", None)
+        if fn is None:
+            continue
+        for p in fn():
+            if (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
+                    and p.numel() % 8 == 0 and p.data_ptr() not in seen):
+                seen.add(p.data_ptr())
+                out.append(p)
     return out
+
+
+class weight_scope:
+    """`with ops.weight_scope(model): ...` -- one forward of `model`: its split weights are
+    re-split in one launch on entry and looked up by every kernel wrapper inside; derived
+    forms of other weights (packed conv weights, dense attention biases) are made once per
+    scope.  Nested scopes reuse the outer one."""
+
+    def __init__(self, module: torch.nn.Module):
+        self.module = module
+        self.owner = False
+
+    def __enter__(self):
+        global _scope
+        if _scope is not None:
+            return self
+        arena = None
+        params = split_params(self.module)
+        if params:
+            arena = getattr(self.module, "_wf_arena", None)
+            if arena is None or arena.key != tuple((p.data_ptr(), p.numel()) for p in params):
+                arena = WeightArena(params)
+                object.__setattr__(self.module, "_wf_arena", arena)
+            arena.refresh()
+        _scope = _Scope(arena)
+        self.owner = True
+        return self
+
+    def __exit__(self, *exc):
+        global _scope
+        if self.owner:
+            _scope = None
+
+
+def per_forward(key: tuple, make):
+    """make() once per weight_scope (once per call outside any scope)."""
+    if _scope is None:
+        return make()
+    v = _scope.cache.get(key)
+    if v is None:
+        v = make()
+        _scope.cache[key] = v
+    return v
+
+
+def split_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None) -> torch.Tensor:
+    """[2][N][K] bf16 {hi, lo} planes of an fp32 weight (wf_split_f32_to_bf16x2): the weight
+    arena's view inside a weight_scope, else split now."""
+    shp = (2,) + tuple(p.shape if shape is None else shape)
+    if _scope is not None and _scope.arena is not None:
+        v = _scope.arena.views.get(p.data_ptr())
+        if v is not None and v.numel() == 2 * p.numel():
+            return v.view(shp)
+
+    def make():
+        src = p.detach()
+        _check(src, "weight")
+        out = torch.empty(shp, dtype=torch.bfloat16, device=src.device)
+        _lib.call("wf_split_f32_to_bf16x2", src.data_ptr(), out.data_ptr(), src.numel(),
+                  _stream())
+        return out
+    return per_forward(("split", p.data_ptr(), shp), make)
 
 
 # ------------------------------------------------------------------------------------------
@@ -362,20 +474,17 @@ def empty_cl(B: int, C: int, D: int, H: int, W: int, device) -> torch.Tensor:
 
 def conv3d_k3_packed(weight: torch.Tensor) -> torch.Tensor:
     """[2][K-steps][Cout][32] bf16 hi / lo planes of a (Cout, Cin, 3, 3, 3) conv weight
-    (wf_conv3d_k3_pack), cached on the parameter until it changes."""
-    ver = weight._version
-    ent = getattr(weight, "_wf_conv3", None)
-    if ent is not None and ent[0] == ver and ent[1] == weight.data_ptr():
-        return ent[2]
-    w = weight.detach()
-    _check(w, "conv weight", contiguous=False)
-    w = w.contiguous()  # a channels_last_3d model keeps its 5-D weights channel-last
-    Cout, Cin = w.shape[:2]
-    n = _lib.query("wf_conv3d_k3_packed_elems", Cin, Cout)
-    out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
-    _lib.call("wf_conv3d_k3_pack", w.data_ptr(), out.data_ptr(), Cin, Cout, _stream())
-    weight._wf_conv3 = (ver, weight.data_ptr(), out)
-    return out
+    (wf_conv3d_k3_pack), made once per weight_scope."""
+    def make():
+        w = weight.detach()
+        _check(w, "conv weight", contiguous=False)
+        w = w.contiguous()  # a channels_last_3d model keeps its 5-D weights channel-last
+        Cout, Cin = w.shape[:2]
+        n = _lib.query("wf_conv3d_k3_packed_elems", Cin, Cout)
+        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+        _lib.call("wf_conv3d_k3_pack", w.data_ptr(), out.data_ptr(), Cin, Cout, _stream())
+        return out
+    return per_forward(("conv3", weight.data_ptr(), tuple(weight.shape)), make)
 
 
 def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -529,10 +638,41 @@ def rel_pos_bias(table: torch.Tensor, index: torch.Tensor) -> torch.Tensor:
     return out
 
 
+_TABLE_OK: Dict[tuple, bool] = {}
+
+
+def index_is_formula(index: torch.Tensor, ws: int) -> bool:
+    """relative_position_index == the reference's formula for window ws (attention.py:40-56)?
+    Cached per (buffer, version): the table-bias kernel evaluates the formula itself."""
+    key = (index.data_ptr(), index._version, ws, str(index.device))
+    ok = _TABLE_OK.get(key)
+    if ok is None:
+        r = torch.arange(ws, device=index.device)
+        s, h, w = torch.meshgrid(r, r, r, indexing="ij")
+        pos = torch.stack([s.reshape(-1), h.reshape(-1), w.reshape(-1)], dim=-1)
+        d = pos[:, None, :] - pos[None, :, :] + (ws - 1)
+        ref = d[..., 0] * (3 * ws - 1) + d[..., 1] * (2 * ws - 1) + d[..., 2]
+        ok = tuple(index.shape) == tuple(ref.shape) and bool(torch.equal(index, ref))
+        _TABLE_OK[key] = ok
+    return ok
+
+
+def attention_bias(table: torch.Tensor, index: torch.Tensor, ws: int, heads: int,
+                   head_dim: int) -> torch.Tensor:
+    """What the window-attention kernels read as the bias: the ((2ws-1)^3, heads) table itself
+    when the table-bias kernel applies (ws 8, head_dim 16, index == the formula), else the
+    dense (heads, N, N) expansion, made once per weight_scope."""
+    if ws == 8 and head_dim == 16 and index_is_formula(index, ws):
+        return table.detach()
+    return per_forward(("relbias", table.data_ptr(), index.data_ptr()),
+                       lambda: rel_pos_bias(table.detach(), index))
+
+
 def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torch.Tensor],
                      bias: torch.Tensor, wproj: torch.Tensor, bproj: Optional[torch.Tensor],
                      ws: int, heads: int, scale: float,
-                     ln: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None) -> torch.Tensor:
+                     ln: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None,
+                     prec: Optional[int] = None) -> torch.Tensor:
     """window_partition + Attention.forward + reshape-reverse (Q1) over a channel-last raster.
     Returns (B, D1, H1, W1, C) whose rows are the window-major attention outputs.  `bias` is
     the dense (heads, N, N) bias, or the ((2ws-1)^3, heads) table itself when the index is the
@@ -556,7 +696,7 @@ def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torc
     if ln is not None:
         lw, lb, eps = ln
     out = torch.empty_like(x_cl)
-    prec = _prec()
+    prec = _prec() if prec is None else prec
     wsb = _lib.query("wf_window_attention_workspace_bytes", B, C, D1, H1, W1, prec)
     work = torch.empty(wsb, dtype=torch.uint8, device=x_cl.device)
     _lib.call("wf_window_attention_fwd_table" if table else "wf_window_attention_fwd",
@@ -604,23 +744,31 @@ def msfuse(srcs: Sequence[torch.Tensor], shortcut: torch.Tensor, ln_eps: Optiona
 def ccf_ffn(xh: torch.Tensor, stats: Optional[torch.Tensor], norm2: Optional[torch.nn.Module],
             mlp: torch.nn.Module, branch_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Block path (stats given): xh + n2 + ffn(n2), n2 = norm2(xh).  Bare (stats None): xh + ffn(xh)."""
-    _check(xh, "x")
-    B, D, H, W, C = xh.shape
-    hid = mlp.C_hid
-    pw = split_weight(mlp.pwconv.weight, (hid, C))
-    fc = split_weight(mlp.fc.weight)
-    prec = _prec()
-    out = torch.empty_like(xh)
-    wsb = _lib.query("wf_ccf_ffn_workspace_bytes", B, C, hid, D, H, W, prec)
-    work = torch.empty(wsb, dtype=torch.uint8, device=xh.device)
     n2w = n2b = None
     if stats is not None:
         n2w, n2b = norm2.weight, norm2.bias
+    return ccf_ffn_raw(xh, stats, n2w, n2b, mlp.pwconv.weight, mlp.pwconv.bias,
+                       mlp.norm1.weight, mlp.norm1.bias, float(mlp.norm1.eps),
+                       mlp.dwconv.weight, mlp.dwconv.bias, mlp.norm2.weight, mlp.norm2.bias,
+                       float(mlp.norm2.eps), mlp.fc.weight, mlp.fc.bias, branch_scale)
+
+
+def ccf_ffn_raw(xh, stats, n2w, n2b, pww, pwb, l1w, l1b, eps1, dww, dwb, l2w, l2b, eps2, fcw, fcb,
+                branch_scale=None, prec: Optional[int] = None) -> torch.Tensor:
+    """ccf_ffn on the parameter tensors themselves (the waveformer::ccf_ffn op's kernel)."""
+    _check(xh, "x")
+    B, D, H, W, C = xh.shape
+    hid = pww.shape[0]
+    pw = split_weight(pww, (hid, C))
+    fc = split_weight(fcw)
+    prec = _prec() if prec is None else prec
+    out = torch.empty_like(xh)
+    wsb = _lib.query("wf_ccf_ffn_workspace_bytes", B, C, hid, D, H, W, prec)
+    work = torch.empty(wsb, dtype=torch.uint8, device=xh.device)
     args = (xh.data_ptr(), _ptr(stats), _ptr(n2w), _ptr(n2b),
-            pw.data_ptr(), _ptr(mlp.pwconv.bias), mlp.norm1.weight.data_ptr(),
-            mlp.norm1.bias.data_ptr(), float(mlp.norm1.eps), mlp.dwconv.weight.data_ptr(),
-            mlp.dwconv.bias.data_ptr(), mlp.norm2.weight.data_ptr(), mlp.norm2.bias.data_ptr(),
-            float(mlp.norm2.eps), fc.data_ptr(), _ptr(mlp.fc.bias), _ptr(branch_scale),
+            pw.data_ptr(), _ptr(pwb), l1w.data_ptr(), l1b.data_ptr(), float(eps1),
+            dww.data_ptr(), dwb.data_ptr(), l2w.data_ptr(), l2b.data_ptr(), float(eps2),
+            fc.data_ptr(), _ptr(fcb), _ptr(branch_scale),
             out.data_ptr(), work.data_ptr(), B, C, hid, D, H, W, prec, _stream())
     # the three launches are issued separately so they can be timed one by one (bench.py)
     ccf_ffn_pwconv(args)
