@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """bench.py -- WaveFormer encoder forward on MI355X (BASELINE.json configs[1]).
 
-    python bench.py [--gpus N --steps K --warmup W --batch B --precision bf16x3|bf16]
+    python bench.py [--gpus N --steps K --warmup W --batch B --precision bf16x3|bf16|fp16]
+    python bench.py --workload full --img 192 --precision fp16    (config 5)
 
 One step = one MultiscaleTransformer forward (PatchEmbed -> 4 stages of DWT / window
 attention / multi-scale fuse / CCF_FFN / PatchMerging -> proj_out; network_models/waveformer.py
@@ -56,7 +57,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None,
                     help="volumes per GPU per step (default: 8 for encoder, 1 for train)")
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"])
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp16"])
     ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
     ap.add_argument("--roofline-op", default="auto")
     ap.add_argument("--cpu-baseline", type=int, default=1)
@@ -65,8 +66,11 @@ def parse():
                     help="0: skip the per-op roofline timing after the timed region (a rocprof "
                          "trace then holds the warm-up and the graph replays only)")
     ap.add_argument("--img", type=int, default=128)
-    ap.add_argument("--workload", default="encoder", choices=["encoder", "sliding", "train"],
-                    help="encoder: config 2 (the driver's line); sliding: config 3, one "
+    ap.add_argument("--workload", default="encoder",
+                    choices=["encoder", "full", "sliding", "train"],
+                    help="encoder: config 2 (the driver's line); full: the whole Waveformer "
+                         "forward (with --img 192 --precision fp16: config 5, HF refinement "
+                         "branch on, Dice vs the reference's 192^3 labels); sliding: config 3, one "
                          "240x240x155x4 case through the full Waveformer with the windows "
                          "sharded over the ranks and all-gathered over RCCL; train: config 4, "
                          "fwd + DiceCE + bwd + clip + AdamW of the full Waveformer, DDP")
@@ -78,7 +82,7 @@ def parse():
         # encoder: B = 8 is the top of SURVEY 8d's C2 range {1, 2, 4, 8} and fills the 8^3 / 16^3
         # stages better than 4 (902 vs 794 volumes/s measured); train: MIOpen find at B > 1 on
         # a fresh box does not finish within the bench's budget
-        args.batch = 1 if args.workload == "train" else 8
+        args.batch = {"train": 1, "full": 2}.get(args.workload, 8)
     return args
 
 
@@ -99,7 +103,7 @@ def _dw_bytes(a, kw, out):
     the (mean, M2) partial per 32 channels of every position."""
     from waveformer_amd import ops
     P, Hd = a[1], a[2]
-    e = 4 if ops.get_precision() == "bf16x3" else 2
+    e = 2 if ops.get_precision() == "bf16" else 4  # bf16x3 / fp16 keep fp32 intermediates
     if _stage1(a):
         C = a[0][20]
         io = 2 * P * C * 4 + (P * 8 if a[0][1] else 0)
@@ -219,6 +223,18 @@ def build_encoder(img, device):
     return m.eval().to(device)
 
 
+def build_full(img, device, hf):
+    """The whole Waveformer (encoder + IDWT decoder + UnetrBasicBlock / UnetResBlock convs),
+    reference init; hf = the HF refinement branch (network_backbone.py:196-197, config 5)."""
+    import waveformer_amd.network_models as NM
+    torch.manual_seed(0)
+    cfg = {"transformer": {"hf_refinement": True}} if hf else None
+    m = NM.Waveformer(img_size=(img,) * 3, in_chans=4, out_chans=4, depths=[2, 2, 2, 2],
+                      feat_size=[48, 96, 192, 384], num_heads=[3, 6, 12, 24],
+                      network_config=cfg)
+    return m.eval().to(device)
+
+
 def cpu_baseline(seconds_budget=20.0):
     """The oracle encoder (fp32 PyTorch on the host CPU) on one 128^3 x 4 volume."""
     from oracle import ref_waveformer as R
@@ -241,19 +257,25 @@ def cpu_baseline(seconds_budget=20.0):
                       f"{dt:.2f} s/volume"}
 
 
-def parity_dice(device):
-    """Full Waveformer at 128^3 x 4 with the golden rule weights vs the reference's labels."""
+def parity_dice(device, case_name="full128"):
+    """Full Waveformer (full128: 128^3 x 4; full192hf: 192^3 x 4 with the HF refinement branch,
+    config 5) with the golden rule weights at the bench's precision vs the reference's labels."""
     from tests import cases as C
-    case = C.cases()["full128"]
+    from waveformer_amd import ops
+    case = C.cases()[case_name]
     m, _ = C.build(case, device)
     with torch.no_grad():
         lab = m(C.case_input(case).to(device)).argmax(1).cpu()
-    ref = C.g("full128_labels").long()
+    ref = C.g(case_name + "_labels").long()
     d = [C.dice(a, b) for a, b in zip(C.brats_regions(lab), C.brats_regions(ref))]
     del m
     torch.cuda.empty_cache()
+    size = case.input_shape[2]
     return {"dice_tc_wt_et": [round(v, 6) for v in d], "dice_delta_max": round(1 - min(d), 6),
-            "vs": "reference Waveformer labels at 128^3x4 (tests/golden/ref_fixtures.npz)"}
+            "precision": ops.get_precision(),
+            "vs": f"reference Waveformer labels at {size}^3x4"
+                  f"{' (HF refinement)' if 'hf' in case_name else ''} "
+                  f"(tests/golden/ref_fixtures.npz)"}
 
 
 def main_sliding(args, world, rank, dev):
@@ -450,13 +472,15 @@ def main():
     if args.workload == "train":
         return main_train(args, world, rank, dev)
 
-    model = build_encoder(args.img, dev)
+    full = args.workload == "full"
+    hf = full and args.img == 192  # config 5: 192^3 crops with the HF refinement branch
+    model = build_full(args.img, dev, hf) if full else build_encoder(args.img, dev)
     x = torch.randn(args.batch, 4, args.img, args.img, args.img, device=dev,
                     generator=torch.Generator(device=dev).manual_seed(1234 + rank))
 
     roof_op = args.roofline_op if args.roofline_op != "auto" else "ccf_ffn_dwconv"
-    timers = {n: OpTimer(n) for n in dict.fromkeys([roof_op, "dwt3d_haar", "msfuse",
-                                                    "window_attention"])}
+    timers = {n: OpTimer(n) for n in dict.fromkeys(
+        [roof_op, "dwt3d_haar", "msfuse", "window_attention"] + (["conv3d_k3"] if full else []))}
 
     def step():
         with torch.no_grad():
@@ -520,7 +544,9 @@ def main():
     if rank == 0:
         vols = args.batch * args.steps * world
         out = {
-            "metric": METRIC,
+            "metric": METRIC if not full else
+            f"{args.img}^3x4 volumes/sec fwd, full Waveformer"
+            f"{' + HF refinement (config 5)' if hf else ''} + Dice delta vs reference",
             "value": vols / dt,
             "unit": "volumes/s",
             "n_gpus": world,
@@ -531,23 +557,30 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.precision,
-            "data": "synthetic: randn 128^3x4 crops resident in HBM, reference-init random weights",
-            "config": {"workload": f"MultiscaleTransformer (WaveFormer encoder) forward, "
-                                   f"{args.img}^3x4 crops",
+            "data": f"synthetic: randn {args.img}^3x4 crops resident in HBM, reference-init "
+                    f"random weights",
+            "config": {"workload": (f"Waveformer forward (encoder + IDWT decoder"
+                                    f"{' + HFRefinementRes' if hf else ''}), "
+                                    if full else "MultiscaleTransformer (WaveFormer encoder) "
+                                                 "forward, ") + f"{args.img}^3x4 crops",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "precision": args.precision,
                        "parallelism": f"replicas x{world} (no data-path collective)",
                        "hip_graph": graph is not None},
         }
         def roofline(name, r):
-            if name == "window_attention":  # MFMA-bound: algorithmic FLOPs vs dense bf16 peak
+            if name in ("window_attention", "conv3d_k3"):
+                # MFMA-bound: algorithmic FLOPs vs the dense bf16 / fp16 peak (the same 2.5
+                # PFLOP/s on gfx950); bf16x3 issues three MFMAs per product
                 ach = r["rate"] / 1e12
+                issue = 3 if args.precision == "bf16x3" else 1
                 return {"bound": "mfma", "kernel": name, "achieved": round(ach, 2),
                         "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
                         "algorithmic_flops_per_launch": r["work_per_launch"],
                         "avg_launch_us": round(r["avg_ms"] * 1e3, 2),
-                        "launches_timed": r["launches"]}
+                        "launches_timed": r["launches"],
+                        "mfma_issue_frac": round(issue * ach / MFMA_BF16_PEAK_TFLOPS, 4)}
             ach = r["rate"] / 1e9
             return {"bound": "hbm", "kernel": name, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
@@ -560,10 +593,10 @@ def main():
         out["rooflines"] = {n: roofline(n, r) for n, r in roofs.items() if r and n != roof_op}
         if args.parity:
             try:
-                out["parity"] = parity_dice(dev)
+                out["parity"] = parity_dice(dev, "full192hf" if hf else "full128")
             except Exception as e:
                 out["parity"] = {"error": str(e)[:200]}
-        if args.cpu_baseline and world == 1:
+        if args.cpu_baseline and world == 1 and not full:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -24,10 +24,13 @@
  *   WF_PREC_BF16X3 (1): fp32-faithful -- every operand x is split into hi = bf16(x) and
  *                      lo = bf16(x - hi) and products take hi*hi + lo*hi + hi*lo on the bf16
  *                      MFMA pipes (relative error ~2^-17); intermediates stored fp32.
- * LayerNorm, softmax, GELU, wavelets, interpolation and residual adds are fp32 in both.
- * Weights passed as `*_bf16x2` are nn.Linear / 1x1x1-Conv3d weights [N][K] as two bf16 planes
- * [2][N][K] = {hi, lo} (wf_split_f32_to_bf16x2); WF_PREC_BF16 reads the hi plane only.  Every
- * other parameter is the fp32 module tensor as-is.
+ *   WF_PREC_FP16  (2): operands rounded to fp16 (relative error 2^-11), fp32 accumulation on
+ *                      the v_mfma_f32_*_f16 pipes; intermediates stored fp32 (config 5).
+ * LayerNorm, softmax, GELU, wavelets, interpolation and residual adds are fp32 in all modes.
+ * Weights passed as `*_bf16x2` are nn.Linear / 1x1x1-Conv3d weights [N][K] as two 16-bit
+ * planes [2][N][K]: {hi, lo} bf16 (wf_split_f32_to_bf16x2) for WF_PREC_BF16X3 and WF_PREC_BF16
+ * (which reads the hi plane only); for WF_PREC_FP16 plane 0 holds fp16(W) (wf_cast_f32_to_f16x2,
+ * plane 1 unused).  Every other parameter is the fp32 module tensor as-is.
  */
 #ifndef WAVEFORMER_HIP_H
 #define WAVEFORMER_HIP_H
@@ -38,9 +41,9 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 8
+#define WF_ABI_VERSION 9
 
-enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1 };
+enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
 enum {
   WF_OK = 0,
@@ -66,6 +69,12 @@ int wf_split_f32_to_bf16x2(const float* in, uint16_t* out, int64_t n, void* stre
  * ([2][numel] bf16 each); total = table[n].                                                */
 int wf_split_f32_to_bf16x2_multi(const int64_t* table_dev, int64_t n, int64_t total,
                                  void* stream);
+
+/* The WF_PREC_FP16 weight planes: out[i] = fp16(in[i]), out[n + i] = 0.  _multi: as
+ * wf_split_f32_to_bf16x2_multi.                                                            */
+int wf_cast_f32_to_f16x2(const float* in, uint16_t* out, int64_t n, void* stream);
+int wf_cast_f32_to_f16x2_multi(const int64_t* table_dev, int64_t n, int64_t total,
+                               void* stream);
 
 /* ---- a10: PatchEmbed -------------------------------------------------------------- */
 /* Replaces monai PatchEmbed.proj = Conv3d(Cin, Cout, k=2, s=2) as called at
@@ -132,6 +141,9 @@ int wf_idwt3d_level(const float* const* coef, const int64_t* coef_strides, int64
  * fp32 (Cout, Cin, 3, 3, 3) weight ([2] hi / lo planes, K-step-major).  precision WF_PREC_*. */
 int64_t wf_conv3d_k3_packed_elems(int64_t Cin, int64_t Cout);
 int wf_conv3d_k3_pack(const float* w, uint16_t* packed, int64_t Cin, int64_t Cout, void* stream);
+/* The same packing as fp16 (plane 0 = fp16(W), plane 1 zero) for WF_PREC_FP16.             */
+int wf_conv3d_k3_pack_f16(const float* w, uint16_t* packed, int64_t Cin, int64_t Cout,
+                          void* stream);
 /* stats_acc: NULL, or a ZEROED (B, Cout, 2) fp64 buffer that receives each output channel's
  * sum and sum of squares per sample (InstanceNorm statistics fused into the epilogue; finish
  * with wf_instnorm_finalize).                                                                 */

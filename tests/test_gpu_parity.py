@@ -9,7 +9,11 @@ Tolerances (stated per check):
       - default precision "bf16x3" (split hi/lo bf16 operands, fp32-faithful): rel-L2 <= 5e-5
         per op and per Block, <= 1e-4 through the encoder and the full model;
       - fast precision "bf16": rel-L2 <= 1e-2 for a single op, <= 2e-2 through a Block,
-        <= 3e-2 through the encoder (bf16 rounds to 2^-9 = 2e-3 relative per operand).
+        <= 3e-2 through the encoder (bf16 rounds to 2^-9 = 2e-3 relative per operand);
+      - config 5's "fp16" (fp16 operands on the f16 MFMA pipes, fp32 accumulation and fp32
+        LayerNorm / softmax / residual): rel-L2 <= 2e-3 for a single op, <= 3e-3 through a
+        Block, <= 5e-3 through the encoder and the full model (fp16 rounds to 2^-12 = 2.4e-4
+        relative per operand, 8x finer than bf16).
   * end-to-end metric (BASELINE.json north_star): Dice of TC / WT / ET of the full model's
     argmax labels at 128^3 x 4 >= 1 - 1e-3 against the reference's labels.
 """
@@ -152,7 +156,7 @@ def test_attention_vs_oracle(ws, heads, dim, B_):
     from waveformer_amd import ops
     x = seeded_randn((B_, ws ** 3, dim), 12)
     ref = R.attention(sd, "", x, heads, ws)
-    for prec, tol in (("bf16x3", 5e-5), ("bf16", 1e-2)):
+    for prec, tol in (("bf16x3", 5e-5), ("bf16", 1e-2), ("fp16", 2e-3)):
         with torch.no_grad(), ops.precision(prec):
             out = m(cuda(x))
         assert C.rel_l2(out, ref) <= tol, prec
@@ -184,7 +188,7 @@ def test_ccf_ffn_stage1_fused_vs_oracle(shape, block):
         ref = x + R.ccf_ffn(sd, "", n2) * bs.view(-1, 1, 1, 1, 1)
     else:
         ref = x + (R.ccf_ffn(sd, "", x) - x) * bs.view(-1, 1, 1, 1, 1)
-    for prec, tol in (("bf16x3", 5e-5), ("bf16", 1e-2)):
+    for prec, tol in (("bf16x3", 5e-5), ("bf16", 1e-2), ("fp16", 2e-3)):
         with torch.no_grad(), ops.precision(prec):
             xc = cuda(x)
             stats = ops.msfuse([], xc, 1e-6)[1] if block else None
@@ -219,12 +223,17 @@ def test_window_attention_q1_layout_on_raster():
 
 
 # ------------------------------------------------------------------------------ module level
+# Dice bound of the fp16 path (see test_full_model_128_dice_vs_reference for why reduced-
+# precision operands move Dice at all with these weights)
+FP16_DICE = 5e-3  # measured 2.4e-3 (192^3 HF) and 2.9e-3 (128^3)
+
 # rel-L2 bounds per precision (measured: bf16x3 2.5e-6..2.6e-5, bf16 1.5e-3..1e-2)
 TOL = {"bf16x3": {"tensor": 5e-5, "block": 5e-5, "encoder": 1e-4, "full": 1e-4},
-       "bf16": {"tensor": 1e-2, "block": 2e-2, "encoder": 3e-2, "full": 3e-2}}
+       "bf16": {"tensor": 1e-2, "block": 2e-2, "encoder": 3e-2, "full": 3e-2},
+       "fp16": {"tensor": 2e-3, "block": 3e-3, "encoder": 5e-3, "full": 5e-3}}
 
 
-@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16", "fp16"])
 @pytest.mark.parametrize("name", ["attn_ws8", "attn_ws2_h1", "attn_ws4_h2", "merge", "ccf_ffn",
                                   "block_l3", "block_l1", "block_l0", "block_ss_l2", "enc32",
                                   "full32", "full32hf"])
@@ -285,20 +294,23 @@ def test_encoder192_vs_reference_summaries():
         assert C.rel_l2(sample, C.g(k + "__sample")) <= 2e-4, (k, C.rel_l2(sample, C.g(k + "__sample")))
 
 
-def test_full_model_192_hf_refinement_dice_vs_reference():
-    """config 5: full model with the HF refinement branch at 192^3 x 4 (bf16x3): Dice of the
-    argmax labels (TC / WT / ET) against the reference's own labels."""
+@pytest.mark.parametrize("prec,bound", [("bf16x3", 1e-3), ("fp16", FP16_DICE)])
+def test_full_model_192_hf_refinement_dice_vs_reference(prec, bound):
+    """config 5: full model with the HF refinement branch at 192^3 x 4: Dice of the argmax
+    labels (TC / WT / ET) against the reference's own labels -- fp32-faithful bf16x3, and the
+    fp16 MFMA path config 5 names (fp16 operands, fp32 accumulation / LayerNorm / softmax)."""
+    from waveformer_amd import ops
     case = C.cases()["full192hf"]
     m, _ = C.build(case, DEV)
-    with torch.no_grad():
+    with torch.no_grad(), ops.precision(prec):
         logits = m(cuda(C.case_input(case)))
     lab = logits.argmax(1).cpu()
     ref = C.g("full192hf_labels").long()
     d = [C.dice(a, b) for a, b in zip(C.brats_regions(lab), C.brats_regions(ref))]
-    assert min(d) >= 1 - 1e-3, d
+    assert min(d) >= 1 - bound, d
 
 
-@pytest.mark.parametrize("prec,bound", [("bf16x3", 1e-3), ("bf16", 5e-2)])
+@pytest.mark.parametrize("prec,bound", [("bf16x3", 1e-3), ("bf16", 5e-2), ("fp16", FP16_DICE)])
 def test_full_model_128_dice_vs_reference(prec, bound):
     """BASELINE north_star: Dice within 1e-3 of the reference (TC / WT / ET of the argmax
     labels of the full model at 128^3 x 4).  The fp32-faithful default (bf16x3) meets it;

@@ -28,6 +28,8 @@ SIGNATURES = {
     "wf_cast_f32_to_bf16": (_I, [_P, _P, _I64, _P]),
     "wf_split_f32_to_bf16x2": (_I, [_P, _P, _I64, _P]),
     "wf_split_f32_to_bf16x2_multi": (_I, [_P, _I64, _I64, _P]),
+    "wf_cast_f32_to_f16x2": (_I, [_P, _P, _I64, _P]),
+    "wf_cast_f32_to_f16x2_multi": (_I, [_P, _I64, _I64, _P]),
     "wf_patch_embed_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwt3d_haar_fwd": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
@@ -36,6 +38,7 @@ SIGNATURES = {
                              _P]),
     "wf_conv3d_k3_packed_elems": (_I64, [_I64, _I64]),
     "wf_conv3d_k3_pack": (_I, [_P, _P, _I64, _I64, _P]),
+    "wf_conv3d_k3_pack_f16": (_I, [_P, _P, _I64, _I64, _P]),
     "wf_conv3d_k3_fwd": (_I, [_P, _I64, _P, _P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I64,
                               _I64, _I, _P]),
     "wf_instnorm_finalize": (_I, [_P, _P, _I64, _I64, _I64, _F, _P]),
@@ -91,7 +94,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 _lock = threading.Lock()
 _lib = None
 _err = None

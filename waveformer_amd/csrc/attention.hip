@@ -35,18 +35,20 @@ __device__ __forceinline__ void attn_block(int gx, int heads, int& qb, int& h, i
   bw = t / heads;
 }
 
-template <bool SPLIT>
+// 8 consecutive values of an activation row as MFMA operands: fp32 storage (PREC_SPLIT,
+// PREC_FP16) converted to the operand kind (+ the split's lo part), or bf16 storage as-is
+template <int P>
 __device__ __forceinline__ void load8_split(const void* base, int64_t off, bf16x8& hi,
                                             bf16x8& lo) {
-  if (SPLIT) {
+  if (store32(P)) {
     const f32x4* p = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(base) + off);
     const f32x4 a = p[0], b = p[1];
     const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint16_t h = f2bf(v[j]);
+      const uint16_t h = op_cvt<P>(v[j]);
       hi[j] = (short)h;
-      lo[j] = (short)f2bf(v[j] - bf2f(h));
+      lo[j] = op_lo<P>(v[j], h);
     }
   } else {
     hi = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(base) + off);
@@ -60,12 +62,13 @@ __device__ __forceinline__ void load8_split(const void* base, int64_t off, bf16x
 // coordinates -- the (heads, N, N) tensor (805 MB of L2 reads per stage-1 launch) is never
 // touched.  The 4 keys a lane holds share (z, y) and have consecutive x, so their indices are
 // i0, i0 - 1, i0 - 2, i0 - 3.
-template <int HD, int KT, bool SPLIT, int WS = 0>
+template <int HD, int KT, int P, int WS = 0>
 __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__ qkv,
                                                         const float* __restrict__ bias,
                                                         void* __restrict__ out,
                                                         float* __restrict__ lse, int N,
                                                         int heads, float scale_log2) {
+  constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   constexpr int TBLN = WS ? (2 * WS - 2) * (3 * WS - 1) + (2 * WS - 2) * (2 * WS - 1) + 2 * WS - 1
                           : 1;  // reachable table rows (Q2 collapses the (2ws-1)^3 table)
   __shared__ float tb[TBLN];
@@ -95,13 +98,13 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
     qfl[c] = bf16x4{0, 0, 0, 0};
     if (!qv) continue;
     const int64_t off = (row0 + q) * ld + h * HD + c * 16 + g4;
-    if (SPLIT) {
+    if (store32(P)) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(qkv) + off);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint16_t hh = f2bf(v[j]);
+        const uint16_t hh = op_cvt<P>(v[j]);
         qf[c][j] = (short)hh;
-        qfl[c][j] = (short)f2bf(v[j] - bf2f(hh));
+        qfl[c][j] = op_lo<P>(v[j], hh);
       }
     } else {
       qf[c] = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const uint16_t*>(qkv) + off);
@@ -129,8 +132,8 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
       bf16x8 kh = {0, 0, 0, 0, 0, 0, 0, 0}, kl = kh, vh = kh, vl = kh;
       if (key < N) {
         const int64_t off = (row0 + key) * ld + h * HD + ch * 8;
-        load8_split<SPLIT>(qkv, off + C, kh, kl);
-        load8_split<SPLIT>(qkv, off + 2 * C, vh, vl);
+        load8_split<P>(qkv, off + C, kh, kl);
+        load8_split<P>(qkv, off + 2 * C, vh, vl);
       }
       *reinterpret_cast<bf16x8*>(&Ks[0][kr * KS + ch * 8]) = kh;
       if (SPLIT) *reinterpret_cast<bf16x8*>(&Ks[NB - 1][kr * KS + ch * 8]) = kl;
@@ -153,10 +156,10 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
         const bf16x4 a = *reinterpret_cast<const bf16x4*>(&Ks[0][ko]);
         if (SPLIT) {
           const bf16x4 al = *reinterpret_cast<const bf16x4*>(&Ks[NB - 1][ko]);
-          s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, qf[c], s[kt], 0, 0, 0);
-          s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, qfl[c], s[kt], 0, 0, 0);
+          s[kt] = mma16<P>(al, qf[c], s[kt]);
+          s[kt] = mma16<P>(a, qfl[c], s[kt]);
         }
-        s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, qf[c], s[kt], 0, 0, 0);
+        s[kt] = mma16<P>(a, qf[c], s[kt]);
       }
     }
     // scale + relative-position bias (log2 domain), key mask
@@ -199,9 +202,9 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
       for (int i = 0; i < 4; ++i) {
         const float p = exp2f(s[kt][i] - mnew);
         psum += p;
-        const uint16_t ph = f2bf(p);
+        const uint16_t ph = op_cvt<P>(p);
         pf[kt][i] = (short)ph;
-        pfl[kt][i] = SPLIT ? (short)f2bf(p - bf2f(ph)) : (short)0;
+        pfl[kt][i] = op_lo<P>(p, ph);
       }
     }
     lrun = lrun * alpha + psum;
@@ -214,10 +217,10 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
         const bf16x4 a = *reinterpret_cast<const bf16x4*>(&Vt[0][vo]);
         if (SPLIT) {
           const bf16x4 al = *reinterpret_cast<const bf16x4*>(&Vt[NB - 1][vo]);
-          o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, pf[kt], o[c], 0, 0, 0);
-          o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pfl[kt], o[c], 0, 0, 0);
+          o[c] = mma16<P>(al, pf[kt], o[c]);
+          o[c] = mma16<P>(a, pfl[kt], o[c]);
         }
-        o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pf[kt], o[c], 0, 0, 0);
+        o[c] = mma16<P>(a, pf[kt], o[c]);
       }
     }
   }
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
     const int64_t off = (row0 + q) * C + h * HD + g4;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      if (SPLIT) {
+      if (store32(P)) {
         *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off + c * 16) = o[c] * inv;
       } else {
         bf16x4 r;
@@ -250,12 +253,13 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
 // 2 barriers + exposed bias loads of attn_core_kernel left the waves waiting on memory 57% of
 // their cycles).  V is stored [key/4][hd][4 keys], so the staging writes 4 keys per
 // ds_write_b64 and the PV A fragment (4 consecutive keys of one hd) is one ds_read_b64.
-template <int HD, bool SPLIT>
+template <int HD, int P>
 __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict__ qkv,
                                                           const float* __restrict__ bias,
                                                           void* __restrict__ out,
                                                           float* __restrict__ lse, int N,
                                                           int heads, float scale_log2) {
+  constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   constexpr int NC = HD / 16;
   constexpr int KT = 64, NKT = KT / 16;
   constexpr int KS = HD + 4;
@@ -280,7 +284,7 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
   for (int it = tid; it < NP * (HD / 8); it += 256) {
     const int kr = it / (HD / 8), ch = it % (HD / 8);
     bf16x8 kh = {0, 0, 0, 0, 0, 0, 0, 0}, kl = kh;
-    if (kr < N) load8_split<SPLIT>(qkv, (row0 + kr) * ld + C + h * HD + ch * 8, kh, kl);
+    if (kr < N) load8_split<P>(qkv, (row0 + kr) * ld + C + h * HD + ch * 8, kh, kl);
     *reinterpret_cast<bf16x8*>(Ks + (size_t)kr * KS + ch * 8) = kh;
     if (SPLIT) *reinterpret_cast<bf16x8*>(Ks + (size_t)(NP + kr) * KS + ch * 8) = kl;
   }
@@ -292,7 +296,7 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
       vh[r] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       vl[r] = vh[r];
       const int key = 4 * k4 + r;
-      if (key < N) load8_split<SPLIT>(qkv, (row0 + key) * ld + 2 * C + h * HD + ch * 8, vh[r], vl[r]);
+      if (key < N) load8_split<P>(qkv, (row0 + key) * ld + 2 * C + h * HD + ch * 8, vh[r], vl[r]);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -312,13 +316,13 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
     qfl[c] = bf16x4{0, 0, 0, 0};
     if (!qv) continue;
     const int64_t off = (row0 + q) * ld + h * HD + c * 16 + g4;
-    if (SPLIT) {
+    if (store32(P)) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(qkv) + off);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint16_t hh = f2bf(v[j]);
+        const uint16_t hh = op_cvt<P>(v[j]);
         qf[c][j] = (short)hh;
-        qfl[c][j] = (short)f2bf(v[j] - bf2f(hh));
+        qfl[c][j] = op_lo<P>(v[j], hh);
       }
     } else {
       qf[c] = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const uint16_t*>(qkv) + off);
@@ -362,10 +366,10 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
         const bf16x4 a = *reinterpret_cast<const bf16x4*>(Ks + ko);
         if (SPLIT) {
           const bf16x4 al = *reinterpret_cast<const bf16x4*>(Ks + (size_t)NP * KS + ko);
-          s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, qf[c], s[kt], 0, 0, 0);
-          s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, qfl[c], s[kt], 0, 0, 0);
+          s[kt] = mma16<P>(al, qf[c], s[kt]);
+          s[kt] = mma16<P>(a, qfl[c], s[kt]);
         }
-        s[kt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, qf[c], s[kt], 0, 0, 0);
+        s[kt] = mma16<P>(a, qf[c], s[kt]);
       }
     }
     float tmax = -INFINITY;
@@ -393,9 +397,9 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
       for (int i = 0; i < 4; ++i) {
         const float p = exp2f(s[kt][i] - mnew);
         psum += p;
-        const uint16_t ph = f2bf(p);
+        const uint16_t ph = op_cvt<P>(p);
         pf[kt][i] = (short)ph;
-        pfl[kt][i] = SPLIT ? (short)f2bf(p - bf2f(ph)) : (short)0;
+        pfl[kt][i] = op_lo<P>(p, ph);
       }
     }
     lrun = lrun * alpha + psum;
@@ -408,10 +412,10 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
         const bf16x4 a = *reinterpret_cast<const bf16x4*>(Vq + vo);
         if (SPLIT) {
           const bf16x4 al = *reinterpret_cast<const bf16x4*>(Vq + (size_t)NP * HD + vo);
-          o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, pf[kt], o[c], 0, 0, 0);
-          o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pfl[kt], o[c], 0, 0, 0);
+          o[c] = mma16<P>(al, pf[kt], o[c]);
+          o[c] = mma16<P>(a, pfl[kt], o[c]);
         }
-        o[c] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pf[kt], o[c], 0, 0, 0);
+        o[c] = mma16<P>(a, pf[kt], o[c]);
       }
     }
   }
@@ -423,7 +427,7 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
     const int64_t off = (row0 + q) * C + h * HD + g4;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      if (SPLIT) {
+      if (store32(P)) {
         *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off + c * 16) = o[c] * inv;
       } else {
         bf16x4 r;
@@ -447,11 +451,12 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
 //                 by reading V at the same keys), x3 for the split.
 // The bias index is the reference's formula (attention.py:40-56, Q2 depth stride 3 ws - 1)
 // with the key part reduced to per-tile constants: a 64-key tile is one z slice of the window.
-template <bool SPLIT>
+template <int P>
 __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict__ qkv,
                                                           const float* __restrict__ table,
                                                           void* __restrict__ out, int heads,
                                                           int qsplit, float scale_log2) {
+  constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   constexpr int N = 512, HD = 16;
   constexpr int TBLN = 547;      // reachable rows of the (15^3, heads) table under Q2
   constexpr int KS = 40;         // K row: hi[16] | lo[16] | pad (80 B: conflict-free b128)
@@ -471,7 +476,7 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
   for (int it = tid; it < N * 2; it += 512) {  // K: (key, 8-value chunk)
     const int key = it >> 1, ch = it & 1;
     bf16x8 hi = z8, lo = z8;
-    load8_split<SPLIT>(qkv, (row0 + key) * ld + C + h * HD + ch * 8, hi, lo);
+    load8_split<P>(qkv, (row0 + key) * ld + C + h * HD + ch * 8, hi, lo);
     *reinterpret_cast<bf16x8*>(&Ks[key * KS + ch * 8]) = hi;
     *reinterpret_cast<bf16x8*>(&Ks[key * KS + 16 + ch * 8]) = SPLIT ? lo : z8;
   }
@@ -482,7 +487,7 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
     for (int r = 0; r < 4; ++r) {
       vh[r] = z8;
       vl[r] = z8;
-      load8_split<SPLIT>(qkv, (row0 + 4 * k4 + r) * ld + 2 * C + h * HD + ch * 8, vh[r], vl[r]);
+      load8_split<P>(qkv, (row0 + 4 * k4 + r) * ld + 2 * C + h * HD + ch * 8, vh[r], vl[r]);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
     bf16x8 b1 = z8, b2 = z8;
     {
       bf16x8 hi = z8, lo = z8;
-      load8_split<SPLIT>(qkv, (row0 + q) * ld + h * HD + 8 * (g4 & 1), hi, lo);
+      load8_split<P>(qkv, (row0 + q) * ld + h * HD + 8 * (g4 & 1), hi, lo);
       b1 = hi;
       b2 = (SPLIT && g4 < 2) ? lo : z8;
     }
@@ -515,8 +520,8 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ks[(t * 64 + kt * 16 + l15) * KS + 8 * g4]);
-        s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        if (SPLIT) s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b2, s[kt], 0, 0, 0);
+        s[kt] = mma32<P>(a, b1, f32x4{0.f, 0.f, 0.f, 0.f});
+        if (SPLIT) s[kt] = mma32<P>(a, b2, s[kt]);
       }
       float tmax = -INFINITY;
 #pragma unroll
@@ -541,9 +546,9 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
         for (int i = 0; i < 4; ++i) {
           const float p = exp2f(s[kt][i] - mnew);
           psum += p;
-          const uint16_t hb = f2bf(p);
+          const uint16_t hb = op_cvt<P>(p);
           ph[kt][i] = (short)hb;
-          pl[kt][i] = SPLIT ? (short)f2bf(p - bf2f(hb)) : (short)0;
+          pl[kt][i] = op_lo<P>(p, hb);
         }
       }
       lrun = lrun * alpha + psum;
@@ -564,17 +569,17 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
           const bf16x4 w1 = *reinterpret_cast<const bf16x4*>(&Vq[VQ + o1]);
           const bf16x4 w2 = *reinterpret_cast<const bf16x4*>(&Vq[VQ + o2]);
           const bf16x8 vl = bf16x8{w1[0], w1[1], w1[2], w1[3], w2[0], w2[1], w2[2], w2[3]};
-          o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, pb, o, 0, 0, 0);
-          o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, plb, o, 0, 0, 0);
+          o = mma32<P>(vl, pb, o);
+          o = mma32<P>(vh, plb, o);
         }
-        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, pb, o, 0, 0, 0);
+        o = mma32<P>(vh, pb, o);
       }
     }
     lrun += __shfl_xor(lrun, 16, 64);
     lrun += __shfl_xor(lrun, 32, 64);
     const float inv = 1.f / lrun;
     const int64_t off = (row0 + q) * C + h * HD + 4 * g4;
-    if (SPLIT) {
+    if (store32(P)) {
       *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off) = o * inv;
     } else {
       bf16x4 r;
@@ -599,6 +604,8 @@ int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, 
   dim3 grid((unsigned)nblk);  // 1-D, decoded XCD-aware by attn_block
   const float sl2 = scale * 1.4426950408889634f;
   const bool split = prec == PREC_SPLIT;
+  const bool f16 = prec == PREC_FP16;
+  if (!valid_prec(prec)) return fail(WF_E_SHAPE, "attention: unknown precision");
   if (table_ws) {  // bias = the (T, heads) table; index from the coordinates
     if (table_ws != 8 || hd != 16 || N != 512)
       return fail(WF_E_SHAPE, "attention (table bias): implemented for ws = 8, head_dim = 16");
@@ -609,50 +616,37 @@ int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, 
       const int64_t wh = Bw * heads;
       const int qsplit = wh >= 512 ? 1 : (wh >= 256 ? 2 : 4);
       const dim3 g1((unsigned)(wh * qsplit));
-      if (split)
-        hipLaunchKernelGGL(attn_tbl_kernel<true>, g1, dim3(512), 0, s, qkv, bias, out, heads,
-                           qsplit, sl2);
-      else
-        hipLaunchKernelGGL(attn_tbl_kernel<false>, g1, dim3(512), 0, s, qkv, bias, out, heads,
-                           qsplit, sl2);
+      auto k = split ? attn_tbl_kernel<PREC_SPLIT>
+                     : (f16 ? attn_tbl_kernel<PREC_FP16> : attn_tbl_kernel<PREC_BF16>);
+      hipLaunchKernelGGL(k, g1, dim3(512), 0, s, qkv, bias, out, heads, qsplit, sl2);
       return check_launch("attention core (table bias, window per workgroup)");
     }
-    if (split)
-      hipLaunchKernelGGL((attn_core_kernel<16, 64, true, 8>), grid, dim3(256), 0, s, qkv, bias,
-                         out, lse, N, heads, sl2);
-    else
-      hipLaunchKernelGGL((attn_core_kernel<16, 64, false, 8>), grid, dim3(256), 0, s, qkv, bias,
-                         out, lse, N, heads, sl2);
+    auto k = split ? attn_core_kernel<16, 64, PREC_SPLIT, 8>
+                   : (f16 ? attn_core_kernel<16, 64, PREC_FP16, 8>
+                          : attn_core_kernel<16, 64, PREC_BF16, 8>);
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, s, qkv, bias, out, lse, N, heads, sl2);
     return check_launch("attention core (table bias)");
   }
   // the window-resident variant measured slower (236 vs 186 us on the stage-1 launch: its
   // 74 KB of LDS leaves 2 workgroups per CU, the tiled kernel's occupancy hides more latency;
   // hoisting the tiled kernel's bias loads over its staging cost occupancy too: 206 us); opt-in
   static const bool use_win = getenv("WF_ATTN_WIN") != nullptr;
-  if (use_win && hd == 16 && attn_win_lds(N, hd, split) <= 80 * 1024) {
+  if (use_win && !f16 && hd == 16 && attn_win_lds(N, hd, split) <= 80 * 1024) {
     const size_t lds = attn_win_lds(N, hd, split);
-    if (split) {
-      auto k = attn_win_kernel<16, true>;
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, qkv, bias, out, lse, N, heads, sl2);
-    } else {
-      auto k = attn_win_kernel<16, false>;
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, qkv, bias, out, lse, N, heads, sl2);
-    }
+    auto k = split ? attn_win_kernel<16, PREC_SPLIT> : attn_win_kernel<16, PREC_BF16>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k, grid, dim3(256), lds, s, qkv, bias, out, lse, N, heads, sl2);
     return check_launch("attention core (window-resident)");
   }
 #define WF_ATTN_CASE(HDV)                                                                  \
-  case HDV:                                                                                \
-    if (split)                                                                             \
-      hipLaunchKernelGGL((attn_core_kernel<HDV, (HDV >= 192 ? 32 : 64), true>), grid,      \
-                         dim3(256), 0, s, qkv, bias, out, lse, N, heads, sl2);             \
-    else                                                                                   \
-      hipLaunchKernelGGL((attn_core_kernel<HDV, 64, false>), grid, dim3(256), 0, s, qkv,   \
-                         bias, out, lse, N, heads, sl2);                                   \
-    break;
+  case HDV: {                                                                              \
+    auto k = split ? attn_core_kernel<HDV, (HDV >= 192 ? 32 : 64), PREC_SPLIT>             \
+                   : (f16 ? attn_core_kernel<HDV, 64, PREC_FP16>                           \
+                          : attn_core_kernel<HDV, 64, PREC_BF16>);                         \
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, s, qkv, bias, out, lse, N, heads, sl2);      \
+    break;                                                                                 \
+  }
   switch (hd) {
     WF_ATTN_CASE(16)
     WF_ATTN_CASE(32)
@@ -677,7 +671,7 @@ __global__ void rel_pos_bias_kernel(const float* __restrict__ table, const int64
   for (int h = 0; h < heads; ++h) bias[h * NN + i] = table[r * heads + h];
 }
 
-static int64_t act_bytes(int prec) { return prec == PREC_SPLIT ? 4 : 2; }
+static int64_t act_bytes(int prec) { return store32(prec) ? 4 : 2; }
 
 }  // namespace wf
 
@@ -715,7 +709,7 @@ static int window_attention_impl(const float* x, const float* ln_w, const float*
   WF_REQUIRE(ws >= 1 && D1 % ws == 0 && H1 % ws == 0 && W1 % ws == 0,
              "the raster must tile into ws^3 windows (window_partition, wave_helper.py:459)");
   WF_REQUIRE(heads >= 1 && C % heads == 0, "dim must be divisible by num_heads");
-  WF_REQUIRE(precision == PREC_BF16 || precision == PREC_SPLIT, "unknown precision");
+  WF_REQUIRE(valid_prec(precision), "unknown precision");
   WF_REQUIRE_PTR(x);
   WF_REQUIRE_PTR(wqkv_bf16x2);
   WF_REQUIRE_PTR(bias);
@@ -730,7 +724,7 @@ static int window_attention_impl(const float* x, const float* ln_w, const float*
   hipStream_t s = (hipStream_t)stream;
   void* qkv = workspace;
   void* ao = reinterpret_cast<char*>(workspace) + (((rows * 3 * C * e) + 255) & ~(int64_t)255);
-  const int obf = precision == PREC_BF16;
+  const int obf = !store32(precision);
   // 1. qkv = Linear(window_partition(norm1?(x)))
   GemmArgs g{};
   g.prec = precision;

@@ -49,8 +49,9 @@ struct Conv3Args {
                       // InstanceNorm statistics of the output, fused into the epilogue
 };
 
-template <int CO_T, int NT, bool SPLIT>
+template <int CO_T, int NT, int P>
 __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
+  constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   constexpr int TX = 16 * NT, TY = 4, HX = TX + 2, HY = TY + 2;
   constexpr int NPOS = 3 * HY * HX;
   constexpr int PS = kConvCC;                       // bf16 per position per plane
@@ -160,9 +161,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
       bf16x4 h, l;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const uint16_t hb = f2bf(v[e]);
+        const uint16_t hb = op_cvt<P>(v[e]);
         h[e] = (short)hb;
-        l[e] = SPLIT ? (short)f2bf(v[e] - bf2f(hb)) : (short)0;
+        l[e] = op_lo<P>(v[e], hb);
       }
       *reinterpret_cast<bf16x4*>(s_hi + pos * PS + 4 * q) = h;
       if (SPLIT) *reinterpret_cast<bf16x4*>(s_lo + pos * PS + 4 * q) = l;
@@ -205,10 +206,10 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
 #pragma unroll
         for (int m = 0; m < CO_T; ++m) {
           if (SPLIT) {
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[m], bl[n], acc[m][n], 0, 0, 0);
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[m], bh[n], acc[m][n], 0, 0, 0);
+            acc[m][n] = mma32<P>(wh[m], bl[n], acc[m][n]);
+            acc[m][n] = mma32<P>(wl[m], bh[n], acc[m][n]);
           }
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[m], bh[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = mma32<P>(wh[m], bh[n], acc[m][n]);
         }
       }
       // keep the next step's fragment reads from being hoisted over these MFMAs (VGPRs: the
@@ -320,13 +321,10 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   }
   dim3 grid((unsigned)a.nblocks, (unsigned)(a.Cout / (16 * CO_T)), (unsigned)a.ksplit);
   const bool post_stats = a.stats && a.ksplit > 1;  // partial outputs: a separate pass below
-  if (prec == PREC_SPLIT) {
-    auto kern = conv3d_k3_kernel<CO_T, NT, true>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
-  } else {
-    auto kern = conv3d_k3_kernel<CO_T, NT, false>;
+  {
+    auto kern = prec == PREC_SPLIT  ? conv3d_k3_kernel<CO_T, NT, PREC_SPLIT>
+                : prec == PREC_FP16 ? conv3d_k3_kernel<CO_T, NT, PREC_FP16>
+                                    : conv3d_k3_kernel<CO_T, NT, PREC_BF16>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
@@ -350,7 +348,7 @@ namespace wf {
 // e = j % 8 for K index kk = 32 ss + j of K-step gs = ch * KS + ss: tap kk / CC, input channel
 // CC ch + kk % CC -- each 16 x 32 MFMA A fragment is 1 KB contiguous, in lane order
 __global__ void conv3d_k3_pack_kernel(const float* __restrict__ w, uint16_t* __restrict__ packed,
-                                      int Cin, int Cout, int64_t total) {
+                                      int Cin, int Cout, int64_t total, int f16) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int e = (int)(i & 7), ln = (int)((i >> 3) & 63);
@@ -365,20 +363,34 @@ __global__ void conv3d_k3_pack_kernel(const float* __restrict__ w, uint16_t* __r
   const int kk = 32 * ss + j;
   const int tap = kk / kConvCC, ci = ch * kConvCC + kk % kConvCC;
   const float v = (tap < 27 && ci < Cin) ? w[((int64_t)co * Cin + ci) * 27 + tap] : 0.f;
+  if (f16) {  // WF_PREC_FP16: plane 0 = fp16(w), plane 1 unused
+    packed[i] = plane ? (uint16_t)0 : f2h(v);
+    return;
+  }
   const uint16_t h = f2bf(v);
   packed[i] = plane ? f2bf(v - bf2f(h)) : h;
 }
 }  // namespace wf
 
-extern "C" int wf_conv3d_k3_pack(const float* w, uint16_t* packed, int64_t Cin, int64_t Cout,
-                                 void* stream) {
+static int conv_pack(const float* w, uint16_t* packed, int64_t Cin, int64_t Cout, int f16,
+                     void* stream) {
   WF_REQUIRE(Cin >= 1 && Cout >= 16 && Cout % 16 == 0, "Cout must be a multiple of 16");
   WF_REQUIRE_PTR(w);
   WF_REQUIRE_PTR(packed);
   const int64_t total = wf_conv3d_k3_packed_elems(Cin, Cout);
   hipLaunchKernelGGL(conv3d_k3_pack_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
-                     (hipStream_t)stream, w, packed, (int)Cin, (int)Cout, total);
+                     (hipStream_t)stream, w, packed, (int)Cin, (int)Cout, total, f16);
   return check_launch("wf_conv3d_k3_pack");
+}
+
+extern "C" int wf_conv3d_k3_pack(const float* w, uint16_t* packed, int64_t Cin, int64_t Cout,
+                                 void* stream) {
+  return conv_pack(w, packed, Cin, Cout, 0, stream);
+}
+
+extern "C" int wf_conv3d_k3_pack_f16(const float* w, uint16_t* packed, int64_t Cin, int64_t Cout,
+                                     void* stream) {
+  return conv_pack(w, packed, Cin, Cout, 1, stream);
 }
 
 extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed,
@@ -392,7 +404,7 @@ extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_p
              "Cout must be a positive multiple of 16 with ldo >= Cout, ldo % 4 == 0");
   WF_REQUIRE(B * D * H * W < ((int64_t)1 << 31) && B * D * H * W * ldx < ((int64_t)1 << 32),
              "input too large (32-bit element offsets)");
-  WF_REQUIRE(precision == PREC_BF16 || precision == PREC_SPLIT, "unknown precision");
+  WF_REQUIRE(valid_prec(precision), "unknown precision");
   WF_REQUIRE_PTR(x);
   WF_REQUIRE_PTR(w_packed);
   WF_REQUIRE_PTR(out);

@@ -367,7 +367,7 @@ int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, f
   int ZS = D;
   while (ZS > 8 && base * cdiv(D, ZS) < 2048) ZS = (ZS + 1) / 2;
   const int64_t blocks = base * cdiv(D, ZS);
-  if (prec == PREC_SPLIT)
+  if (store32(prec))
     hipLaunchKernelGGL((dwconv3d_kernel<float>), dim3((unsigned)blocks), dim3(256), 0, s,
                        reinterpret_cast<const float*>(in), w, b, reinterpret_cast<float*>(out),
                        pstats, B, Hd, D, H, W, ZS);
@@ -413,7 +413,7 @@ int launch_dwconv_ln_gelu(const void* in, const float* w, const float* b, const 
   else if (tw_eff <= 8) tw_t = 8;
   const size_t lds = ((size_t)R * tw_t * (Hd + 4) + 2 * (size_t)R * tw_t) * 4;
   const int64_t blocks = (int64_t)B * D * cdiv(H, R) * cdiv(W, tw_t);
-  if (prec == PREC_SPLIT)
+  if (store32(prec))
     launch_dw<float>(tw_t, dim3((unsigned)blocks), dim3(threads), lds, s, in, w, b, ln_w, ln_b,
                      eps, out, B, Hd, D, H, W, R);
   else
@@ -429,7 +429,7 @@ using namespace wf;
 extern "C" int64_t wf_ccf_ffn_workspace_bytes(int64_t B, int64_t C, int64_t hidden, int64_t D,
                                               int64_t H, int64_t W, int precision) {
   (void)C;
-  const int64_t e = precision == PREC_SPLIT ? 4 : 2;
+  const int64_t e = store32(precision) ? 4 : 2;
   const int64_t one = ((B * D * H * W * hidden * e) + 255) & ~(int64_t)255;
   // + the dwconv's per-32-channel-group {mean, M2} of every position (LN2 in the fc loader)
   const int64_t st = B * D * H * W * (hidden / DW_STAT_GROUP) * 2 * 4;
@@ -452,7 +452,7 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   WF_REQUIRE(stage >= 0 && stage <= 3, "stage must be 0 (all), 1 (pwconv), 2 (dwconv) or 3 (fc)");
   WF_REQUIRE(B >= 1 && D >= 1 && H >= 1 && W >= 1, "empty volume");
   WF_REQUIRE(C % 8 == 0 && hidden % 8 == 0, "C and hidden must be multiples of 8");
-  WF_REQUIRE(precision == PREC_BF16 || precision == PREC_SPLIT, "unknown precision");
+  WF_REQUIRE(valid_prec(precision), "unknown precision");
   WF_REQUIRE_PTR(xh);
   WF_REQUIRE_PTR(pw_bf16x2);
   WF_REQUIRE_PTR(ln1_w);
@@ -470,11 +470,11 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   }
   hipStream_t s = (hipStream_t)stream;
   const int64_t M = B * D * H * W;
-  const int64_t e = precision == PREC_SPLIT ? 4 : 2;
+  const int64_t e = store32(precision) ? 4 : 2;
   const int64_t one = ((M * hidden * e) + 255) & ~(int64_t)255;
   void* h1 = workspace;
   void* h2 = reinterpret_cast<char*>(workspace) + one;
-  const int hbf = precision == PREC_BF16;
+  const int hbf = !store32(precision);
 
   GemmArgs g{};
   g.prec = precision;
@@ -505,7 +505,7 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   // the full weight per 16 rows (measured 107 / 145 us per launch at B = 4).  Instead: the
   // K-chunked GEMM with a plain bias epilogue, then one in-place LayerNorm + GELU row pass.
   static const bool no_split_ln1 = getenv("WF_FFN_NO_SPLIT_LN1") != nullptr;
-  const bool split_ln1 = !no_split_ln1 && precision == PREC_SPLIT && hidden >= 768 &&
+  const bool split_ln1 = !no_split_ln1 && store32(precision) && hidden >= 768 &&
                          hidden <= 1536;
   // C = 48 / hidden = 192 (stage 1), opt-in (WF_FFN_FUSED=1): the whole FFN in one kernel
   // (ffn_fused.hip), h1 and h2 stay on chip; stage 2 is that kernel, stages 1 and 3 are part
@@ -648,7 +648,7 @@ extern "C" int wf_patch_merging_fwd(const float* x, const float* ln_w, const flo
   WF_REQUIRE(B >= 1 && C % 8 == 0 && C >= 8, "C must be a positive multiple of 8");
   WF_REQUIRE(D % 2 == 0 && H % 2 == 0 && W % 2 == 0 && D >= 2 && H >= 2 && W >= 2,
              "odd sizes (the F.pad branch, wave_helper.py:180-182) are not supported");
-  WF_REQUIRE(precision == PREC_BF16 || precision == PREC_SPLIT, "unknown precision");
+  WF_REQUIRE(valid_prec(precision), "unknown precision");
   WF_REQUIRE_PTR(x);
   WF_REQUIRE_PTR(ln_w);
   WF_REQUIRE_PTR(ln_b);

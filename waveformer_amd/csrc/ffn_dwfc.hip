@@ -74,8 +74,9 @@ struct H1Load<uint16_t> {
   }
 };
 
-template <int C, int HID, int TY, int TX, bool SPLIT, typename T>
+template <int C, int HID, int TY, int TX, int P, typename T>
 __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_kernel(DwFcArgs a) {
+  constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   typedef DwFcCfg<C, HID, TY, TX> K;
   typedef H1Load<T> L;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -213,12 +214,12 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
     float* nxt = planes + ((p - z0) & 1) * K::PLANE_F;
     // ---- scatter plane p into output planes p+1 (kz 0), p (kz 1), p-1 (kz 2)
     {
-      const float* P = cur + xi * HID + 2 * cp;
+      const float* Pin = cur + xi * HID + 2 * cp;
 #pragma unroll
       for (int r = 0; r < K::PY; ++r) {
-        const f32x2 v0 = *reinterpret_cast<const f32x2*>(P + (r * K::PX + 0) * HID);
-        const f32x2 v1 = *reinterpret_cast<const f32x2*>(P + (r * K::PX + 1) * HID);
-        const f32x2 v2 = *reinterpret_cast<const f32x2*>(P + (r * K::PX + 2) * HID);
+        const f32x2 v0 = *reinterpret_cast<const f32x2*>(Pin + (r * K::PX + 0) * HID);
+        const f32x2 v1 = *reinterpret_cast<const f32x2*>(Pin + (r * K::PX + 1) * HID);
+        const f32x2 v2 = *reinterpret_cast<const f32x2*>(Pin + (r * K::PX + 2) * HID);
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
           const int o = r - ky;
@@ -299,9 +300,9 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
           bf16x4 hi4, lo4;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const uint16_t hb = f2bf(y[e]);
+            const uint16_t hb = op_cvt<P>(y[e]);
             hi4[e] = (short)hb;
-            lo4[e] = SPLIT ? (short)f2bf(y[e] - bf2f(hb)) : (short)0;
+            lo4[e] = op_lo<P>(y[e], hb);
           }
           *reinterpret_cast<bf16x4*>(rowh + c) = hi4;
           if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + c) = lo4;
@@ -330,10 +331,10 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
           if (SPLIT) {
             const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
             const bf16x8 wl = *reinterpret_cast<const bf16x8*>(Wh + C * K::WKP + k);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bl, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, bh, acc, 0, 0, 0);
+            acc = mma32<P>(wh, bl, acc);
+            acc = mma32<P>(wl, bh, acc);
           }
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bh, acc, 0, 0, 0);
+          acc = mma32<P>(wh, bh, acc);
         }
         // ---- epilogue: bias + Q4 residual, 16-byte store
         f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
@@ -369,8 +370,9 @@ static int go_dwfc(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks) {
   while (ZS > 8 && base * cdiv(g.D, ZS) < min_blocks) ZS = (ZS + 1) / 2;
   g.ZS = ZS;
   const int64_t blocks = base * cdiv(g.D, ZS);
-  void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_dwfc_kernel<C, HID, TY, TX, true, float>
-                                              : ffn_dwfc_kernel<C, HID, TY, TX, false, uint16_t>;
+  void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_dwfc_kernel<C, HID, TY, TX, PREC_SPLIT, float>
+                           : prec == PREC_FP16 ? ffn_dwfc_kernel<C, HID, TY, TX, PREC_FP16, float>
+                                               : ffn_dwfc_kernel<C, HID, TY, TX, PREC_BF16, uint16_t>;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::LDS_BYTES);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(K::NTH), K::LDS_BYTES, s, g);

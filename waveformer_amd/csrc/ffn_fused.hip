@@ -57,8 +57,9 @@ static_assert(NPOS * LN_LANES <= NTH, "LN2 lanes");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 }  // namespace ff
 
-template <bool SPLIT>
+template <int P>
 __global__ __launch_bounds__(ff::NTH, 1) void ffn_fused_kernel(DwFcArgs a) {
+  constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   using namespace ff;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* u1 = lds;                                                 // [PP][HS]
@@ -184,9 +185,9 @@ __global__ __launch_bounds__(ff::NTH, 1) void ffn_fused_kernel(DwFcArgs a) {
       const f32x4 n = (u - smu) * srs * w4 + b4;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const uint16_t hb = f2bf(n[e]);
+        const uint16_t hb = op_cvt<P>(n[e]);
         bh[ks][e] = (short)hb;
-        bl[ks][e] = SPLIT ? (short)f2bf(n[e] - bf2f(hb)) : (short)0;
+        bl[ks][e] = op_lo<P>(n[e], hb);
       }
     }
 #pragma unroll
@@ -199,10 +200,10 @@ __global__ __launch_bounds__(ff::NTH, 1) void ffn_fused_kernel(DwFcArgs a) {
         const bf16x4 wh = *reinterpret_cast<const bf16x4*>(Wr + 16 * ks);
         if (SPLIT) {
           const bf16x4 wl = *reinterpret_cast<const bf16x4*>(Wr + HID * WK1 + 16 * ks);
-          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wh, bl[ks], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wl, bh[ks], c, 0, 0, 0);
+          c = mma16<P>(wh, bl[ks], c);
+          c = mma16<P>(wl, bh[ks], c);
         }
-        c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wh, bh[ks], c, 0, 0, 0);
+        c = mma16<P>(wh, bh[ks], c);
       }
       acc[j] = c + *reinterpret_cast<const f32x4*>(pwb + ct * 16 + lkc);
     }
@@ -297,12 +298,12 @@ __global__ __launch_bounds__(ff::NTH, 1) void ffn_fused_kernel(DwFcArgs a) {
   auto step = [&](int p, const f32x4& xr_c, const f32x2& es_c, f32x4& xr_n, f32x2& es_n) {
     // ---- S1: scatter plane p into output planes p+1 (kz 0), p (kz 1), p-1 (kz 2)
     if (!(a.dbg & 1)) {
-      const float* P = u1 + xi * HS + 2 * cp;
+      const float* Pin = u1 + xi * HS + 2 * cp;
 #pragma unroll
       for (int r = 0; r < PY; ++r) {
-        const f32x2 v0 = *reinterpret_cast<const f32x2*>(P + (r * PX + 0) * HS);
-        const f32x2 v1 = *reinterpret_cast<const f32x2*>(P + (r * PX + 1) * HS);
-        const f32x2 v2 = *reinterpret_cast<const f32x2*>(P + (r * PX + 2) * HS);
+        const f32x2 v0 = *reinterpret_cast<const f32x2*>(Pin + (r * PX + 0) * HS);
+        const f32x2 v1 = *reinterpret_cast<const f32x2*>(Pin + (r * PX + 1) * HS);
+        const f32x2 v2 = *reinterpret_cast<const f32x2*>(Pin + (r * PX + 2) * HS);
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
           const int o = r - ky;
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(ff::NTH, 1) void ffn_fused_kernel(DwFcArgs a) {
 #pragma unroll
       for (int o = 0; o < TY; ++o) {
         f32x2 h = accA[o] + bias2;
-        if (!SPLIT) {  // bf16 mode: h2 carries bf16 rounding like the staged path
+        if (P == PREC_BF16) {  // bf16 mode: h2 carries bf16 rounding like the staged path
           h.x = bf2f(f2bf(h.x));
           h.y = bf2f(f2bf(h.y));
         }
@@ -394,9 +395,9 @@ __global__ __launch_bounds__(ff::NTH, 1) void ffn_fused_kernel(DwFcArgs a) {
           bf16x4 hi4, lo4;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const uint16_t hb = f2bf(y[e]);
+            const uint16_t hb = op_cvt<P>(y[e]);
             hi4[e] = (short)hb;
-            lo4[e] = SPLIT ? (short)f2bf(y[e] - bf2f(hb)) : (short)0;
+            lo4[e] = op_lo<P>(y[e], hb);
           }
           *reinterpret_cast<bf16x4*>(rowh + c) = hi4;
           if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + c) = lo4;
@@ -417,10 +418,10 @@ __global__ __launch_bounds__(ff::NTH, 1) void ffn_fused_kernel(DwFcArgs a) {
         if (SPLIT) {
           const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
           const bf16x8 wl = *reinterpret_cast<const bf16x8*>(Wh + C * WKP + k);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bl, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, bh, acc, 0, 0, 0);
+          acc = mma32<P>(wh, bl, acc);
+          acc = mma32<P>(wl, bh, acc);
         }
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bh, acc, 0, 0, 0);
+        acc = mma32<P>(wh, bh, acc);
       }
       f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
       if (a.stats) {
@@ -458,7 +459,9 @@ int launch_ffn_fused(const DwFcArgs& a, int prec, hipStream_t s) {
   const char* dbg = getenv("WF_FFN_DBG");  // timing experiments: phases to skip (bit mask)
   g.dbg = dbg ? atoi(dbg) : 0;
   const int64_t blocks = base * cdiv(g.D, ZS);
-  void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_fused_kernel<true> : ffn_fused_kernel<false>;
+  void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_fused_kernel<PREC_SPLIT>
+                           : prec == PREC_FP16 ? ffn_fused_kernel<PREC_FP16>
+                                               : ffn_fused_kernel<PREC_BF16>;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTH), LDS_BYTES, s, g);

@@ -90,8 +90,9 @@ __device__ __forceinline__ float tpr_sum(float v) {
   return v;
 }
 
-template <int BM, bool SPLIT>
+template <int BM, int P>
 __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
+  constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TPR = 256 / BM;  // threads per row in row-assigned phases
   constexpr int MT = BM / 16;
@@ -185,9 +186,9 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const uint16_t hi = f2bf(v[j]);
+          const uint16_t hi = op_cvt<P>(v[j]);
           o[j] = (short)hi;
-          if (SPLIT) olo[j] = (short)f2bf(v[j] - bf2f(hi));
+          if (SPLIT) olo[j] = op_lo<P>(v[j], hi);
         }
       }
       *reinterpret_cast<bf16x8*>(A + (size_t)r * KP + ch * 8) = o;
@@ -226,10 +227,10 @@ __global__ __launch_bounds__(256) void gemm_ares_kernel(GemmArgs g) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + aoff);
         if (SPLIT) {
           const bf16x8 al = *reinterpret_cast<const bf16x8*>(Alo + aoff);
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, acc[mt], 0, 0, 0);
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[mt], 0, 0, 0);
+          acc[mt] = mma32<P>(al, b, acc[mt]);
+          acc[mt] = mma32<P>(a, bl, acc[mt]);
         }
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[mt], 0, 0, 0);
+        acc[mt] = mma32<P>(a, b, acc[mt]);
       }
     }
     if (nv) {
@@ -338,15 +339,21 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
   };
   if (split) {
     switch (BM) {
-      case 64: go(gemm_ares_kernel<64, true>); break;
-      case 32: go(gemm_ares_kernel<32, true>); break;
-      default: go(gemm_ares_kernel<16, true>); break;
+      case 64: go(gemm_ares_kernel<64, PREC_SPLIT>); break;
+      case 32: go(gemm_ares_kernel<32, PREC_SPLIT>); break;
+      default: go(gemm_ares_kernel<16, PREC_SPLIT>); break;
+    }
+  } else if (g.prec == PREC_FP16) {
+    switch (BM) {
+      case 64: go(gemm_ares_kernel<64, PREC_FP16>); break;
+      case 32: go(gemm_ares_kernel<32, PREC_FP16>); break;
+      default: go(gemm_ares_kernel<16, PREC_FP16>); break;
     }
   } else {
     switch (BM) {
-      case 64: go(gemm_ares_kernel<64, false>); break;
-      case 32: go(gemm_ares_kernel<32, false>); break;
-      default: go(gemm_ares_kernel<16, false>); break;
+      case 64: go(gemm_ares_kernel<64, PREC_BF16>); break;
+      case 32: go(gemm_ares_kernel<32, PREC_BF16>); break;
+      default: go(gemm_ares_kernel<16, PREC_BF16>); break;
     }
   }
   return check_launch(who);

@@ -30,9 +30,10 @@ struct KcCfg {
   static constexpr int WPT = (WITEMS + 255) / 256;  // per thread
 };
 
-template <int NT, bool SPLIT, int MAP, int EPI, bool ABF16>
+template <int NT, int P, int MAP, int EPI, bool ABF16>
 __global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
   typedef KcCfg<NT> C;
+  constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   constexpr int RT = C::RT, NC = C::NC, NPL = SPLIT ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) uint16_t Wl[];  // [2][NPL][NC][KC_KP]
   const int K = g.K, N = g.N;
@@ -207,9 +208,9 @@ __global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float x = kv ? v[rt][j] : 0.f;
-          const uint16_t h = f2bf(x);
+          const uint16_t h = op_cvt<P>(x);
           ah[rt][j] = (short)h;
-          al[rt][j] = SPLIT ? (short)f2bf(x - bf2f(h)) : (short)0;
+          al[rt][j] = op_lo<P>(x, h);
         }
       }
     }
@@ -222,13 +223,13 @@ __global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
         const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Wb + NC * KC_KP + wo);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
-          acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al[rt], acc[rt][t], 0, 0, 0);
-          acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah[rt], acc[rt][t], 0, 0, 0);
+          acc[rt][t] = mma32<P>(bh, al[rt], acc[rt][t]);
+          acc[rt][t] = mma32<P>(bl, ah[rt], acc[rt][t]);
         }
       }
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
-        acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah[rt], acc[rt][t], 0, 0, 0);
+        acc[rt][t] = mma32<P>(bh, ah[rt], acc[rt][t]);
       if (t % 4 == 3) __builtin_amdgcn_sched_barrier(0);
     }
     wcommit(buf ^ 1);
@@ -314,10 +315,14 @@ static void go_kc(const GemmArgs& g, hipStream_t s) {
   typedef KcCfg<NT> C;
   const bool split = g.prec == PREC_SPLIT;
   void (*kern)(GemmArgs);
-  if (g.a_bf16)
-    kern = split ? gemm_kc_kernel<NT, true, MAP, EPI, true> : gemm_kc_kernel<NT, false, MAP, EPI, true>;
+  if (g.a_bf16)  // bf16 activations only exist in PREC_BF16
+    kern = gemm_kc_kernel<NT, PREC_BF16, MAP, EPI, true>;
+  else if (split)
+    kern = gemm_kc_kernel<NT, PREC_SPLIT, MAP, EPI, false>;
+  else if (g.prec == PREC_FP16)
+    kern = gemm_kc_kernel<NT, PREC_FP16, MAP, EPI, false>;
   else
-    kern = split ? gemm_kc_kernel<NT, true, MAP, EPI, false> : gemm_kc_kernel<NT, false, MAP, EPI, false>;
+    kern = gemm_kc_kernel<NT, PREC_BF16, MAP, EPI, false>;
   const size_t lds = (size_t)2 * (split ? 2 : 1) * C::NC * KC_KP * 2 +
                      (g.a_ln != LN_NONE ? (size_t)2 * cdiv(g.K, KC_BK) * KC_BK * 4 : 0);
   if (lds > 64 * 1024)

@@ -7,7 +7,7 @@
 //     columns x K) in LDS once, then its 8 waves walk 16-row tiles of A persistently;
 //   * a wave loads its A fragments straight from global memory into registers (lane l: row
 //     l&15, k = 8*(l>>4) .. +7 of each 32-deep k step), applies the row gather / LayerNorm /
-//     bf16 hi-lo split on the fly, and issues NT v_mfma_f32_16x16x32_bf16 (x3 for PREC_SPLIT)
+//     bf16 hi-lo split on the fly, and issues NT v_mfma_f32_16x16x32_bf16 (x3 for PREC_SPLIT; the _f16 form for PREC_FP16)
 //     per k step against B fragments read from LDS with ds_read_b128;
 //   * the epilogue runs on the accumulators in registers (C layout: lane l holds rows
 //     4*(l>>4)+i, column l&15 of each 16-wide tile): bias, LayerNorm over the full row
@@ -20,8 +20,9 @@
 
 namespace wf {
 
-template <int NT, bool SPLIT, int MAP, int EPI, bool ABF16>
+template <int NT, int P, int MAP, int EPI, bool ABF16>
 __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
+  constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   extern __shared__ __attribute__((aligned(16))) uint16_t Wl[];  // [NB][NT*16][KP]
   const int K = g.K, N = g.N;
   const int M = (int)g.M;
@@ -166,9 +167,9 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float x = kv ? v[j] : 0.f;
-        const uint16_t h = f2bf(x);
+        const uint16_t h = op_cvt<P>(x);
         ah[j] = (short)h;
-        al[j] = SPLIT ? (short)f2bf(x - bf2f(h)) : (short)0;
+        al[j] = op_lo<P>(x, h);
       }
       // transposed product C^T = Wt . A^T: the weight fragment is the A operand (rows =
       // output channels), the activation fragment the B operand (columns = positions), so
@@ -179,10 +180,10 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
         const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Wl + wo);
         if (SPLIT) {
           const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Wl + NCOL * KP + wo);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc[t], 0, 0, 0);
+          acc[t] = mma32<P>(bh, al, acc[t]);
+          acc[t] = mma32<P>(bl, ah, acc[t]);
         }
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc[t], 0, 0, 0);
+        acc[t] = mma32<P>(bh, ah, acc[t]);
         // keep the LDS fragment reads from being hoisted all at once (VGPR pressure ->
         // occupancy): a scheduling fence every 3 tiles
         if (t % 3 == 2) __builtin_amdgcn_sched_barrier(0);
@@ -266,12 +267,15 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
 
 template <int NT, int MAP, int EPI>
 static void go_rows(const GemmArgs& g, dim3 grid, size_t lds, hipStream_t s) {
-  const bool split = g.prec == PREC_SPLIT;
   void (*kern)(GemmArgs);
-  if (g.a_bf16)
-    kern = split ? gemm_rows_kernel<NT, true, MAP, EPI, true> : gemm_rows_kernel<NT, false, MAP, EPI, true>;
+  if (g.a_bf16)  // bf16 activations only exist in PREC_BF16
+    kern = gemm_rows_kernel<NT, PREC_BF16, MAP, EPI, true>;
+  else if (g.prec == PREC_SPLIT)
+    kern = gemm_rows_kernel<NT, PREC_SPLIT, MAP, EPI, false>;
+  else if (g.prec == PREC_FP16)
+    kern = gemm_rows_kernel<NT, PREC_FP16, MAP, EPI, false>;
   else
-    kern = split ? gemm_rows_kernel<NT, true, MAP, EPI, false> : gemm_rows_kernel<NT, false, MAP, EPI, false>;
+    kern = gemm_rows_kernel<NT, PREC_BF16, MAP, EPI, false>;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

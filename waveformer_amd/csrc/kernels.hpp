@@ -10,7 +10,42 @@ namespace wf {
 //                 lo = bf16(x - hi); products use hi*hi + lo*hi + hi*lo (the lo*lo term is
 //                 below 2^-17 relative), i.e. fp32-faithful results on the bf16 MFMA pipes;
 //                 intermediates stay fp32.
-enum Prec { PREC_BF16 = 0, PREC_SPLIT = 1 };
+//   PREC_FP16  -- operands rounded to fp16 (10-bit mantissa), fp32 accumulation on the
+//                 v_mfma_f32_*_f16 pipes; intermediates stay fp32 like PREC_SPLIT (config 5).
+enum Prec { PREC_BF16 = 0, PREC_SPLIT = 1, PREC_FP16 = 2 };
+
+// ---- MFMA operand kinds (compile-time twin of Prec): conversion and matrix instruction
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+
+template <int P>
+__device__ __forceinline__ uint16_t op_cvt(float x) {  // the operand (hi part) of x
+  if constexpr (P == PREC_FP16) return f2h(x);
+  else return f2bf(x);
+}
+template <int P>
+__device__ __forceinline__ short op_lo(float x, uint16_t hi) {  // the split's lo part, else 0
+  if constexpr (P == PREC_SPLIT) return (short)f2bf(x - bf2f(hi));
+  else return (short)0;
+}
+template <int P>
+__device__ __forceinline__ f32x4 mma32(bf16x8 a, bf16x8 b, f32x4 c) {  // 16x16x32
+  if constexpr (P == PREC_FP16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <int P>
+__device__ __forceinline__ f32x4 mma16(bf16x4 a, bf16x4 b, f32x4 c) {  // 16x16x16
+  if constexpr (P == PREC_FP16)
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(f16x4, a),
+                                                 __builtin_bit_cast(f16x4, b), c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+// fp32 storage of the GEMM-to-GEMM intermediates (workspaces): every mode but PREC_BF16
+__host__ __device__ constexpr bool store32(int p) { return p != PREC_BF16; }
+inline bool valid_prec(int p) { return p == PREC_BF16 || p == PREC_SPLIT || p == PREC_FP16; }
 
 // ---- A-resident MFMA GEMM:  out[m, n] = epilogue( sum_k A[m, k] * Wt[n, k] ) -------------
 // A rows are produced by a loader (gather + optional LayerNorm + bf16 rounding) into LDS once

@@ -43,6 +43,7 @@ __global__ void split_f32_bf16x2_kernel(const float* __restrict__ in, uint16_t* 
 // Many weights in one launch: table = [n + 1] int64 element offsets (prefix sums), then n
 // source pointers, then n destination pointers, all in device memory.  Destination d of
 // weight s holds its [2][numel] {hi, lo} planes, as wf_split_f32_to_bf16x2 writes them.
+template <bool F16>
 __global__ void split_multi_kernel(const int64_t* __restrict__ table, int n, int64_t total) {
   const int64_t* pre = table;
   const float* const* src = reinterpret_cast<const float* const*>(table + n + 1);
@@ -56,9 +57,24 @@ __global__ void split_multi_kernel(const int64_t* __restrict__ table, int n, int
     }
     const int64_t j = i - pre[lo], m = pre[lo + 1] - pre[lo];
     const float v = src[lo][j];
-    const uint16_t h = f2bf(v);
-    dst[lo][j] = h;
-    dst[lo][m + j] = f2bf(v - bf2f(h));
+    if (F16) {
+      dst[lo][j] = f2h(v);
+      dst[lo][m + j] = 0;
+    } else {
+      const uint16_t h = f2bf(v);
+      dst[lo][j] = h;
+      dst[lo][m + j] = f2bf(v - bf2f(h));
+    }
+  }
+}
+
+__global__ void cast_f16x2_kernel(const float* __restrict__ in, uint16_t* __restrict__ out,
+                                  int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    out[i] = f2h(in[i]);
+    out[n + i] = 0;
   }
 }
 
@@ -66,16 +82,42 @@ __global__ void split_multi_kernel(const int64_t* __restrict__ table, int n, int
 
 extern "C" int wf_abi_version(void) { return WF_ABI_VERSION; }
 
-extern "C" int wf_split_f32_to_bf16x2_multi(const int64_t* table_dev, int64_t n, int64_t total,
-                                            void* stream) {
+static int split_multi(const int64_t* table_dev, int64_t n, int64_t total, void* stream,
+                       bool f16) {
   WF_REQUIRE(n >= 0 && total >= 0, "negative count");
   if (n == 0 || total == 0) return WF_OK;
   WF_REQUIRE_PTR(table_dev);
   int64_t blocks = wf::cdiv(total, 256);
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(wf::split_multi_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                     (hipStream_t)stream, table_dev, (int)n, total);
+  if (f16)
+    hipLaunchKernelGGL(wf::split_multi_kernel<true>, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, table_dev, (int)n, total);
+  else
+    hipLaunchKernelGGL(wf::split_multi_kernel<false>, dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, table_dev, (int)n, total);
   return wf::check_launch("wf_split_f32_to_bf16x2_multi");
+}
+
+extern "C" int wf_split_f32_to_bf16x2_multi(const int64_t* table_dev, int64_t n, int64_t total,
+                                            void* stream) {
+  return split_multi(table_dev, n, total, stream, false);
+}
+
+extern "C" int wf_cast_f32_to_f16x2_multi(const int64_t* table_dev, int64_t n, int64_t total,
+                                          void* stream) {
+  return split_multi(table_dev, n, total, stream, true);
+}
+
+extern "C" int wf_cast_f32_to_f16x2(const float* in, uint16_t* out, int64_t n, void* stream) {
+  WF_REQUIRE(n >= 0, "n < 0");
+  if (n == 0) return WF_OK;
+  WF_REQUIRE_PTR(in);
+  WF_REQUIRE_PTR(out);
+  int64_t blocks = wf::cdiv(n, 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(wf::cast_f16x2_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     (hipStream_t)stream, in, out, n);
+  return wf::check_launch("wf_cast_f32_to_f16x2");
 }
 
 extern "C" const char* wf_last_error(void) { return wf::g_last_error.c_str(); }
@@ -115,7 +157,7 @@ extern "C" int wf_linear_fwd(const float* x, const uint16_t* w_bf16x2, const flo
                              int precision, void* stream) {
   WF_REQUIRE(M >= 0 && K >= 8 && K % 8 == 0 && N >= 4 && N % 4 == 0,
              "need K a multiple of 8 and N a multiple of 4");
-  WF_REQUIRE(precision == PREC_BF16 || precision == PREC_SPLIT, "unknown precision");
+  WF_REQUIRE(valid_prec(precision), "unknown precision");
   WF_REQUIRE_PTR(x);
   WF_REQUIRE_PTR(w_bf16x2);
   WF_REQUIRE_PTR(out);

@@ -206,7 +206,7 @@ def window_attn(x: Tensor, ln_w: Optional[Tensor], ln_b: Optional[Tensor], eps: 
     B, D1, H1, W1, _ = x.shape
     N = ws ** 3
     bias = ops.rel_pos_bias(table.detach(), index)
-    wq, wp = ops.split_weight(wqkv), ops.split_weight(wproj)
+    wq, wp = ops.split_weight(wqkv, prec=SPLIT), ops.split_weight(wproj, prec=SPLIT)
     out = torch.empty_like(x)
     wsb = _lib.query("wf_window_attention_workspace_bytes", B, C, D1, H1, W1, SPLIT)
     work = torch.empty(wsb, dtype=torch.uint8, device=x.device)
@@ -396,8 +396,8 @@ def ccf_ffn(xh: Tensor, stats: Optional[Tensor], n2w: Optional[Tensor], n2b: Opt
         return out, _empty(xh)
     B, D, H, W, C = xh.shape
     hid = pww.shape[0]
-    pw = ops.split_weight(pww, (hid, C))
-    fc = ops.split_weight(fcw)
+    pw = ops.split_weight(pww, (hid, C), SPLIT)
+    fc = ops.split_weight(fcw, prec=SPLIT)
     out = torch.empty_like(xh)
     wsb = _lib.query("wf_ccf_ffn_workspace_bytes", B, C, hid, D, H, W, SPLIT)
     work = torch.empty(wsb, dtype=torch.uint8, device=xh.device)

@@ -47,7 +47,8 @@ def _check(t: torch.Tensor, name: str, dtype=torch.float32, contiguous=True) -> 
 # ------------------------------------------------------------------------------------------
 # precision of the MFMA operands (include/waveformer_hip.h, WF_PREC_*)
 # ------------------------------------------------------------------------------------------
-PRECISIONS = {"bf16": 0, "bf16x3": 1}
+PRECISIONS = {"bf16": 0, "bf16x3": 1, "fp16": 2}
+FP16 = PRECISIONS["fp16"]
 _precision = os.environ.get("WAVEFORMER_PRECISION", "bf16x3")
 if _precision not in PRECISIONS:
     raise ValueError(f"WAVEFORMER_PRECISION={_precision!r}: expected one of {sorted(PRECISIONS)}")
@@ -55,7 +56,9 @@ if _precision not in PRECISIONS:
 
 def set_precision(p: str) -> None:
     """'bf16x3' (default): fp32-faithful split-bf16 MFMA operands, fp32 intermediates.
-    'bf16': plain bf16 operands and bf16 GEMM-to-GEMM intermediates (fastest)."""
+    'bf16': plain bf16 operands and bf16 GEMM-to-GEMM intermediates (fastest).
+    'fp16': fp16 operands (10-bit mantissa) on the f16 MFMA pipes, fp32 intermediates
+    (config 5's fp16 MFMA path)."""
     global _precision
     if p not in PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {p!r}")
@@ -98,11 +101,13 @@ def prec_id() -> int:
 # too, so replays always see the current weights.
 # ------------------------------------------------------------------------------------------
 class WeightArena:
-    """The [2][numel] bf16 {hi, lo} planes of a list of fp32 CUDA weights in one buffer,
-    refreshed by one wf_split_f32_to_bf16x2_multi launch."""
+    """The [2][numel] 16-bit planes of a list of fp32 CUDA weights in one buffer -- bf16
+    {hi, lo} (f16=False) or {fp16, 0} (f16=True, WF_PREC_FP16) -- refreshed by one
+    wf_split_f32_to_bf16x2_multi / wf_cast_f32_to_f16x2_multi launch."""
 
-    def __init__(self, params: Sequence[torch.Tensor]):
+    def __init__(self, params: Sequence[torch.Tensor], f16: bool = False):
         dev = params[0].device
+        self.f16 = f16
         self.key = tuple((p.data_ptr(), p.numel()) for p in params)
         pre, dsts, off = [0], [], 0
         blocks = []
@@ -121,8 +126,8 @@ class WeightArena:
         self.table = torch.tensor(table, dtype=torch.int64).to(dev)
 
     def refresh(self) -> None:
-        _lib.call("wf_split_f32_to_bf16x2_multi", self.table.data_ptr(), self.n, self.total,
-                  _stream())
+        _lib.call("wf_cast_f32_to_f16x2_multi" if self.f16 else "wf_split_f32_to_bf16x2_multi",
+                  self.table.data_ptr(), self.n, self.total, _stream())
 
 
 class _Scope:
@@ -167,10 +172,18 @@ class weight_scope:
         arena = None
         params = split_params(self.module)
         if params:
-            arena = getattr(self.module, "_wf_arena", None)
+            # the operand format this forward's kernels read: fp16 for an fp16 inference
+            # forward, else bf16 hi / lo (training always runs fp32-faithful bf16x3)
+            train = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+            f16 = _precision == "fp16" and not train
+            arenas = getattr(self.module, "_wf_arenas", None)
+            if arenas is None:
+                arenas = {}
+                object.__setattr__(self.module, "_wf_arenas", arenas)
+            arena = arenas.get(f16)
             if arena is None or arena.key != tuple((p.data_ptr(), p.numel()) for p in params):
-                arena = WeightArena(params)
-                object.__setattr__(self.module, "_wf_arena", arena)
+                arena = WeightArena(params, f16)
+                arenas[f16] = arena
             arena.refresh()
         _scope = _Scope(arena)
         self.owner = True
@@ -193,11 +206,14 @@ def per_forward(key: tuple, make):
     return v
 
 
-def split_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None) -> torch.Tensor:
-    """[2][N][K] bf16 {hi, lo} planes of an fp32 weight (wf_split_f32_to_bf16x2): the weight
-    arena's view inside a weight_scope, else split now."""
+def split_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None,
+                 prec: Optional[int] = None) -> torch.Tensor:
+    """[2][N][K] 16-bit operand planes of an fp32 weight for kernels running at `prec`:
+    bf16 {hi, lo} (wf_split_f32_to_bf16x2), or {fp16, 0} for WF_PREC_FP16
+    (wf_cast_f32_to_f16x2).  The weight arena's view inside a weight_scope, else made now."""
     shp = (2,) + tuple(p.shape if shape is None else shape)
-    if _scope is not None and _scope.arena is not None:
+    f16 = (_prec() if prec is None else prec) == FP16
+    if _scope is not None and _scope.arena is not None and _scope.arena.f16 == f16:
         v = _scope.arena.views.get(p.data_ptr())
         if v is not None and v.numel() == 2 * p.numel():
             return v.view(shp)
@@ -205,11 +221,11 @@ def split_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None) -> to
     def make():
         src = p.detach()
         _check(src, "weight")
-        out = torch.empty(shp, dtype=torch.bfloat16, device=src.device)
-        _lib.call("wf_split_f32_to_bf16x2", src.data_ptr(), out.data_ptr(), src.numel(),
-                  _stream())
+        out = torch.empty(shp, dtype=torch.bfloat16, device=src.device)  # 16-bit words
+        _lib.call("wf_cast_f32_to_f16x2" if f16 else "wf_split_f32_to_bf16x2", src.data_ptr(),
+                  out.data_ptr(), src.numel(), _stream())
         return out
-    return per_forward(("split", p.data_ptr(), shp), make)
+    return per_forward(("split", p.data_ptr(), shp, f16), make)
 
 
 # ------------------------------------------------------------------------------------------
@@ -472,9 +488,12 @@ def empty_cl(B: int, C: int, D: int, H: int, W: int, device) -> torch.Tensor:
                        memory_format=torch.channels_last_3d)
 
 
-def conv3d_k3_packed(weight: torch.Tensor) -> torch.Tensor:
-    """[2][K-steps][Cout][32] bf16 hi / lo planes of a (Cout, Cin, 3, 3, 3) conv weight
-    (wf_conv3d_k3_pack), made once per weight_scope."""
+def conv3d_k3_packed(weight: torch.Tensor, prec: Optional[int] = None) -> torch.Tensor:
+    """[2][K-steps][Cout][32] 16-bit planes of a (Cout, Cin, 3, 3, 3) conv weight: bf16 hi /
+    lo (wf_conv3d_k3_pack), or fp16 for WF_PREC_FP16 (wf_conv3d_k3_pack_f16); made once per
+    weight_scope."""
+    f16 = (_prec() if prec is None else prec) == FP16
+
     def make():
         w = weight.detach()
         _check(w, "conv weight", contiguous=False)
@@ -482,9 +501,10 @@ def conv3d_k3_packed(weight: torch.Tensor) -> torch.Tensor:
         Cout, Cin = w.shape[:2]
         n = _lib.query("wf_conv3d_k3_packed_elems", Cin, Cout)
         out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
-        _lib.call("wf_conv3d_k3_pack", w.data_ptr(), out.data_ptr(), Cin, Cout, _stream())
+        _lib.call("wf_conv3d_k3_pack_f16" if f16 else "wf_conv3d_k3_pack", w.data_ptr(),
+                  out.data_ptr(), Cin, Cout, _stream())
         return out
-    return per_forward(("conv3", weight.data_ptr(), tuple(weight.shape)), make)
+    return per_forward(("conv3", weight.data_ptr(), tuple(weight.shape), f16), make)
 
 
 def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -509,8 +529,9 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor
     acc = None
     if norm_eps is not None:
         acc = torch.zeros((B, Cout, 2), dtype=torch.float64, device=x.device)
-    _lib.call("wf_conv3d_k3_fwd", x.data_ptr(), cl_ld(x), conv3d_k3_packed(weight).data_ptr(),
-              _ptr(bias), out.data_ptr(), ldo, _ptr(acc), B, Cin, Cout, D, H, W, _prec(),
+    prec = _prec()
+    _lib.call("wf_conv3d_k3_fwd", x.data_ptr(), cl_ld(x), conv3d_k3_packed(weight, prec).data_ptr(),
+              _ptr(bias), out.data_ptr(), ldo, _ptr(acc), B, Cin, Cout, D, H, W, prec,
               _stream())
     if acc is None:
         return out
@@ -569,11 +590,12 @@ def linear_rows(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Te
     N = weight.shape[0]
     w2 = weight.reshape(N, K)
     if cache:
-        wb = split_weight(weight, (N, K))
+        wb = split_weight(weight, (N, K), _prec())
     else:
         w2 = w2.contiguous()
         wb = torch.empty((2, N, K), dtype=torch.bfloat16, device=x2d.device)
-        _lib.call("wf_split_f32_to_bf16x2", w2.data_ptr(), wb.data_ptr(), w2.numel(), _stream())
+        _lib.call("wf_cast_f32_to_f16x2" if _prec() == FP16 else "wf_split_f32_to_bf16x2",
+                  w2.data_ptr(), wb.data_ptr(), w2.numel(), _stream())
     if bias is not None:
         _check(bias, "bias")
     out = torch.empty((M, N), dtype=torch.float32, device=x2d.device)
@@ -679,8 +701,9 @@ def window_attention(x_cl: torch.Tensor, wqkv: torch.Tensor, bqkv: Optional[torc
     reference's formula (wf_window_attention_fwd_table, ws 8 / head_dim 16)."""
     _check(x_cl, "x")
     B, D1, H1, W1, C = x_cl.shape
-    wq = split_weight(wqkv)
-    wp = split_weight(wproj)
+    prec = _prec() if prec is None else prec
+    wq = split_weight(wqkv, prec=prec)
+    wp = split_weight(wproj, prec=prec)
     if bqkv is not None:
         _check(bqkv, "qkv.bias")
     if bproj is not None:
@@ -759,9 +782,9 @@ def ccf_ffn_raw(xh, stats, n2w, n2b, pww, pwb, l1w, l1b, eps1, dww, dwb, l2w, l2
     _check(xh, "x")
     B, D, H, W, C = xh.shape
     hid = pww.shape[0]
-    pw = split_weight(pww, (hid, C))
-    fc = split_weight(fcw)
     prec = _prec() if prec is None else prec
+    pw = split_weight(pww, (hid, C), prec)
+    fc = split_weight(fcw, prec=prec)
     out = torch.empty_like(xh)
     wsb = _lib.query("wf_ccf_ffn_workspace_bytes", B, C, hid, D, H, W, prec)
     work = torch.empty(wsb, dtype=torch.uint8, device=xh.device)
@@ -803,7 +826,7 @@ def patch_merging(x_cl: torch.Tensor, norm: torch.nn.LayerNorm, reduction: torch
 def _patch_merging_raw(x_cl, ln_w, ln_b, eps, red_w, v2, prec) -> torch.Tensor:
     _check(x_cl, "x")
     B, D, H, W, C = x_cl.shape
-    red = split_weight(red_w)
+    red = split_weight(red_w, prec=prec)
     out = torch.empty((B, D // 2, H // 2, W // 2, 2 * C), dtype=torch.float32, device=x_cl.device)
     _lib.call("wf_patch_merging_fwd", x_cl.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
               float(eps), red.data_ptr(), int(bool(v2)), out.data_ptr(), B, C, D, H, W, prec,
