@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 9
+#define WF_ABI_VERSION 10
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
@@ -167,6 +167,21 @@ int wf_instnorm_finalize(const double* acc, float* stats, int64_t B, int64_t C, 
 int wf_norm_act_cl(const float* a, int64_t lda, const float* stats_a, const float* r, int64_t ldr,
                    const float* stats_r, float* out, int64_t ldo, int64_t B, int64_t C, int64_t P,
                    float slope, void* stream);
+
+/* HFRefinementRes (network_models/idwt_upsample.py:12-50, config 5) over the 7 detail
+ * tensors of one wavelet level: out_k = x_k * sigmoid(conv1x1(relu(IN_affine(dwconv3(x_k)))))
+ * (sigmoid = 0: no sigmoid, hf_refinement.use_sigmoid False).  details: host array of 7
+ * device pointers, each a channel-last (B, D, H, W, C) fp32 tensor with batch stride ldb
+ * (the detail bands of wf_dwt3d_haar_fwd qualify); dw_w (C, 27), dw_b (C): the depthwise
+ * conv1; in_w / in_b (C): the InstanceNorm3d affine, eps its eps (biased variance per
+ * (detail, sample, channel)); pw_w (C, C), pw_b (C): conv2.  out: (7, B, D, H, W, C).
+ * workspace: wf_hf_refine_workspace_bytes(B, C) bytes.  fp32 arithmetic throughout.          */
+int64_t wf_hf_refine_workspace_bytes(int64_t B, int64_t C);
+int wf_hf_refine_fwd(const float* const* details, int64_t ldb, const float* dw_w,
+                     const float* dw_b, const float* in_w, const float* in_b, float eps,
+                     const float* pw_w, const float* pw_b, int sigmoid, float* out,
+                     void* workspace, int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                     void* stream);
 
 /* nn.Upsample(scale_factor=s, mode='trilinear', align_corners) of a channel-last tensor
  * (B, d, h, w, C) -> (B, D, H, W, C), PyTorch's upsample_trilinear3d index arithmetic: the

@@ -207,3 +207,38 @@ def test_conv3d_k3_autograd(cin, cout, S):
     assert C.rel_l2(xg.grad, xc.grad) <= 1e-5
     assert C.rel_l2(wg.grad, wc.grad) <= 1e-5
     assert C.rel_l2(bg.grad, bc.grad) <= 1e-5
+
+
+@pytest.mark.parametrize("C_,B,S,sig", [
+    (48, 2, (12, 12, 12), True),    # decoder2 level shapes (C 48)
+    (96, 1, (6, 7, 9), True),       # ragged planes / rows, z not a multiple of the 8-plane tile
+    (192, 2, (3, 3, 3), True),      # decoder4 (C 192), fewer positions than one workgroup
+    (48, 1, (17, 5, 4), False),     # hf_refinement.use_sigmoid False
+    (24, 1, (4, 9, 10), True),      # C / 4 not dividing 256 evenly
+])
+def test_hf_refinement_fused_vs_module(C_, B, S, sig):
+    """ops.hf_refine (csrc/hfref.hip, two passes over the 7 detail tensors of a level) against
+    HFRefinementRes's own PyTorch forward in fp64 on the CPU (idwt_upsample.py:39-50), detail
+    tensors as the DWT hands them over: channel-last views of one (8, B, D, H, W, C) band
+    buffer.  All-fp32 kernel arithmetic: rel-L2 <= 1e-5."""
+    import waveformer_amd.network_models as NM
+    from waveformer_amd import ops
+    cfg = None if sig else {"hf_refinement": {"use_sigmoid": False}}
+    m = NM.HFRefinementRes(C_, network_config=cfg)
+    with torch.no_grad():
+        for i, p in enumerate(m.parameters()):
+            p.copy_(seeded_randn(tuple(p.shape), 40 + i) * (0.5 if p.dim() > 1 else 0.2)
+                    + (1.0 if p.dim() == 1 and i == 2 else 0.0))
+    bands = (seeded_randn((8, B) + S + (C_,), 7) * 1.5 + 0.2)
+    det = {k: bands[i + 1].permute(0, 4, 1, 2, 3) for i, k in enumerate(ops.DETAIL_KEYS)}
+    md = m.double()
+    with torch.no_grad():
+        want = {k: md(v.double()) for k, v in det.items()}
+    m = m.float().cuda()
+    bc = bands.cuda()
+    dc = {k: bc[i + 1].permute(0, 4, 1, 2, 3) for i, k in enumerate(ops.DETAIL_KEYS)}
+    with torch.no_grad():
+        assert m.fast_ok(dc["aad"])
+        got = ops.hf_refine(dc, m)
+    for k in ops.DETAIL_KEYS:
+        assert C.rel_l2(got[k], want[k]) <= 1e-5, k

@@ -44,6 +44,9 @@ SIGNATURES = {
     "wf_instnorm_finalize": (_I, [_P, _P, _I64, _I64, _I64, _F, _P]),
     "wf_instnorm_workspace_bytes": (_I64, [_I64, _I64]),
     "wf_instnorm_stats_cl": (_I, [_P, _I64, _I64, _I64, _I64, _F, _P, _P, _P]),
+    "wf_hf_refine_workspace_bytes": (_I64, [_I64, _I64]),
+    "wf_hf_refine_fwd": (_I, [_P, _I64, _P, _P, _P, _P, _F, _P, _P, _I, _P, _P, _I64, _I64,
+                              _I64, _I64, _I64, _P]),
     "wf_norm_act_cl": (_I, [_P, _I64, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "wf_upsample_trilinear_cl": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64,
                                       _I, _P]),
@@ -94,7 +97,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 _lock = threading.Lock()
 _lib = None
 _err = None

@@ -1,7 +1,8 @@
 """IDWT decoder block.
 
 Mirrors network_models/idwt_upsample.py (HFRefinementRes :12-50, UnetrIDWTBlock :53-166):
-same constructor and state_dict keys.  The wavelet synthesis (ptwt.waverec3, :160) and the
+same constructor and state_dict keys.  HFRefinementRes runs as one fused HIP call per level
+at inference (ops.hf_refine; PyTorch modules under autograd).  The wavelet synthesis (ptwt.waverec3, :160) and the
 concatenation with the skip (:163) run as one wf_idwt3d_haar launch that writes straight into
 the first half of the concatenated buffer; the surrounding convolutions are PyTorch/MIOpen.
 """
@@ -30,6 +31,19 @@ class HFRefinementRes(nn.Module):
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = nn.Conv3d(in_channels, in_channels, kernel_size=1, bias=True)
         self.sigmoid = nn.Sigmoid() if hf_config.get('use_sigmoid', True) else None
+
+    def fast_ok(self, x) -> bool:
+        """The fused HIP path (ops.hf_refine, inference) covers this module: depthwise 3^3
+        conv with bias, InstanceNorm3d(affine, no running stats), 1x1 conv with bias."""
+        c1, n, c2 = self.conv1, self.norm, self.conv2
+        return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 5
+                and not (torch.is_grad_enabled() and (
+                    x.requires_grad or any(p.requires_grad for p in self.parameters())))
+                and x.shape[1] % 4 == 0 and x.shape[1] <= 256
+                and c1.kernel_size == (3, 3, 3) and c1.padding == (1, 1, 1)
+                and c1.groups == c1.in_channels and c1.bias is not None
+                and n.affine and not n.track_running_stats
+                and c2.kernel_size == (1, 1, 1) and c2.bias is not None)
 
     def forward(self, x):
         r = self.conv2(self.relu(self.norm(self.conv1(x))))
@@ -62,8 +76,11 @@ class UnetrIDWTBlock(nn.Module):
     def forward(self, inp, skip, hf_coeffs):
         inp = self.conv_lf_block(inp)
         if self.hf_refinement:
-            hf_coeffs = tuple({k: self.hf_ref[i](d[k]) for k in d}
-                              for i, d in enumerate(hf_coeffs))
+            # inference: the 7 details of a level in one fused HIP call (ops.hf_refine)
+            hf_coeffs = tuple(
+                ops.hf_refine(d, self.hf_ref[i]) if self.hf_ref[i].fast_ok(d["aad"])
+                else {k: self.hf_ref[i](d[k]) for k in d}
+                for i, d in enumerate(hf_coeffs))
         wname = str(getattr(self.wavelet, "name", self.wavelet))
         if wname not in ("db1", "haar"):
             # longer filters (config 5): one wf_idwt3d_level launch per level, the finest

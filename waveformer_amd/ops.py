@@ -478,6 +478,41 @@ def cl_ld(x: torch.Tensor) -> Optional[int]:
     return ld
 
 
+def hf_refine(details: Dict[str, torch.Tensor], mod) -> Dict[str, torch.Tensor]:
+    """HFRefinementRes (idwt_upsample.py:12-50) of the 7 detail tensors of one level in one
+    wf_hf_refine_fwd call (two passes: depthwise conv + InstanceNorm moments, then conv +
+    norm + ReLU + 1x1 conv + sigmoid + product).  details: {key: (B, C, D, H, W)} channel-last
+    views (the DWT's detail bands); returns the refined tensors the same way, as views of one
+    (7, B, D, H, W, C) buffer (what idwt3d_haar reads)."""
+    ts = [details[k] for k in DETAIL_KEYS]
+    B, C, D, H, W = ts[0].shape
+    P = D * H * W
+
+    def dense_cl(t):  # (b, c, z, y, x) at b*s0 + ((z*H + y)*W + x)*C + c
+        st = t.stride()
+        return cl_ld(t) == C and st[2:] == (H * W * C, W * C, C)
+    ts = [t if dense_cl(t) else t.contiguous(memory_format=torch.channels_last_3d) for t in ts]
+    if len({t.stride(0) for t in ts}) != 1:
+        ts = [t.contiguous(memory_format=torch.channels_last_3d) for t in ts]
+    for t in ts:
+        if tuple(t.shape) != (B, C, D, H, W):
+            raise ValueError("hf_refine: the 7 detail tensors must share one shape")
+        _check(t, "detail", contiguous=False)
+    c1, nrm, c2 = mod.conv1, mod.norm, mod.conv2
+    for prm, nm in ((c1.weight, "conv1.weight"), (c1.bias, "conv1.bias"), (nrm.weight, "norm.weight"),
+                    (nrm.bias, "norm.bias"), (c2.weight, "conv2.weight"), (c2.bias, "conv2.bias")):
+        _check(prm, nm)
+    out = torch.empty((7, B, D, H, W, C), dtype=torch.float32, device=ts[0].device)
+    ws = torch.empty(_lib.query("wf_hf_refine_workspace_bytes", B, C), dtype=torch.uint8,
+                     device=out.device)
+    ptrs = (ctypes.c_void_p * 7)(*[t.data_ptr() for t in ts])
+    _lib.call("wf_hf_refine_fwd", ptrs, ts[0].stride(0), c1.weight.data_ptr(), c1.bias.data_ptr(),
+              nrm.weight.data_ptr(), nrm.bias.data_ptr(), float(nrm.eps), c2.weight.data_ptr(),
+              c2.bias.data_ptr(), int(mod.sigmoid is not None), out.data_ptr(), ws.data_ptr(),
+              B, C, D, H, W, _stream())
+    return {k: out[i].permute(0, 4, 1, 2, 3) for i, k in enumerate(DETAIL_KEYS)}
+
+
 def to_cl(x: torch.Tensor) -> torch.Tensor:
     """x itself if it is channel-last already, else a channels_last_3d copy."""
     return x if cl_ld(x) is not None else x.contiguous(memory_format=torch.channels_last_3d)
