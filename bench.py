@@ -53,8 +53,10 @@ PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_fused_kernel" if os.environ.get("WF_FFN_FUS
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: enough for a >= 2 s timed region -- encoder 250, "
+                         "full 40, sliding / train 20)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 10 / 3)")
     ap.add_argument("--batch", type=int, default=None,
                     help="volumes per GPU per step (default: 8 for encoder, 1 for train)")
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16", "fp16"])
@@ -83,6 +85,10 @@ def parse():
         # stages better than 4 (902 vs 794 volumes/s measured); train: MIOpen find at B > 1 on
         # a fresh box does not finish within the bench's budget
         args.batch = {"train": 1, "full": 2}.get(args.workload, 8)
+    if args.steps is None:
+        args.steps = {"encoder": 250, "full": 40}.get(args.workload, 20)
+    if args.warmup is None:
+        args.warmup = 10 if args.workload == "encoder" else 3
     return args
 
 
