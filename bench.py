@@ -77,14 +77,15 @@ def parse():
                          "sharded over the ranks and all-gathered over RCCL; train: config 4, "
                          "fwd + DiceCE + bwd + clip + AdamW of the full Waveformer, DDP")
     ap.add_argument("--tta", type=int, default=0, help="sliding: 8-way flip TTA")
-    ap.add_argument("--miopen-find", type=int, default=1,
-                    help="train: MIOpen find mode (cudnn.benchmark) for the decoder convs")
+    ap.add_argument("--miopen-find", type=int, default=0,
+                    help="train: cudnn.benchmark (MIOpen find); no convolution of the step runs "
+                         "on MIOpen any more (autograd.conv_train), so it only matters for "
+                         "non-default module shapes")
     args = ap.parse_args()
     if args.batch is None:
         # encoder: B = 8 is the top of SURVEY 8d's C2 range {1, 2, 4, 8} and fills the 8^3 / 16^3
-        # stages better than 4 (902 vs 794 volumes/s measured); train: MIOpen find at B > 1 on
-        # a fresh box does not finish within the bench's budget
-        args.batch = {"train": 1, "full": 2}.get(args.workload, 8)
+        # stages better than 4 (902 vs 794 volumes/s measured); train: config 4's B = 4 / GPU
+        args.batch = {"train": 4, "full": 2}.get(args.workload, 8)
     if args.steps is None:
         args.steps = {"encoder": 250, "full": 40}.get(args.workload, 20)
     if args.warmup is None:
@@ -384,14 +385,13 @@ def main_train(args, world, rank, dev):
     DiceCE(to_onehot_y, softmax) -> backward -> clip_grad_norm_(12) -> AdamW(1e-4).  N > 1: DDP
     over RCCL (bucketed all-reduce of the fp32 gradients, overlapped with the backward).
     Encoder forward = HIP kernels (bf16x3 MFMA), encoder backward = HIP kernels + hipBLASLt
-    fp32 GEMM gradients, decoder convolutions = MIOpen (as in the reference)."""
+    fp32 GEMM gradients, decoder 3^3 convolutions = HIP forward / input- / weight-gradient
+    kernels, 1x1 / transposed convs = hipBLASLt GEMMs (no MIOpen convolution, no find)."""
     import waveformer_amd.network_models as NM
     from waveformer_amd.losses import DiceCELoss
     torch.manual_seed(0)
-    # the decoder's MONAI convolutions train on MIOpen (as in the reference): channels_last_3d
-    # lets MIOpen use its NDHWC implicit-GEMM xdlops solvers, and find mode (cudnn.benchmark)
-    # picks them over the naive fallbacks immediate mode returns for 3-D fp32 backward
-    # (measured 0.21 s vs 3.1 s backward at B=1); the first step pays the find
+    # every decoder convolution trains on waveformer_amd kernels / GEMMs (autograd.conv_train);
+    # with MIOpen convolutions (round 1) the first step paid minutes of find at B = 4
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     model = NM.Waveformer(img_size=(args.img,) * 3, in_chans=4, out_chans=4,
                           depths=[2, 2, 2, 2], feat_size=[48, 96, 192, 384],

@@ -151,6 +151,18 @@ int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed, cons
                      float* out, int64_t ldo, double* stats_acc, int64_t B, int64_t Cin,
                      int64_t Cout, int64_t D, int64_t H, int64_t W, int precision, void* stream);
 
+/* Weight gradient of wf_conv3d_k3_fwd (training, config 4):
+ *   dw[co, ci, kz, ky, kx] (+)= sum_p dy[p, co] * x[p + (kz-1, ky-1, kx-1), ci]
+ * x, dy channel-last (positions ldx / ldg floats apart), dw (Cout, Cin, 3, 3, 3) fp32
+ * (accumulate = 1 adds to it).  fp32-faithful bf16x3 MFMAs, deterministic (per-workgroup
+ * partials in workspace, summed in a fixed order).  Cin % 4 == 0, Cout % 16 == 0.
+ * workspace: wf_conv3d_k3_wgrad_workspace_bytes(B, Cin, Cout, D, H, W) bytes.                */
+int64_t wf_conv3d_k3_wgrad_workspace_bytes(int64_t B, int64_t Cin, int64_t Cout, int64_t D,
+                                           int64_t H, int64_t W);
+int wf_conv3d_k3_wgrad(const float* x, int64_t ldx, const float* dy, int64_t ldg, float* dw,
+                       int accumulate, void* workspace, int64_t B, int64_t Cin, int64_t Cout,
+                       int64_t D, int64_t H, int64_t W, void* stream);
+
 /* InstanceNorm3d(affine=False) statistics of a channel-last tensor: P positions per sample,
  * element (b, p, c) at x[(b*P + p)*ldx + c].  stats: (B, 2, C) fp32 {mean row, rstd row},
  * rstd = 1/sqrt(biased var + eps).  workspace: wf_instnorm_workspace_bytes(B, C) bytes.
@@ -189,6 +201,14 @@ int wf_hf_refine_fwd(const float* const* details, int64_t ldb, const float* dw_w
 int wf_upsample_trilinear_cl(const float* in, float* out, int64_t B, int64_t C, int64_t d,
                              int64_t h, int64_t w, int64_t D, int64_t H, int64_t W,
                              int align_corners, void* stream);
+
+/* Predictor.predict_raw_probability (light_training/prediction.py:35-63): channel-first
+ * (C, d, h, w) fp32 (channel stride ldc) -> (C, D, H, W) per channel
+ * F.interpolate(mode='trilinear', align_corners), written fp16 (out_f16 = 1, the reference's
+ * torch.half buffer) or fp32.  PyTorch's upsample_trilinear3d index arithmetic.             */
+int wf_resample_trilinear_cf(const float* in, int64_t ldc, int64_t C, int64_t d, int64_t h,
+                             int64_t w, int64_t D, int64_t H, int64_t W, int align_corners,
+                             void* out, int out_f16, void* stream);
 
 /* out (M, N) = bias + act(x) (M, K) . W^T, act = GELU(erf) if gelu_in else identity; fp32
  * rows, W as [2][N][K] bf16 hi / lo planes (wf_split_f32_to_bf16x2).  The 1x1x1 convolutions

@@ -242,3 +242,26 @@ def test_hf_refinement_fused_vs_module(C_, B, S, sig):
         got = ops.hf_refine(dc, m)
     for k in ops.DETAIL_KEYS:
         assert C.rel_l2(got[k], want[k]) <= 1e-5, k
+
+
+@pytest.mark.parametrize("B,Cin,Cout,S", [
+    (1, 4, 48, (20, 18, 70)),     # encoder1's first conv (Cin 4: one partial 16-channel slice)
+    (2, 96, 48, (9, 13, 33)),     # decoder conv_block conv1 (2C -> C), ragged x / y tiles
+    (1, 48, 48, (8, 5, 17)),
+    (1, 192, 96, (6, 7, 11)),     # Cout 96 = two 48-channel blocks
+    (1, 384, 192, (8, 8, 8)),     # decoder4.conv_lf_block shape
+    (1, 20, 32, (3, 4, 5)),       # Cin % 16 != 0, Cout % 48 != 0 (16-channel blocks)
+])
+def test_conv3d_k3_wgrad_vs_cpu(B, Cin, Cout, S):
+    """wf_conv3d_k3_wgrad (csrc/conv3d_wgrad.hip) against torch.nn.grad.conv3d_weight in fp64
+    on the CPU: bf16x3 operands, fp32 accumulation over B*D*H*W positions: rel-L2 <= 1e-5;
+    two runs bit-identical (no atomics)."""
+    from waveformer_amd import ops
+    x = seeded_randn((B, Cin) + S, 11) * 2 + 0.1
+    g = seeded_randn((B, Cout) + S, 12)
+    want = torch.nn.grad.conv3d_weight(x.double(), (Cout, Cin, 3, 3, 3), g.double(), padding=1)
+    xc = x.cuda().contiguous(memory_format=torch.channels_last_3d)
+    gc = g.cuda().contiguous(memory_format=torch.channels_last_3d)
+    got = ops.conv3d_k3_wgrad(xc, gc, (Cout, Cin, 3, 3, 3))
+    assert C.rel_l2(got, want) <= 1e-5
+    assert torch.equal(got, ops.conv3d_k3_wgrad(xc, gc, (Cout, Cin, 3, 3, 3)))

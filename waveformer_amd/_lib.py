@@ -44,6 +44,11 @@ SIGNATURES = {
     "wf_instnorm_finalize": (_I, [_P, _P, _I64, _I64, _I64, _F, _P]),
     "wf_instnorm_workspace_bytes": (_I64, [_I64, _I64]),
     "wf_instnorm_stats_cl": (_I, [_P, _I64, _I64, _I64, _I64, _F, _P, _P, _P]),
+    "wf_resample_trilinear_cf": (_I, [_P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I,
+                                      _P, _I, _P]),
+    "wf_conv3d_k3_wgrad_workspace_bytes": (_I64, [_I64] * 6),
+    "wf_conv3d_k3_wgrad": (_I, [_P, _I64, _P, _I64, _P, _I, _P, _I64, _I64, _I64, _I64, _I64,
+                                _I64, _P]),
     "wf_hf_refine_workspace_bytes": (_I64, [_I64, _I64]),
     "wf_hf_refine_fwd": (_I, [_P, _I64, _P, _P, _P, _P, _F, _P, _P, _I, _P, _P, _I64, _I64,
                               _I64, _I64, _I64, _P]),

@@ -208,8 +208,8 @@ def upsample_cl(x: torch.Tensor, size) -> torch.Tensor:
 class Conv3dK3(torch.autograd.Function):
     """Conv3d(k=3, stride 1, padding 1) on the implicit-GEMM MFMA kernel (bf16x3) with its
     input gradient on the same kernel: dx = conv(dy, W~), W~[ci, co, k] = W[co, ci, 26 - k]
-    (flipped taps, swapped channels).  The weight gradient is the framework's conv3d_weight
-    (MIOpen), as in the reference's training."""
+    (flipped taps, swapped channels), and its weight gradient on wf_conv3d_k3_wgrad (implicit
+    GEMM over the positions, bf16x3, deterministic) -- no MIOpen find for any shape."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -232,7 +232,10 @@ class Conv3dK3(torch.autograd.Function):
             else:
                 dx = torch.nn.grad.conv3d_input(xc.shape, w, g, padding=1)
         if ctx.needs_input_grad[1]:
-            dw = torch.nn.grad.conv3d_weight(xc, w.shape, g, padding=1)
+            if w.shape[0] % 16 == 0 and w.shape[1] % 4 == 0:
+                dw = ops.conv3d_k3_wgrad(xc, g, w.shape)   # HIP, no MIOpen find
+            else:
+                dw = torch.nn.grad.conv3d_weight(xc, w.shape, g, padding=1)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.sum(dim=(0, 2, 3, 4))
         return dx, dw, db
@@ -240,3 +243,79 @@ class Conv3dK3(torch.autograd.Function):
 
 def conv3d_k3(x, w, b=None):
     return Conv3dK3.apply(x, w, b)
+
+
+# ------------------------------------------------------------------------------------------
+# the decoder's other convolutions in training: depthwise 3^3 on HIP, 1x1 and the 2^3
+# transposed conv as channel-last GEMMs (hipBLASLt) -- no MIOpen convolution anywhere, so a
+# training step needs no MIOpen find / kernel compilation (minutes at B = 4 on a fresh box)
+# ------------------------------------------------------------------------------------------
+class DWConv3dK3(torch.autograd.Function):
+    """Depthwise Conv3d(C, C, 3, padding=1, groups=C) channel-last: forward wf_dwconv3d_cl,
+    input gradient the same kernel with flipped taps, weight gradient wf_dwconv3d_wgrad."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xc = ops.to_cl(x)
+        ctx.save_for_backward(xc, w)
+        ctx.has_bias = b is not None
+        return ops.dwconv3d_cl(xc, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, w = ctx.saved_tensors
+        g = ops.to_cl(g)
+        B, C, D, H, W = xc.shape
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.empty_cl(B, C, D, H, W, g.device)
+            _lib.call("wf_dwconv3d_cl", g.data_ptr(), _f32(w.detach()).data_ptr(), None, 1,
+                      dx.data_ptr(), B, C, D, H, W, _s())
+        if ctx.needs_input_grad[1]:
+            part = torch.empty(_lib.query("wf_dwconv_wgrad_ws_floats", B * D * H * W, C),
+                               dtype=torch.float32, device=g.device)
+            dw = torch.empty(C * 27, dtype=torch.float32, device=g.device)
+            _lib.call("wf_dwconv3d_wgrad", g.data_ptr(), xc.data_ptr(), part.data_ptr(),
+                      dw.data_ptr(), B, C, D, H, W, _s())
+            dw = dw.view_as(w)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = colsum(g.permute(0, 2, 3, 4, 1).reshape(-1, C))
+        return dx, dw, db
+
+
+def _rows(x: torch.Tensor) -> torch.Tensor:
+    """(B, C, D, H, W) -> the (B, D, H, W, C) channel-last view (a copy if x is not)."""
+    return ops.to_cl(x).permute(0, 2, 3, 4, 1)
+
+
+def conv_train(conv: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """A decoder Conv3d / ConvTranspose3d under autograd on the waveformer_amd paths:
+    3^3 dense (Conv3dK3), 3^3 depthwise (DWConv3dK3), 1^3 (F.linear over channel-last rows),
+    2^3 stride-2 transposed (one GEMM into the 8 sub-voxels).  Other shapes: the module."""
+    F = torch.nn.functional
+    nn = torch.nn
+    ok = x.is_cuda and x.dtype == torch.float32 and x.dim() == 5
+    if ok and type(conv) is nn.Conv3d and conv.padding_mode == "zeros" \
+            and conv.dilation == (1, 1, 1) and conv.stride == (1, 1, 1):
+        Cin, Cout = conv.in_channels, conv.out_channels
+        if conv.kernel_size == (3, 3, 3) and conv.padding == (1, 1, 1):
+            if conv.groups == 1 and Cin % 4 == 0 and Cout % 16 == 0:
+                return conv3d_k3(x, conv.weight, conv.bias)
+            if conv.groups == Cin == Cout and Cin % 4 == 0:
+                return DWConv3dK3.apply(x, conv.weight, conv.bias)
+        if conv.kernel_size == (1, 1, 1) and conv.padding == (0, 0, 0) and conv.groups == 1:
+            y = F.linear(_rows(x), conv.weight.view(Cout, Cin), conv.bias)
+            return y.permute(0, 4, 1, 2, 3)
+    if ok and type(conv) is nn.ConvTranspose3d and conv.kernel_size == (2, 2, 2) \
+            and conv.stride == (2, 2, 2) and conv.padding == (0, 0, 0) \
+            and conv.output_padding == (0, 0, 0) and conv.groups == 1 \
+            and conv.dilation == (1, 1, 1):
+        B, Cin, d, h, w = x.shape
+        Cout = conv.out_channels
+        wr = conv.weight.permute(0, 2, 3, 4, 1).reshape(Cin, 8 * Cout)
+        y = (_rows(x).reshape(-1, Cin) @ wr).view(B, d, h, w, 2, 2, 2, Cout)
+        y = y.permute(0, 1, 4, 2, 5, 3, 6, 7).reshape(B, 2 * d, 2 * h, 2 * w, Cout)
+        if conv.bias is not None:
+            y = y + conv.bias
+        return y.permute(0, 4, 1, 2, 3)
+    return conv(x)

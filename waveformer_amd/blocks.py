@@ -6,8 +6,9 @@ These are the decoder's full-resolution 3^3 convolutions.  In
 1) on the waveformer_amd kernels, channel-last end to end: the implicit-GEMM MFMA convolution
 (ops.conv3d_k3), InstanceNorm statistics and one fused norm + residual + LeakyReLU pass
 (ops.instnorm_stats / ops.norm_act), the 1x1 residual conv as one GEMM.  Training (autograd)
-and the other layers (transposed / depthwise / 1x1 convs) run as PyTorch-ROCm modules (MIOpen),
-as in the reference.  norm_name is always "instance" (InstanceNorm3d, affine=False) and the
+runs every convolution through wfa.conv_train: the 3^3 convs on the HIP forward / input- /
+weight-gradient kernels, 1x1 and 2^3 transposed convs as hipBLASLt GEMMs -- no MIOpen
+convolution, hence no MIOpen find.  norm_name is always "instance" (InstanceNorm3d, affine=False) and the
 activation LeakyReLU(0.01), as Waveformer builds them.
 """
 from __future__ import annotations
@@ -75,11 +76,9 @@ class Convolution(nn.Sequential):
         conv = self.conv
         if _fast_ok(x, self) and _k3_ok(conv, x.shape[1]):
             return ops.conv3d_k3(x, conv.weight, conv.bias)
-        if x.is_cuda and x.dtype == torch.float32 and x.dim() == 5 and _k3_ok(conv, x.shape[1]):
-            # training (autograd recording): the MFMA conv forward and input gradient
-            # (wfa.Conv3dK3, channel-last), MIOpen for the weight gradient
-            return wfa.conv3d_k3(x, conv.weight, conv.bias)
-        return conv(x)
+        # training (autograd recording): the MFMA conv forward / input / weight gradients
+        # (wfa.Conv3dK3), 1x1 and transposed convs as channel-last GEMMs (wfa.conv_train)
+        return wfa.conv_train(conv, x)
 
 
 def get_conv_layer(spatial_dims: int, in_channels: int, out_channels: int,

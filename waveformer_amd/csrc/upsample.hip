@@ -62,9 +62,86 @@ __global__ __launch_bounds__(256) void upsample_cl_kernel(const float* __restric
   }
 }
 
+// Predictor.predict_raw_probability (light_training/prediction.py:35-63): every class channel
+// of one case's (C, d, h, w) probability volume resampled to the pre-resample shape with
+// F.interpolate(mode='trilinear', align_corners=False), stored fp16 (the reference's
+// torch.half buffer) or fp32.  Channel-first, one thread per 4 consecutive x outputs: the 8
+// source rows of a thread are shared by its x neighbours (L1 / L2), the fp16 output is
+// written once, 8 B per thread, coalesced along x.
+template <bool F16>
+__global__ __launch_bounds__(256) void resample_cf_kernel(const float* __restrict__ in,
+                                                          int64_t ldc, void* __restrict__ out,
+                                                          int d, int h, int w, int D, int H,
+                                                          int W, int64_t total, int ac) {
+  const int W4 = (W + 3) >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = i / W4;
+    const int x0 = 4 * (int)(i - t * W4);
+    const int y = (int)(t % H);
+    t /= H;
+    const int z = (int)(t % D);
+    const int64_t c = t / D;
+    const Src1 sz = src_index(z, d, D, ac), sy = src_index(y, h, H, ac);
+    const float* base = in + c * ldc;
+    const float* r00 = base + ((int64_t)sz.i0 * h + sy.i0) * w;
+    const float* r01 = base + ((int64_t)sz.i0 * h + sy.i1) * w;
+    const float* r10 = base + ((int64_t)sz.i1 * h + sy.i0) * w;
+    const float* r11 = base + ((int64_t)sz.i1 * h + sy.i1) * w;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int x = min(x0 + e, W - 1);
+      const Src1 sx = src_index(x, w, W, ac);
+      const float a0 = sy.l0 * (sx.l0 * r00[sx.i0] + sx.l1 * r00[sx.i1]) +
+                       sy.l1 * (sx.l0 * r01[sx.i0] + sx.l1 * r01[sx.i1]);
+      const float a1 = sy.l0 * (sx.l0 * r10[sx.i0] + sx.l1 * r10[sx.i1]) +
+                       sy.l1 * (sx.l0 * r11[sx.i0] + sx.l1 * r11[sx.i1]);
+      v[e] = sz.l0 * a0 + sz.l1 * a1;
+    }
+    const int64_t o = ((c * D + z) * H + y) * (int64_t)W + x0;
+    if (F16) {
+      _Float16* oh = reinterpret_cast<_Float16*>(out) + o;
+      if (x0 + 4 <= W && (o & 3) == 0) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<h4*>(oh) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2],
+                                        (_Float16)v[3]};
+      } else {
+        for (int e = 0; e < 4 && x0 + e < W; ++e) oh[e] = (_Float16)v[e];
+      }
+    } else {
+      float* of = reinterpret_cast<float*>(out) + o;
+      if (x0 + 4 <= W && (o & 3) == 0) {
+        *reinterpret_cast<f32x4*>(of) = f32x4{v[0], v[1], v[2], v[3]};
+      } else {
+        for (int e = 0; e < 4 && x0 + e < W; ++e) of[e] = v[e];
+      }
+    }
+  }
+}
+
 }  // namespace wf
 
 using namespace wf;
+
+extern "C" int wf_resample_trilinear_cf(const float* in, int64_t ldc, int64_t C, int64_t d,
+                                        int64_t h, int64_t w, int64_t D, int64_t H, int64_t W,
+                                        int align_corners, void* out, int out_f16,
+                                        void* stream) {
+  WF_REQUIRE(C >= 1 && d >= 1 && h >= 1 && w >= 1 && D >= 1 && H >= 1 && W >= 1,
+             "empty tensor");
+  WF_REQUIRE(ldc >= d * h * w, "channel stride smaller than one (d, h, w) volume");
+  WF_REQUIRE(C * D * H * W < ((int64_t)1 << 40), "output too large");
+  WF_REQUIRE_PTR(in);
+  WF_REQUIRE_PTR(out);
+  const int64_t total = C * D * H * ((W + 3) / 4);
+  int64_t blocks = cdiv(total, 256);
+  if (blocks > 16384) blocks = 16384;
+  auto k = out_f16 ? resample_cf_kernel<true> : resample_cf_kernel<false>;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in, ldc, out,
+                     (int)d, (int)h, (int)w, (int)D, (int)H, (int)W, total, align_corners);
+  return check_launch("wf_resample_trilinear_cf");
+}
 
 extern "C" int wf_upsample_trilinear_cl(const float* in, float* out, int64_t B, int64_t C,
                                         int64_t d, int64_t h, int64_t w, int64_t D, int64_t H,

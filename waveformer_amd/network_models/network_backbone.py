@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from functools import partial
 
+from .. import autograd as wfa
 from .. import ops
 
 from ..blocks import UnetOutBlock, UnetrBasicBlock, UnetrUpBlock
@@ -64,10 +65,12 @@ class ChannelCalibration(nn.Module):
         self.relu = nn.ReLU()
 
     def forward(self, x):
-        identity = self.residual(x)
-        x = self.relu(self.norm_reduce(self.reduce(x)))
-        x = self.relu(self.norm_conv(self.conv(x)))
-        x = self.norm_expand(self.expand(x))
+        # the convs through wfa.conv_train under autograd (GEMM 1x1s, HIP 3^3), else modules
+        cv = wfa.conv_train if torch.is_grad_enabled() else (lambda m, t: m(t))
+        identity = cv(self.residual, x)
+        x = self.relu(self.norm_reduce(cv(self.reduce, x)))
+        x = self.relu(self.norm_conv(cv(self.conv, x)))
+        x = self.norm_expand(cv(self.expand, x))
         b, c = x.shape[:2]
         se = self.sigmoid(self.fc2(F.relu(self.fc1(self.global_pool(x).view(b, c)))))
         return self.relu(x * se.view(b, c, 1, 1, 1) + identity)

@@ -109,13 +109,20 @@ class ProjectionUpsample(nn.Module):
             return self._forward_hip(x)
         if x.is_cuda and x.dtype == torch.float32 and x.dim() == 5:
             # training on the GPU: the trilinear up-sampling (and its adjoint) on HIP, the convs
-            # on PyTorch / MIOpen; the residual's 1x1 conv runs before its up-sampling (linear,
-            # interpolation weights sum to 1: the same function and gradients)
+            # through wfa.conv_train (HIP depthwise, GEMM 1x1s); the residual's 1x1 conv runs
+            # before its up-sampling (linear, interpolation weights sum to 1: the same function
+            # and gradients)
             size = tuple(s * self.stride for s in x.shape[2:])
-            y = self.conv3(self.act(self.conv2(self.norm(self.conv1[1](wfa.upsample_cl(x, size))))))
+            cv = wfa.conv_train
+            y = cv(self.conv2, self.norm(cv(self.conv1[1], wfa.upsample_cl(x, size))))
+            y = self.act(y)
+            if self.use_double_conv:
+                y = cv(self.conv3[2], self.conv3[1](cv(self.conv3[0], y)))
+            else:
+                y = cv(self.conv3, y)
             if not self.do_res:
                 return y
-            return y + wfa.upsample_cl(self.res_conv[1](x), size)
+            return y + wfa.upsample_cl(cv(self.res_conv[1], x), size)
         y = self.conv3(self.act(self.conv2(self.norm(self.conv1(x)))))
         return y + self.res_conv(x) if self.do_res else y
 

@@ -478,6 +478,27 @@ def cl_ld(x: torch.Tensor) -> Optional[int]:
     return ld
 
 
+def resample_trilinear_cf(x: torch.Tensor, size: Sequence[int], dtype=torch.float16,
+                          align_corners: bool = False) -> torch.Tensor:
+    """(C, d, h, w) -> (C, *size) trilinear resampling of every channel
+    (F.interpolate(x[c][None, None], size, mode='trilinear', align_corners)), output `dtype`
+    fp16 or fp32 (wf_resample_trilinear_cf): Predictor.predict_raw_probability's resample."""
+    if x.dim() != 4:
+        raise ValueError(f"resample_trilinear_cf: (C, d, h, w) expected, got {tuple(x.shape)}")
+    if dtype not in (torch.float16, torch.float32):
+        raise TypeError("resample_trilinear_cf: fp16 or fp32 output")
+    x = x if x.dtype == torch.float32 else x.float()
+    if x.stride()[1:] != (x.shape[2] * x.shape[3], x.shape[3], 1):
+        x = x.contiguous()
+    _check(x, "x", contiguous=False)
+    C, d, h, w = x.shape
+    D, H, W = (int(v) for v in size)
+    out = torch.empty((C, D, H, W), dtype=dtype, device=x.device)
+    _lib.call("wf_resample_trilinear_cf", x.data_ptr(), x.stride(0), C, d, h, w, D, H, W,
+              int(bool(align_corners)), out.data_ptr(), int(dtype == torch.float16), _stream())
+    return out
+
+
 def hf_refine(details: Dict[str, torch.Tensor], mod) -> Dict[str, torch.Tensor]:
     """HFRefinementRes (idwt_upsample.py:12-50) of the 7 detail tensors of one level in one
     wf_hf_refine_fwd call (two passes: depthwise conv + InstanceNorm moments, then conv +
@@ -613,6 +634,25 @@ def dwconv3d_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tens
     _lib.call("wf_dwconv3d_cl", x.data_ptr(), weight.data_ptr(), _ptr(bias), 0, out.data_ptr(),
               B, C, D, H, W, _stream())
     return out
+
+
+def conv3d_k3_wgrad(x: torch.Tensor, dy: torch.Tensor, wshape) -> torch.Tensor:
+    """dW of conv3d_k3 (wf_conv3d_k3_wgrad): x (B, Cin, D, H, W), dy (B, Cout, D, H, W), both
+    channel-last (copied to it otherwise) -> (Cout, Cin, 3, 3, 3) fp32."""
+    x, dy = to_cl(x), to_cl(dy)
+    _check(x, "x", contiguous=False)
+    _check(dy, "dy", contiguous=False)
+    B, Cin, D, H, W = x.shape
+    Cout = dy.shape[1]
+    if tuple(wshape) != (Cout, Cin, 3, 3, 3) or tuple(dy.shape) != (B, Cout, D, H, W):
+        raise ValueError(f"conv3d_k3_wgrad: x {tuple(x.shape)}, dy {tuple(dy.shape)}, weight "
+                         f"{tuple(wshape)} do not match")
+    dw = torch.empty(tuple(wshape), dtype=torch.float32, device=x.device)
+    ws = torch.empty(_lib.query("wf_conv3d_k3_wgrad_workspace_bytes", B, Cin, Cout, D, H, W),
+                     dtype=torch.uint8, device=x.device)
+    _lib.call("wf_conv3d_k3_wgrad", x.data_ptr(), cl_ld(x), dy.data_ptr(), cl_ld(dy),
+              dw.data_ptr(), 0, ws.data_ptr(), B, Cin, Cout, D, H, W, _stream())
+    return dw
 
 
 def linear_rows(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
