@@ -1,0 +1,45 @@
+"""Run-to-run determinism of the encoder forward (the benched path) with the caching
+allocator's free memory filled with NaN before every run: a kernel that reads memory it did
+not write shows up as NaN, a race as a bitwise difference between runs.  (The encoder's
+inference kernels use no atomics; the decoder's split-K convolution and InstanceNorm moments
+do, and are not covered here.)"""
+import pytest
+import torch
+
+from tests import cases as C
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from waveformer_amd import _lib
+    _lib.load()
+    yield
+
+
+def _flat(r):
+    outs, hfs = r
+    return list(outs) + [d[k] for h in hfs for d in h for k in sorted(d)]
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "fp16"])
+def test_encoder128_bitwise_deterministic_under_nan_filled_memory(prec):
+    from waveformer_amd import ops
+    case = C.cases()["enc128"]
+    m, _ = C.build(case, "cuda")
+    x = torch.cat([C.case_input(case)] * 2).cuda()
+    runs = []
+    for _ in range(3):
+        junk = torch.full((3 * 1024 ** 3 // 4,), float("nan"), device="cuda")
+        del junk
+        with torch.no_grad(), ops.precision(prec):
+            runs.append([t.clone() for t in _flat(m(x))])
+        torch.cuda.synchronize()
+    for t in runs[0]:
+        assert not torch.isnan(t).any()
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)

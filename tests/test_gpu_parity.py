@@ -196,6 +196,41 @@ def test_ccf_ffn_stage1_fused_vs_oracle(shape, block):
         assert C.rel_l2(out, ref) <= tol, prec
 
 
+@pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (3, 7, 4, 9)])
+@pytest.mark.parametrize("block", [False, True])
+def test_ccf_ffn_stage2_vs_oracle(shape, block):
+    """C = 96, hidden = 384 (encoder stage 2): the pwconv + LN1 + GELU GEMM with the columns
+    split over the waves (gemm_lnw.hip; rows not a multiple of its 64-row tile included), the
+    z-marching depthwise conv with LN2 moments, the fc with LN2 + GELU in its loader and the
+    Q4 residual -- same bars as stage 1."""
+    import waveformer_amd.network_models as NM
+    from oracle.weight_rule import rule_state_dict
+    from waveformer_amd import ops
+    B = shape[0]
+    mlp = NM.CCF_FFN(96, 384, img_size=shape[1:])
+    sd = rule_state_dict(mlp.state_dict())
+    mlp.load_state_dict(sd)
+    mlp = mlp.eval().to(DEV)
+    norm2 = torch.nn.LayerNorm(96, eps=1e-6)
+    with torch.no_grad():
+        norm2.weight.copy_(seeded_randn((96,), 34) * 0.2 + 1)
+        norm2.bias.copy_(seeded_randn((96,), 35) * 0.1)
+    norm2 = norm2.to(DEV)
+    x = seeded_randn(shape + (96,), 36)
+    bs = torch.tensor([0.5, 2.0, 1.0][:B])
+    if block:
+        n2 = F.layer_norm(x, [96], norm2.weight.detach().cpu(), norm2.bias.detach().cpu(), 1e-6)
+        ref = x + R.ccf_ffn(sd, "", n2) * bs.view(-1, 1, 1, 1, 1)
+    else:
+        ref = x + (R.ccf_ffn(sd, "", x) - x) * bs.view(-1, 1, 1, 1, 1)
+    for prec, tol in (("bf16x3", 5e-5), ("bf16", 1e-2), ("fp16", 2e-3)):
+        with torch.no_grad(), ops.precision(prec):
+            xc = cuda(x)
+            stats = ops.msfuse([], xc, 1e-6)[1] if block else None
+            out = ops.ccf_ffn(xc, stats, norm2 if block else None, mlp, cuda(bs))
+        assert C.rel_l2(out, ref) <= tol, prec
+
+
 @pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (1, 16, 16, 16), (1, 3, 12, 9)])
 @pytest.mark.parametrize("block", [False, True])
 def test_ccf_ffn_stage1_whole_kernel_vs_oracle(shape, block, monkeypatch):

@@ -322,6 +322,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
   static const bool ares_only = getenv("WF_GEMM_ARES_ONLY") != nullptr;
   static const bool no_kc = getenv("WF_GEMM_NO_KC") != nullptr;
   if (!ares_only) {
+    if (try_launch_gemm_lnw(g, s)) return check_launch(who);
     if (try_launch_gemm_rows(g, s, !no_kc)) return check_launch(who);
     if (!no_kc && try_launch_gemm_kc(g, s)) return check_launch(who);
   }
