@@ -9,8 +9,8 @@ namespace wf {
 // ---------------------------------------------------------------------------------------
 // PatchEmbed: Conv3d(Cin, Cout, k=2, s=2) on NCDHW input -> channel-last output.
 // monai/networks/blocks/patchembedding.py:214 via network_models/waveformer.py:281,286.
-// Workgroup = one output row (b, z, y): the 2x2 input rows of every input channel are staged
-// in LDS (coalesced along x), the weights next to them; outputs are written channel-last.
+// Workgroup = R output rows (b, z, y0 .. y0 + R - 1): the 2x2 input rows of every input
+// channel are staged in LDS (coalesced along x); outputs are written channel-last.
 // ---------------------------------------------------------------------------------------
 // Thread = (output channel co, x group xg): the Cin*8 weights of co sit in registers and the
 // thread walks x = xg, xg + XG, ...; the slab reads are wave-wide broadcasts (a wave covers at
@@ -20,33 +20,80 @@ __global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restric
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ out, int Cin_rt,
-                                                          int Cout, int D, int H, int W) {
-  extern __shared__ __attribute__((aligned(16))) float slab[];  // [Cin][dz][dy][2W]
+                                                          int Cout, int D, int H, int W, int R) {
+  extern __shared__ __attribute__((aligned(16))) float slab[];  // [R][Cin][dz][dy][2W]
   const int Cin = CIN > 0 ? CIN : Cin_rt;
   const int W2 = 2 * W, H2 = 2 * H, D2 = 2 * D;
+  const int nyb = (H + R - 1) / R;
   int r = blockIdx.x;
-  const int y = r % H;
-  r /= H;
+  const int y0 = (r % nyb) * R;
+  r /= nyb;
   const int z = r % D;
   const int b = r / D;
+  const int nr = min(R, H - y0);  // output rows of this workgroup
   const int tid = threadIdx.x;
-  // stage the 2x2 input rows of every input channel (float4 when the row allows it)
+  const int rowf = Cin * 4 * W2;   // slab floats per output row
+  // stage the 2x2 input rows of every input channel for the nr output rows (float4 when the
+  // row allows it): R rows per workgroup keep R times the bytes in flight per load phase
   if ((W2 & 3) == 0) {
-    const int n4 = Cin * 4 * (W2 >> 2);
-    for (int i = tid; i < n4; i += blockDim.x) {
-      const int x4 = i % (W2 >> 2);
-      const int t = i / (W2 >> 2);
+    const int per = rowf >> 2;
+    for (int i = tid; i < nr * per; i += blockDim.x) {
+      const int rr = i / per, j = i - rr * per;
+      const int x4 = j % (W2 >> 2);
+      const int t = j / (W2 >> 2);
       const int dy = t & 1, dz = (t >> 1) & 1, ci = t >> 2;
       reinterpret_cast<f32x4*>(slab)[i] = reinterpret_cast<const f32x4*>(
-          x + ((((int64_t)b * Cin + ci) * D2 + 2 * z + dz) * H2 + 2 * y + dy) * W2)[x4];
+          x + ((((int64_t)b * Cin + ci) * D2 + 2 * z + dz) * H2 + 2 * (y0 + rr) + dy) * W2)[x4];
     }
   } else {
-    for (int i = tid; i < Cin * 4 * W2; i += blockDim.x) {
-      const int xx = i % W2;
-      const int t = i / W2;
+    for (int i = tid; i < nr * rowf; i += blockDim.x) {
+      const int rr = i / rowf, j = i - rr * rowf;
+      const int xx = j % W2;
+      const int t = j / W2;
       const int dy = t & 1, dz = (t >> 1) & 1, ci = t >> 2;
-      slab[i] = x[((((int64_t)b * Cin + ci) * D2 + 2 * z + dz) * H2 + 2 * y + dy) * W2 + xx];
+      slab[i] = x[((((int64_t)b * Cin + ci) * D2 + 2 * z + dz) * H2 + 2 * (y0 + rr) + dy) * W2 + xx];
     }
+  }
+  if (CIN > 0 && (Cout & 3) == 0) {
+    // thread = (4-channel group, x group): the 4 x 8 CIN weights in registers as channel
+    // pairs, packed FMAs (v_pk_fma_f32) over two channel pairs per slab value -- per output
+    // 4 LDS reads and 16 packed FMAs instead of 16 and 32 -- and one 16-byte store
+    constexpr int NK = CIN > 0 ? CIN * 8 : 1;
+    const int C4 = Cout >> 2;
+    const int XG = blockDim.x / C4;
+    const int cq = tid % C4, xg = tid / C4;
+    const bool act = xg < XG;
+    const int c0 = 4 * (act ? cq : 0);
+    f32x2 wa[NK], wb[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      wa[k] = f32x2{w[(int64_t)(c0 + 0) * NK + k], w[(int64_t)(c0 + 1) * NK + k]};
+      wb[k] = f32x2{w[(int64_t)(c0 + 2) * NK + k], w[(int64_t)(c0 + 3) * NK + k]};
+    }
+    const f32x2 ba = bias ? f32x2{bias[c0], bias[c0 + 1]} : f32x2{0.f, 0.f};
+    const f32x2 bb = bias ? f32x2{bias[c0 + 2], bias[c0 + 3]} : f32x2{0.f, 0.f};
+    __syncthreads();
+    if (!act) return;
+    for (int rr = 0; rr < nr; ++rr) {
+      const float* sl = slab + rr * rowf;
+      float* orow = out + (((int64_t)b * D + z) * H + y0 + rr) * W * (int64_t)Cout;
+      for (int xo = xg; xo < W; xo += XG) {
+        f32x2 a0 = ba, a1 = bb;
+#pragma unroll
+        for (int ci = 0; ci < NK / 8; ++ci)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float2 v = *reinterpret_cast<const float2*>(sl + (ci * 4 + q) * W2 + 2 * xo);
+            const int k = ci * 8 + 2 * q;
+            a0 = wa[k] * v.x + a0;
+            a1 = wb[k] * v.x + a1;
+            a0 = wa[k + 1] * v.y + a0;
+            a1 = wb[k + 1] * v.y + a1;
+          }
+        *reinterpret_cast<f32x4*>(orow + (int64_t)xo * Cout + c0) = f32x4{a0.x, a0.y, a1.x, a1.y};
+      }
+    }
+    return;
   }
   const int XG = blockDim.x / Cout;
   const int co = tid % Cout, xg = tid / Cout;
@@ -62,26 +109,29 @@ __global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restric
   const float bv = bias ? bias[cw] : 0.f;
   __syncthreads();
   if (!act) return;
-  float* orow = out + (((int64_t)b * D + z) * H + y) * W * (int64_t)Cout;
-  for (int xo = xg; xo < W; xo += XG) {
-    float acc = bv;
-    if (CIN > 0) {
+  for (int rr = 0; rr < nr; ++rr) {
+    const float* sl = slab + rr * rowf;
+    float* orow = out + (((int64_t)b * D + z) * H + y0 + rr) * W * (int64_t)Cout;
+    for (int xo = xg; xo < W; xo += XG) {
+      float acc = bv;
+      if (CIN > 0) {
 #pragma unroll
-      for (int ci = 0; ci < CIN; ++ci)
+        for (int ci = 0; ci < CIN; ++ci)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {  // q = dz * 2 + dy; the dx pair is adjacent in the slab
-          const float2 v = *reinterpret_cast<const float2*>(slab + (ci * 4 + q) * W2 + 2 * xo);
-          acc += wr[ci * 8 + 2 * q] * v.x + wr[ci * 8 + 2 * q + 1] * v.y;
-        }
-    } else {
-      for (int ci = 0; ci < Cin; ++ci)
-        for (int q = 0; q < 4; ++q) {
-          const float2 v = *reinterpret_cast<const float2*>(slab + (ci * 4 + q) * W2 + 2 * xo);
-          acc += w[((int64_t)co * Cin + ci) * 8 + 2 * q] * v.x +
-                 w[((int64_t)co * Cin + ci) * 8 + 2 * q + 1] * v.y;
-        }
+          for (int q = 0; q < 4; ++q) {  // q = dz * 2 + dy; the dx pair is adjacent in the slab
+            const float2 v = *reinterpret_cast<const float2*>(sl + (ci * 4 + q) * W2 + 2 * xo);
+            acc += wr[ci * 8 + 2 * q] * v.x + wr[ci * 8 + 2 * q + 1] * v.y;
+          }
+      } else {
+        for (int ci = 0; ci < Cin; ++ci)
+          for (int q = 0; q < 4; ++q) {
+            const float2 v = *reinterpret_cast<const float2*>(sl + (ci * 4 + q) * W2 + 2 * xo);
+            acc += w[((int64_t)co * Cin + ci) * 8 + 2 * q] * v.x +
+                   w[((int64_t)co * Cin + ci) * 8 + 2 * q + 1] * v.y;
+          }
+      }
+      orow[(int64_t)xo * Cout + co] = acc;
     }
-    orow[(int64_t)xo * Cout + co] = acc;
   }
 }
 
@@ -348,17 +398,24 @@ extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* b
   WF_REQUIRE_PTR(w);
   WF_REQUIRE_PTR(out);
   WF_REQUIRE(Cout <= 256, "PatchEmbed: at most 256 output channels");
-  const size_t lds = (size_t)Cin * 8 * W * sizeof(float);
-  WF_REQUIRE(lds <= 64 * 1024, "PatchEmbed row tile exceeds 64 KB of LDS");
-  const dim3 grid((unsigned)(B * D * H)), block(256);
+  const size_t row_lds = (size_t)Cin * 8 * W * sizeof(float);
+  WF_REQUIRE(row_lds <= 64 * 1024, "PatchEmbed row tile exceeds 64 KB of LDS");
+  // rows per workgroup: up to 4 within 32 KB of LDS, while the grid keeps >= 2048 workgroups
+  static const int rmax = getenv("WF_PE_ROWS") ? atoi(getenv("WF_PE_ROWS")) : 4;
+  int R = 1;
+  while (R * 2 <= rmax && R * 2 <= H && row_lds * R * 2 <= 32 * 1024 &&
+         B * D * cdiv(H, R * 2) >= 2048)
+    R *= 2;
+  const size_t lds = row_lds * R;
+  const dim3 grid((unsigned)(B * D * cdiv(H, R))), block(256);
   hipStream_t s = (hipStream_t)stream;
   const int ci = (int)Cin, co = (int)Cout, d = (int)D, h = (int)H, ww = (int)W;
   switch (Cin) {
-    case 1: hipLaunchKernelGGL(patch_embed_kernel<1>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
-    case 2: hipLaunchKernelGGL(patch_embed_kernel<2>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
-    case 3: hipLaunchKernelGGL(patch_embed_kernel<3>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
-    case 4: hipLaunchKernelGGL(patch_embed_kernel<4>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
-    default: hipLaunchKernelGGL(patch_embed_kernel<0>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww); break;
+    case 1: hipLaunchKernelGGL(patch_embed_kernel<1>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww, R); break;
+    case 2: hipLaunchKernelGGL(patch_embed_kernel<2>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww, R); break;
+    case 3: hipLaunchKernelGGL(patch_embed_kernel<3>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww, R); break;
+    case 4: hipLaunchKernelGGL(patch_embed_kernel<4>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww, R); break;
+    default: hipLaunchKernelGGL(patch_embed_kernel<0>, grid, block, lds, s, x, w, bias, out, ci, co, d, h, ww, R); break;
   }
   return check_launch("wf_patch_embed_fwd");
 }
