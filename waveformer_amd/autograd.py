@@ -289,7 +289,7 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
 
 
 def conv_train(conv: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
-    """A decoder Conv3d / ConvTranspose3d under autograd on the waveformer_amd paths:
+    """A decoder Conv3d / ConvTranspose3d on the waveformer_amd paths (autograd-aware):
     3^3 dense (Conv3dK3), 3^3 depthwise (DWConv3dK3), 1^3 (F.linear over channel-last rows),
     2^3 stride-2 transposed (one GEMM into the 8 sub-voxels).  Other shapes: the module."""
     F = torch.nn.functional

@@ -46,8 +46,8 @@ class HFRefinementRes(nn.Module):
                 and c2.kernel_size == (1, 1, 1) and c2.bias is not None)
 
     def forward(self, x):
-        # under autograd the convs run through wfa.conv_train (HIP depthwise, GEMM 1x1)
-        cv = wfa.conv_train if torch.is_grad_enabled() else (lambda m, t: m(t))
+        # the convs through wfa.conv_train (HIP depthwise, GEMM 1x1; modules for CPU tensors)
+        cv = wfa.conv_train
         r = cv(self.conv2, self.relu(self.norm(cv(self.conv1, x))))
         if self.sigmoid is not None:
             r = self.sigmoid(r)

@@ -65,8 +65,9 @@ class ChannelCalibration(nn.Module):
         self.relu = nn.ReLU()
 
     def forward(self, x):
-        # the convs through wfa.conv_train under autograd (GEMM 1x1s, HIP 3^3), else modules
-        cv = wfa.conv_train if torch.is_grad_enabled() else (lambda m, t: m(t))
+        # the convs through wfa.conv_train (GEMM 1x1s, HIP 3^3; the modules for CPU tensors):
+        # MIOpen picks its naive direct kernels for these NCDHW 6^3 shapes (2 ms a launch)
+        cv = wfa.conv_train
         identity = cv(self.residual, x)
         x = self.relu(self.norm_reduce(cv(self.reduce, x)))
         x = self.relu(self.norm_conv(cv(self.conv, x)))
