@@ -26,7 +26,6 @@
 
 namespace wf {
 
-namespace {
 
 constexpr int WG_TX = 32, WG_TY = 4, WG_HX = 34, WG_XR = 40, WG_HY = 6;
 constexpr int WG_NPOS = WG_TX * WG_TY;           // 128 positions per tile
@@ -251,8 +250,6 @@ int wgrad_nsplit(int64_t ntiles, int64_t Cin, int64_t Cout) {
   ns = std::min<int64_t>(ns, std::max<int64_t>(1, ntiles / 8));
   return (int)ns;
 }
-
-}  // namespace
 
 }  // namespace wf
 

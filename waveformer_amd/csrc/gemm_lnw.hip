@@ -22,7 +22,6 @@
 
 namespace wf {
 
-namespace {
 
 constexpr int LW_RT = 4;           // row tiles (16 rows) per workgroup
 constexpr int LW_NTW = 6;          // column tiles per wave
@@ -203,8 +202,6 @@ void go_lnw(const GemmArgs& g, hipStream_t s) {
                                  : gemm_lnw_kernel<PREC_BF16, KS>;
   hipLaunchKernelGGL(k, grid, dim3(256), 0, s, g);
 }
-
-}  // namespace
 
 int try_launch_gemm_lnw(const GemmArgs& g, hipStream_t s) {
   static const bool off = getenv("WF_GEMM_NO_LNW") != nullptr;  // A/B switch

@@ -23,7 +23,6 @@
 
 namespace wf {
 
-namespace {
 
 constexpr int HF_ZS = 8;  // planes per apply tile
 
@@ -242,8 +241,6 @@ __global__ __launch_bounds__(256) void hf_apply_kernel(HfArgs a) {
     *reinterpret_cast<f32x4*>(ob + off) = xv * g;
   }
 }
-
-}  // namespace
 
 }  // namespace wf
 
