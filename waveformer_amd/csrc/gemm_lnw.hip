@@ -23,12 +23,12 @@
 namespace wf {
 
 
-constexpr int LW_RT = 4;           // row tiles (16 rows) per workgroup
-constexpr int LW_NTW = 6;          // column tiles per wave
-constexpr int LW_N = 4 * LW_NTW * 16;  // 384
-
-template <int P, int KS>
+// LW_NTW column tiles per wave (N = 64 LW_NTW), LW_RT row tiles of 16 rows per workgroup:
+// (6, 4) for N = 384 (stage 2).  (3, 8) for the stage-1 N = 192 measured slower than gemm_rows
+// (909 vs 974 volumes/s: K = 48 pads to two 32-wide K-steps and the A staging is exposed)
+template <int P, int KS, int LW_NTW, int LW_RT>
 __global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
+  constexpr int LW_N = 4 * LW_NTW * 16;
   constexpr bool SPLIT = P == PREC_SPLIT;
   constexpr int NPL = SPLIT ? 2 : 1;
   constexpr int K32 = KS * 32;
@@ -194,28 +194,32 @@ __global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
   }
 }
 
-template <int KS>
+template <int KS, int NTW, int RT>
 void go_lnw(const GemmArgs& g, hipStream_t s) {
-  const dim3 grid((unsigned)cdiv(g.M, LW_RT * 16));
-  auto k = g.prec == PREC_SPLIT  ? gemm_lnw_kernel<PREC_SPLIT, KS>
-           : g.prec == PREC_FP16 ? gemm_lnw_kernel<PREC_FP16, KS>
-                                 : gemm_lnw_kernel<PREC_BF16, KS>;
+  const dim3 grid((unsigned)cdiv(g.M, RT * 16));
+  auto k = g.prec == PREC_SPLIT  ? gemm_lnw_kernel<PREC_SPLIT, KS, NTW, RT>
+           : g.prec == PREC_FP16 ? gemm_lnw_kernel<PREC_FP16, KS, NTW, RT>
+                                 : gemm_lnw_kernel<PREC_BF16, KS, NTW, RT>;
   hipLaunchKernelGGL(k, grid, dim3(256), 0, s, g);
 }
 
 int try_launch_gemm_lnw(const GemmArgs& g, hipStream_t s) {
   static const bool off = getenv("WF_GEMM_NO_LNW") != nullptr;  // A/B switch
   if (off || g.epi != EPI_LN_GELU || g.a_map != MAP_IDENTITY || g.a_bf16 || g.a_gelu ||
-      !(g.a_ln == LN_NONE || g.a_ln == LN_GIVEN) || g.N != LW_N || g.a_C != g.K ||
-      g.K % 8 != 0 || g.M >= ((int64_t)1 << 31) || g.ldo < g.N || g.ldo % 4 != 0)
+      !(g.a_ln == LN_NONE || g.a_ln == LN_GIVEN) || g.a_C != g.K || g.K % 8 != 0 ||
+      g.M >= ((int64_t)1 << 31) || g.ldo < g.N || g.ldo % 4 != 0)
     return 0;
-  switch ((g.K + 31) / 32) {
-    case 1: go_lnw<1>(g, s); return 1;
-    case 2: go_lnw<2>(g, s); return 1;
-    case 3: go_lnw<3>(g, s); return 1;
-    case 4: go_lnw<4>(g, s); return 1;
-    default: return 0;
+  const int ks = (g.K + 31) / 32;
+  if (g.N == 384) {
+    switch (ks) {
+      case 1: go_lnw<1, 6, 4>(g, s); return 1;
+      case 2: go_lnw<2, 6, 4>(g, s); return 1;
+      case 3: go_lnw<3, 6, 4>(g, s); return 1;
+      case 4: go_lnw<4, 6, 4>(g, s); return 1;
+      default: return 0;
+    }
   }
+  return 0;
 }
 
 }  // namespace wf
