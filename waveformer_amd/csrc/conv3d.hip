@@ -55,7 +55,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   constexpr int TX = 16 * NT, TY = 4, HX = TX + 2, HY = TY + 2;
   constexpr int NPOS = 3 * HY * HX;
   constexpr int PS = kConvCC;                       // bf16 per position per plane
-  constexpr int NFRAG = kConvKS * 2 * CO_T;          // weight fragments (1 KB each) per chunk
+  constexpr int NPL = SPLIT ? 2 : 1;                 // operand planes staged (lo only for SPLIT)
+  constexpr int NFRAG = kConvKS * NPL * CO_T;        // weight fragments (1 KB each) per chunk
   constexpr int NW = (NFRAG * 64 + 255) / 256;       // 16-B weight pieces per thread
   constexpr int QN = kConvCC / 4, PSTEP = 256 / QN;  // float4 per position, positions per pass
   constexpr int NJ = (NPOS * QN + 255) / 256;        // input float4 per thread
@@ -63,8 +64,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   // [step][plane][m][lane][8] bf16 in MFMA operand order (a wave reads 1 KB contiguous)
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* s_hi = lds;
-  uint16_t* s_lo = lds + NPOS * PS;
-  uint16_t* s_w = lds + 2 * NPOS * PS;
+  uint16_t* s_lo = lds + NPOS * PS;                  // SPLIT only
+  uint16_t* s_w = lds + NPL * NPOS * PS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l15 = lane & 15, g4 = lane >> 4;
 
@@ -142,12 +143,10 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
     for (int w = 0; w < NW; ++w) {
       const int i = min(tid + 256 * w, NFRAG * 64 - 1);
       const int f = i >> 6, ln = i & 63;
-      const int m = f % CO_T, sp = f / CO_T;  // sp = step * 2 + plane
-      const int st = sp >> 1, pl = sp & 1;
+      const int m = f % CO_T, sp = f / CO_T;  // sp = step * NPL + plane
+      const int st = sp / NPL, pl = sp - st * NPL;
       const int64_t frag = ((int64_t)(ch * kConvKS + st) * 2 + pl) * cblk + co0 / 16 + m;
-      sw[w] = (SPLIT || pl == 0)
-                  ? *reinterpret_cast<const bf16x8*>(a.w + (frag * 64 + ln) * 8)
-                  : zero8;
+      sw[w] = *reinterpret_cast<const bf16x8*>(a.w + (frag * 64 + ln) * 8);
     }
   };
   auto commit = [&](int ch) {
@@ -190,8 +189,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
       bf16x8 bh[NT], bl[NT], wh[CO_T], wl[CO_T];
 #pragma unroll
       for (int m = 0; m < CO_T; ++m) {
-        wh[m] = *reinterpret_cast<const bf16x8*>(lw + ((s * 2 + 0) * CO_T + m) * 1024);
-        wl[m] = SPLIT ? *reinterpret_cast<const bf16x8*>(lw + ((s * 2 + 1) * CO_T + m) * 1024)
+        wh[m] = *reinterpret_cast<const bf16x8*>(lw + ((s * NPL + 0) * CO_T + m) * 1024);
+        wl[m] = SPLIT ? *reinterpret_cast<const bf16x8*>(lw + ((s * NPL + NPL - 1) * CO_T + m) * 1024)
                       : zero8;
       }
 #pragma unroll
@@ -307,7 +306,10 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   a.tiles_y = (int)cdiv(a.H, 4);
   a.nblocks = (int64_t)a.B * a.D * a.tiles_y * a.tiles_x;
   if (a.nblocks >= ((int64_t)1 << 31)) return fail(WF_E_SHAPE, "wf_conv3d_k3_fwd: too many tiles");
-  const size_t lds = ((size_t)2 * 3 * 6 * (TX + 2) * kConvCC + (size_t)kConvKS * 2 * CO_T * 512) *
+  // operand planes staged: hi + lo for the split, hi only otherwise (half the LDS: twice the
+  // workgroups per CU for bf16 / fp16)
+  const size_t npl = prec == PREC_SPLIT ? 2 : 1;
+  const size_t lds = (npl * 3 * 6 * (TX + 2) * kConvCC + (size_t)kConvKS * npl * CO_T * 512) *
                      sizeof(uint16_t);
   // small grids (the 8^3 / 16^3 decoder convs): split the Cin chunks over blockIdx.z so the
   // launch covers the 256 CUs; partial sums meet in the zeroed output through fp32 atomics

@@ -358,6 +358,303 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Wave-specialised variant (same math, same tile): 6 "D" waves run the depthwise scatter while
+// 6 "E" waves run everything else one output plane behind -- LN2 + GELU + split of plane z-2,
+// its fc MFMAs and store, the staging of the next h1 plane -- so the two VALU-heavy phases
+// overlap instead of taking turns between barriers.  Per input plane p, two barriers:
+//   phase 1:  D  scatter rows 0..1 of plane p
+//             E  epilogue rows of z = p-2, LN2 + GELU of h2 tile (p-2) in place (waves 6..9:
+//                8 lanes x 24 channels)
+//   phase 2:  D  scatter rows 2..5 of plane p -> output plane p-1 complete -> h2 tile (p-1)
+//             E  commit plane p+1, fetch plane p+2, fc GEMM of tile (p-2) (6 waves: 2 row x
+//                3 column tiles, weights in VGPRs) + bias + Q4 residual + store
+// h2 tiles are double-buffered ((p-1) is written while (p-2) is read); 144 KB of LDS (the fc
+// weights live in the E waves' registers instead).
+// ---------------------------------------------------------------------------------------
+template <int P, typename T>
+__global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
+  constexpr int C = 48, HID = 192, TY = 4, TX = 8;
+  constexpr bool SPLIT = P == PREC_SPLIT;
+  typedef DwFcCfg<C, HID, TY, TX> K;
+  typedef H1Load<T> L;
+  constexpr int NPAIR = HID / 2;                  // 96 channel pairs
+  constexpr int NE = 384;                         // E threads
+  constexpr int NLDE = (K::PP * K::NV + NE - 1) / NE;  // staged f32x4 per E thread (8)
+  constexpr int H2F = K::NPOS * K::HS;            // one h2 tile (floats)
+  constexpr int LNL = 8, LNC = HID / LNL;         // LN2: 8 lanes x 24 channels per position
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* planes = lds;                                  // [2][PP][HID]
+  float* h2b = lds + 2 * K::PLANE_F;                     // [2][NPOS][HS]
+  float* lnw = h2b + 2 * H2F;                            // [HID] (halved: GELU from x / 2)
+  float* lnb = lnw + HID;
+  float* fcb = lnb + HID;                                // [C]
+  float* n2w = fcb + C;
+  float* n2b = n2w + C;
+
+  const int tid = threadIdx.x;
+  const int wid = tid >> 6;
+  const bool isD = wid < 6;
+  const int D = a.D, H = a.H, W = a.W;
+  const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY, nzs = (D + a.ZS - 1) / a.ZS;
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int xt = t % ntx;
+  t /= ntx;
+  const int yt = t % nty;
+  t /= nty;
+  const int zt = t % nzs;
+  const int b = t / nzs;
+  const int x0 = xt * TX, y0 = yt * TY, z0 = zt * a.ZS, z1 = min(z0 + a.ZS, D);
+  const int64_t plane_sz = (int64_t)H * W;
+
+  for (int i = tid; i < HID; i += K::NTH) {
+    lnw[i] = 0.5f * a.ln2_w[i];
+    lnb[i] = 0.5f * a.ln2_b[i];
+  }
+  for (int i = tid; i < C; i += K::NTH) {
+    fcb[i] = a.fc_b ? a.fc_b[i] : 0.f;
+    n2w[i] = a.stats ? a.n2_w[i] : 1.f;
+    n2b[i] = a.stats ? a.n2_b[i] : 0.f;
+  }
+  // depthwise weights, coalesced into the (not yet used) plane buffer
+  for (int i = tid; i < HID * 27; i += K::NTH) planes[i] = a.dw_w[i];
+  __syncthreads();
+
+  const T* src = reinterpret_cast<const T*>(a.h1) + (int64_t)b * D * H * W * HID;
+  const int64_t plane_elems = (int64_t)H * W * HID;
+  const float bs = a.bscale ? a.bscale[b] : 1.f;
+
+  if (isD) {
+    // ================================ D waves: depthwise scatter ==========================
+    const int cp = tid % NPAIR, xg = tid / NPAIR;  // columns xg and xg + 4
+    f32x2 w2[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k)
+      w2[k] = f32x2{planes[(2 * cp) * 27 + k], planes[(2 * cp + 1) * 27 + k]};
+    const f32x2 bias2 = f32x2{a.dw_b[2 * cp], a.dw_b[2 * cp + 1]};
+    f32x2 aA[2][TY], aB[2][TY], aC[2][TY];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int o = 0; o < TY; ++o) aA[c][o] = aB[c][o] = aC[c][o] = f32x2{0.f, 0.f};
+    __syncthreads();  // (prologue) weights read out of the plane buffer
+    __syncthreads();  // (prologue) planes z0-1 committed
+    auto rows = [&](const float* cur, int r_lo, int r_hi) {
+#pragma unroll
+      for (int r = 0; r < K::PY; ++r) {
+        if (r < r_lo || r >= r_hi) continue;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float* Pin = cur + (xg + 4 * c) * HID + 2 * cp;
+          const f32x2 v0 = *reinterpret_cast<const f32x2*>(Pin + (r * K::PX + 0) * HID);
+          const f32x2 v1 = *reinterpret_cast<const f32x2*>(Pin + (r * K::PX + 1) * HID);
+          const f32x2 v2 = *reinterpret_cast<const f32x2*>(Pin + (r * K::PX + 2) * HID);
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            const int o = r - ky;
+            if (o < 0 || o >= TY) continue;
+            const f32x2* w0 = w2 + ky * 3;
+            aC[c][o] = w0[2] * v2 + (w0[1] * v1 + (w0[0] * v0 + aC[c][o]));
+            aB[c][o] = w0[11] * v2 + (w0[10] * v1 + (w0[9] * v0 + aB[c][o]));
+            aA[c][o] = w0[20] * v2 + (w0[19] * v1 + (w0[18] * v0 + aA[c][o]));
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one input row in flight at a time (VGPRs)
+      }
+    };
+    for (int p = z0 - 1; p <= z1 + 1; ++p) {
+      const bool live = p <= z1;
+      const float* cur = planes + ((p - z0 + 1) & 1) * K::PLANE_F;
+      if (live) rows(cur, 0, a.ws_split);
+      __syncthreads();  // 1 -> 2
+      if (live) {
+        rows(cur, a.ws_split, K::PY);
+        const int zo = p - 1;
+        if (zo >= z0) {
+          float* h2t = h2b + ((zo - z0) & 1) * H2F;
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int o = 0; o < TY; ++o) {
+              f32x2 h = aA[c][o] + bias2;
+              if (sizeof(T) == 2) {
+                h.x = bf2f(f2bf(h.x));
+                h.y = bf2f(f2bf(h.y));
+              }
+              *reinterpret_cast<f32x2*>(h2t + (o * TX + xg + 4 * c) * K::HS + 2 * cp) = h;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int o = 0; o < TY; ++o) {
+            aA[c][o] = aB[c][o];
+            aB[c][o] = aC[c][o];
+            aC[c][o] = f32x2{0.f, 0.f};
+          }
+      }
+      __syncthreads();  // 2 -> next 1
+    }
+    return;
+  }
+
+  // ================================== E waves ============================================
+  const int et = tid - NE, ewid = et >> 6, eln = et & 63;
+  const int l15 = eln & 15, g4 = eln >> 4;
+  const int rt = ewid / 3, ct = ewid % 3;  // fc tile of this wave
+  // fc weights in registers: A operand rows ct*16 + l15, k = ks*32 + 8 g4
+  bf16x8 fwh[HID / 32], fwl[HID / 32];
+  {
+    const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint16_t* wr = a.fc + (size_t)(ct * 16 + l15) * HID + 8 * g4;
+#pragma unroll
+    for (int ks = 0; ks < HID / 32; ++ks) {
+      fwh[ks] = *reinterpret_cast<const bf16x8*>(wr + ks * 32);
+      fwl[ks] = SPLIT ? *reinterpret_cast<const bf16x8*>(wr + (size_t)C * HID + ks * 32) : z8;
+    }
+  }
+  // h1 plane staging: item j -> (haloed position, 4-channel vector); offsets fixed per tile
+  int off[NLDE];
+  unsigned okmask = 0;
+#pragma unroll
+  for (int j = 0; j < NLDE; ++j) {
+    const int i = min(j * NE + et, K::PP * K::NV - 1);
+    const int pos = i / K::NV, v = i - pos * K::NV;
+    const int yy = y0 - 1 + pos / K::PX, xx = x0 - 1 + pos % K::PX;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    const int yc = min(max(yy, 0), H - 1), xc = min(max(xx, 0), W - 1);
+    off[j] = (yc * W + xc) * HID + 4 * v;
+    okmask |= (ok ? 1u : 0u) << j;
+  }
+  typename L::raw stg[NLDE];
+  auto fetch = [&](int p) {
+    const T* base = src + (int64_t)min(max(p, 0), D - 1) * plane_elems;
+#pragma unroll
+    for (int j = 0; j < NLDE; ++j) stg[j] = L::load(base, off[j]);
+  };
+  auto commit = [&](int p, float* dst) {
+    const bool pz = p >= 0 && p < D;
+#pragma unroll
+    for (int j = 0; j < NLDE; ++j) {
+      const int i = j * NE + et;
+      const bool ok = pz && ((okmask >> j) & 1u);
+      const f32x4 u = L::up(stg[j]);
+      if (i < K::PP * K::NV)
+        *reinterpret_cast<f32x4*>(dst + (size_t)i * 4) = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  const int lp = rt * 16 + l15;              // tile position of this lane's fc row
+  const int yo = y0 + lp / TX, xo = x0 + lp % TX;
+  const bool rv = yo < H && xo < W;
+  const int col = ct * 16 + 4 * g4;
+  const float* sbase = a.stats ? a.stats : a.x;
+  f32x4 xr = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x2 es = f32x2{0.f, 1.f};
+
+  fetch(z0 - 1);
+  __syncthreads();  // (prologue) weights read out of the plane buffer
+  commit(z0 - 1, planes);
+  fetch(z0);
+  __syncthreads();  // (prologue) plane z0-1 visible
+  for (int p = z0 - 1; p <= z1 + 1; ++p) {
+    const int zo = p - 2;  // output plane this iteration finishes
+    const bool epi = zo >= z0 && zo < z1;
+    // ---- phase 1: epilogue rows of plane p-2, LN2 + GELU of its h2 tile
+    asm volatile("" ::"v"(xr), "v"(es));
+    if (epi) {
+      const int64_t gpos = (int64_t)b * D * plane_sz + (int64_t)zo * plane_sz +
+                           (int64_t)min(yo, H - 1) * W + min(xo, W - 1);
+      xr = *reinterpret_cast<const f32x4*>(a.x + gpos * C + col);
+      es = *reinterpret_cast<const f32x2*>(sbase + 2 * gpos);
+    }
+    float* h2t = h2b + ((zo - z0) & 1) * H2F;
+    if (epi && ewid < 4) {
+      int ltid = et;
+      asm volatile("" : "+v"(ltid));
+      const int pos = ltid / LNL, g = ltid % LNL;
+      float* row = h2t + pos * K::HS;
+      float v[LNC];
+#pragma unroll
+      for (int j = 0; j < LNC / 4; ++j) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(row + g * LNC + 4 * j);
+        v[4 * j] = u.x;
+        v[4 * j + 1] = u.y;
+        v[4 * j + 2] = u.z;
+        v[4 * j + 3] = u.w;
+      }
+      float sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < LNC; ++j) sm += v[j];
+      const float mean = group_sum<LNL>(sm) * (1.f / HID);
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < LNC; ++j) {
+        const float d = v[j] - mean;
+        q += d * d;
+      }
+      const float rstd = rsqrtf(group_sum<LNL>(q) * (1.f / HID) + a.eps2);
+      const float nmr = -mean * rstd;
+      uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
+#pragma unroll
+      for (int j = 0; j < LNC / 4; ++j) {
+        const int c = g * LNC + 4 * j;
+        const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + c);
+        const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + c);
+        const f32x4 y = gelu_half4((f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]} *
+                                    rstd + nmr) * lw4 + lb4);
+        bf16x4 hi4, lo4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint16_t hb = op_cvt<P>(y[e]);
+          hi4[e] = (short)hb;
+          lo4[e] = op_lo<P>(y[e], hb);
+        }
+        *reinterpret_cast<bf16x4*>(rowh + c) = hi4;
+        if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + c) = lo4;
+      }
+    }
+    __syncthreads();  // 1 -> 2: LN rows of tile (p-2) visible
+    // ---- phase 2: commit plane p+1 into the free buffer (D is done with plane p-1 since the
+    // last barrier of iteration p-1), fetch p+2, fc GEMM of tile (p-2) + residual + store
+#pragma unroll
+    for (int j = 0; j < NLDE; ++j) asm volatile("" ::"v"(stg[j]));
+    if (p + 1 <= z1) commit(p + 1, planes + ((p - z0) & 1) * K::PLANE_F);
+    if (p + 2 <= z1) fetch(p + 2);
+    if (epi) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)lp * (2 * K::HS);
+#pragma unroll
+      for (int ks = 0; ks < HID / 32; ++ks) {
+        const int k = ks * 32 + 8 * g4;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bh + k);
+        if (SPLIT) {
+          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
+          acc = mma32<P>(fwh[ks], bl, acc);
+          acc = mma32<P>(fwl[ks], bh, acc);
+        }
+        acc = mma32<P>(fwh[ks], bh, acc);
+      }
+      f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+      if (a.stats) {
+        const f32x4 lw = *reinterpret_cast<const f32x4*>(n2w + col);
+        const f32x4 lb = *reinterpret_cast<const f32x4*>(n2b + col);
+        const f32x4 n2 = (xr - es.x) * es.y * lw + lb;
+        v = xr + (n2 + v) * bs;
+      } else {
+        v = xr + v * bs;
+      }
+      if (rv) {
+        const int64_t gpos = (int64_t)b * D * plane_sz + (int64_t)zo * plane_sz +
+                             (int64_t)yo * W + xo;
+        *reinterpret_cast<f32x4*>(a.out + gpos * C + col) = v;
+      }
+    }
+    __syncthreads();  // 2 -> next 1
+  }
+}
+
 template <int TY, int TX>
 static int go_dwfc(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks) {
   constexpr int C = 48, HID = 192;
@@ -379,9 +676,37 @@ static int go_dwfc(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks) {
   return check_launch("ffn_dwfc");
 }
 
+static int go_dwfc_ws(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks) {
+  constexpr int C = 48, HID = 192, TY = 4, TX = 8;
+  typedef DwFcCfg<C, HID, TY, TX> K;
+  DwFcArgs g = a;
+  const int64_t base = (int64_t)g.B * cdiv(g.H, TY) * cdiv(g.W, TX);
+  int ZS = g.D;
+  while (ZS > 8 && base * cdiv(g.D, ZS) < min_blocks) ZS = (ZS + 1) / 2;
+  g.ZS = ZS;
+  const int64_t blocks = base * cdiv(g.D, ZS);
+  const size_t lds = (size_t)(2 * K::PLANE_F + 2 * K::H2_F + 2 * HID + 3 * C) * 4;
+  // D's input rows split over the two phases: rows 0..1 (3 of the 12 row-tap FMA groups)
+  // alongside E's LN2 + GELU, rows 2..5 alongside E's commit + fetch + fc (B = 8 stage 1,
+  // split 0..5: 916, 894, 879-888, 903, 934, 952 us; the classic kernel 1072 us)
+  static const int split = getenv("WF_FFN_WS_SPLIT") ? atoi(getenv("WF_FFN_WS_SPLIT")) : 2;
+  g.ws_split = split;
+  void (*kern)(DwFcArgs) = prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>
+                           : prec == PREC_FP16 ? ffn_dwfc_ws_kernel<PREC_FP16, float>
+                                               : ffn_dwfc_ws_kernel<PREC_BF16, uint16_t>;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(K::NTH), lds, s, g);
+  return check_launch("ffn_dwfc_ws");
+}
+
 int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s) {
   // 4 x 8 tiles: 12 waves (the register-file limit at ~168 VGPRs) and ~154 KB of LDS, one
   // workgroup per CU.  (4 x 4 tiles with two 6-wave workgroups per CU measured 1.5x slower.)
+  // Default: the wave-specialised kernel (947 vs 1072 us per stage-1 launch at B = 8);
+  // WF_FFN_DWFC_CLASSIC=1 selects the all-waves-in-lockstep original for A/B
+  static const bool classic = getenv("WF_FFN_DWFC_CLASSIC") != nullptr;
+  if (!classic) return go_dwfc_ws(a, prec, s, 1024);
   return go_dwfc<4, 8>(a, prec, s, 1024);
 }
 

@@ -146,6 +146,7 @@ struct DwFcArgs {
   const float* ln1_b;
   float eps1;
   int dbg;               // timing experiments only (WF_FFN_DBG): bit mask of phases skipped
+  int ws_split;          // wave-specialised ffn_dwfc: D rows of a plane in phase 1 (1..5)
 };
 int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s);
 // ---- the whole CCF_FFN + norm2 + Q4 residual in one kernel for C = 48, hidden = 192: the
