@@ -45,7 +45,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 # bench op name -> kernel-name substring in the PMC summary (profiles/*pmc*.json)
 PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_fused_kernel" if os.environ.get("WF_FFN_FUSED")
-              else "ffn_dwfc_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
+              else "ffn_dwfc_kernel" if os.environ.get("WF_FFN_DWFC_CLASSIC")
+              else "ffn_dwfc_ws_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
               "window_attention": "attn_core_kernel",
               "msfuse": "msfuse", "proj_out": "proj_out"}
 
