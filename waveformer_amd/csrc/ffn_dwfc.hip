@@ -467,10 +467,11 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
     for (int p = z0 - 1; p <= z1 + 1; ++p) {
       const bool live = p <= z1;
       const float* cur = planes + ((p - z0 + 1) & 1) * K::PLANE_F;
-      if (live) rows(cur, 0, a.ws_split);
+      const bool dscat = !(a.dbg & 1);  // timing experiments only (WF_FFN_DBG)
+      if (live && dscat) rows(cur, 0, a.ws_split);
       __syncthreads();  // 1 -> 2
       if (live) {
-        rows(cur, a.ws_split, K::PY);
+        if (dscat) rows(cur, a.ws_split, K::PY);
         const int zo = p - 1;
         if (zo >= z0) {
           float* h2t = h2b + ((zo - z0) & 1) * H2F;
@@ -570,7 +571,7 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
       es = *reinterpret_cast<const f32x2*>(sbase + 2 * gpos);
     }
     float* h2t = h2b + ((zo - z0) & 1) * H2F;
-    if (epi && ewid < 4) {
+    if (epi && ewid < 4 && !(a.dbg & 2)) {
       int ltid = et;
       asm volatile("" : "+v"(ltid));
       const int pos = ltid / LNL, g = ltid % LNL;
@@ -620,9 +621,9 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
     // last barrier of iteration p-1), fetch p+2, fc GEMM of tile (p-2) + residual + store
 #pragma unroll
     for (int j = 0; j < NLDE; ++j) asm volatile("" ::"v"(stg[j]));
-    if (p + 1 <= z1) commit(p + 1, planes + ((p - z0) & 1) * K::PLANE_F);
-    if (p + 2 <= z1) fetch(p + 2);
-    if (epi) {
+    if (p + 1 <= z1 && !(a.dbg & 8)) commit(p + 1, planes + ((p - z0) & 1) * K::PLANE_F);
+    if (p + 2 <= z1 && !(a.dbg & 8)) fetch(p + 2);
+    if (epi && !(a.dbg & 4)) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
       const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)lp * (2 * K::HS);
 #pragma unroll
@@ -691,6 +692,8 @@ static int go_dwfc_ws(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks
   // split 0..5: 916, 894, 879-888, 903, 934, 952 us; the classic kernel 1072 us)
   static const int split = getenv("WF_FFN_WS_SPLIT") ? atoi(getenv("WF_FFN_WS_SPLIT")) : 2;
   g.ws_split = split;
+  static const int dbg = getenv("WF_FFN_DBG") ? atoi(getenv("WF_FFN_DBG")) : 0;
+  g.dbg = dbg;  // timing experiments only: bit mask of phases skipped (results invalid)
   void (*kern)(DwFcArgs) = prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>
                            : prec == PREC_FP16 ? ffn_dwfc_ws_kernel<PREC_FP16, float>
                                                : ffn_dwfc_ws_kernel<PREC_BF16, uint16_t>;
