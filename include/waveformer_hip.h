@@ -195,6 +195,20 @@ int wf_hf_refine_fwd(const float* const* details, int64_t ldb, const float* dw_w
                      void* workspace, int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
                      void* stream);
 
+/* Backward of y = LeakyReLU(slope)((a - mean_a) * rstd_a + r') (wf_norm_act_cl; training of
+ * UnetResBlock / UnetBasicBlock): dz = dy * (y > 0 ? 1 : slope),
+ *   da = rstd_a * (dz - mean_P(dz) - xhat_a * mean_P(dz * xhat_a)),
+ *   dr = rstd_r * (dz - mean_P(dz) - xhat_r * mean_P(dz * xhat_r)) with stats_r (normed
+ *   residual, r given), dz without (plain residual), not written when dr == NULL.
+ * Channel-last operands (positions ld* floats apart), stats (B, 2, C) {mean, rstd} as
+ * wf_instnorm_stats_cl returns them.  workspace: wf_norm_act_bwd_workspace_bytes(B, C).      */
+int64_t wf_norm_act_bwd_workspace_bytes(int64_t B, int64_t C);
+int wf_norm_act_bwd_cl(const float* dy, int64_t ldd, const float* y, int64_t ldy,
+                       const float* a, int64_t lda, const float* stats_a, const float* r,
+                       int64_t ldr, const float* stats_r, float* da, int64_t ldda, float* dr,
+                       int64_t lddr, int64_t B, int64_t C, int64_t P, float slope,
+                       void* workspace, void* stream);
+
 /* nn.Upsample(scale_factor=s, mode='trilinear', align_corners) of a channel-last tensor
  * (B, d, h, w, C) -> (B, D, H, W, C), PyTorch's upsample_trilinear3d index arithmetic: the
  * decoder's ProjectionUpsample (network_models/wave_helper.py:33-81, align_corners=True).    */

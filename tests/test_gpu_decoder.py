@@ -265,3 +265,32 @@ def test_conv3d_k3_wgrad_vs_cpu(B, Cin, Cout, S):
     got = ops.conv3d_k3_wgrad(xc, gc, (Cout, Cin, 3, 3, 3))
     assert C.rel_l2(got, want) <= 1e-5
     assert torch.equal(got, ops.conv3d_k3_wgrad(xc, gc, (Cout, Cin, 3, 3, 3)))
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("B,C_,S", [(2, 48, (9, 10, 11)), (1, 96, (4, 5, 6)), (2, 16, (16, 3, 7))])
+def test_norm_act_autograd_vs_torch(mode, B, C_, S):
+    """autograd.NormActFn (InstanceNorm3d(affine=False) + residual (none / plain / normed) +
+    LeakyReLU, forward wf_instnorm_stats_cl + wf_norm_act_cl, backward wf_norm_act_bwd_cl)
+    against the framework's InstanceNorm3d / LeakyReLU in fp64 on the CPU: forward and both
+    input gradients rel-L2 <= 1e-5."""
+    from waveformer_amd import autograd as wfa
+    a = seeded_randn((B, C_) + S, 61) * 2 + 0.3
+    r = seeded_randn((B, C_) + S, 62) * 1.5 - 0.2
+    gy = seeded_randn((B, C_) + S, 63)
+    ad, rd = a.double().requires_grad_(True), r.double().requires_grad_(True)
+    z = F.instance_norm(ad, eps=1e-5)
+    if mode == 1:
+        z = z + rd
+    elif mode == 2:
+        z = z + F.instance_norm(rd, eps=1e-5)
+    want = F.leaky_relu(z, 0.01)
+    want.backward(gy.double())
+    ac = a.cuda().contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+    rc = r.cuda().contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+    got = wfa.norm_act(ac, rc if mode else None, 0.01, 1e-5, 1e-5, normed_residual=mode == 2)
+    got.backward(gy.cuda())
+    assert C.rel_l2(got, want) <= 1e-5
+    assert C.rel_l2(ac.grad, ad.grad) <= 1e-5
+    if mode:
+        assert C.rel_l2(rc.grad, rd.grad) <= 1e-5

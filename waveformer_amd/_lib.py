@@ -49,6 +49,9 @@ SIGNATURES = {
     "wf_conv3d_k3_wgrad_workspace_bytes": (_I64, [_I64] * 6),
     "wf_conv3d_k3_wgrad": (_I, [_P, _I64, _P, _I64, _P, _I, _P, _I64, _I64, _I64, _I64, _I64,
                                 _I64, _P]),
+    "wf_norm_act_bwd_workspace_bytes": (_I64, [_I64, _I64]),
+    "wf_norm_act_bwd_cl": (_I, [_P, _I64, _P, _I64, _P, _I64, _P, _P, _I64, _P, _P, _I64, _P, _I64,
+                                _I64, _I64, _I64, _F, _P, _P]),
     "wf_hf_refine_workspace_bytes": (_I64, [_I64, _I64]),
     "wf_hf_refine_fwd": (_I, [_P, _I64, _P, _P, _P, _P, _F, _P, _P, _I, _P, _P, _I64, _I64,
                               _I64, _I64, _I64, _P]),

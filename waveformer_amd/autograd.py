@@ -319,3 +319,48 @@ def conv_train(conv: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
             y = y + conv.bias
         return y.permute(0, 4, 1, 2, 3)
     return conv(x)
+
+
+# ------------------------------------------------------------------------------------------
+# InstanceNorm3d(affine=False) + residual + LeakyReLU of UnetResBlock / UnetBasicBlock in
+# training: the forward's HIP statistics + fused pass, the backward's two HIP passes
+# (wf_norm_act_bwd_cl) -- instead of the framework's layout copies, batch-norm kernels,
+# LeakyReLU and add, each a full-resolution pass of its own
+# ------------------------------------------------------------------------------------------
+class NormActFn(torch.autograd.Function):
+    """y = LeakyReLU(slope)(IN_eps(a) + r'), r' = IN_eps_r(r) (mode 2), r (mode 1) or 0."""
+
+    @staticmethod
+    def forward(ctx, a, r, slope, eps, eps_r, mode):
+        a = ops.to_cl(a)
+        sa = ops.instnorm_stats(a, eps)
+        sr = None
+        if mode == 2:
+            r = ops.to_cl(r)
+            sr = ops.instnorm_stats(r, eps_r)
+        y = ops.norm_act(a, sa, r if mode else None, sr, slope)
+        ctx.save_for_backward(a, r if mode == 2 else None, y, sa, sr)
+        ctx.slope, ctx.mode = slope, mode
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        a, r, y, sa, sr = ctx.saved_tensors
+        g = ops.to_cl(g)
+        B, C, D, H, W = a.shape
+        P = D * H * W
+        da = ops.empty_cl(B, C, D, H, W, a.device)
+        want_r = ctx.mode and ctx.needs_input_grad[1]
+        dr = ops.empty_cl(B, C, D, H, W, a.device) if want_r else None
+        ws = torch.empty(_lib.query("wf_norm_act_bwd_workspace_bytes", B, C), dtype=torch.uint8,
+                         device=a.device)
+        _lib.call("wf_norm_act_bwd_cl", g.data_ptr(), ops.cl_ld(g), y.data_ptr(), ops.cl_ld(y),
+                  a.data_ptr(), ops.cl_ld(a), sa.data_ptr(), _p(r), ops.cl_ld(r) if r is not None
+                  else 0, _p(sr), da.data_ptr(), C, _p(dr), C if dr is not None else 0, B, C, P,
+                  float(ctx.slope), ws.data_ptr(), _s())
+        return da, dr, None, None, None, None
+
+
+def norm_act(a, r=None, slope=0.01, eps=1e-5, eps_r=1e-5, normed_residual=False):
+    mode = 0 if r is None else (2 if normed_residual else 1)
+    return NormActFn.apply(a, r, float(slope), float(eps), float(eps_r), mode)

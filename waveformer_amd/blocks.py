@@ -140,10 +140,27 @@ class UnetResBlock(nn.Module):
                 return ops.norm_act(out, s2, res, ops.instnorm_stats(res, self.norm3.eps),
                                     slope=slope, out=out)
             return ops.norm_act(out, s2, x, slope=slope, out=out)
+        if self._train_ok(inp):
+            # training on the GPU: convolutions through wfa.conv_train, each InstanceNorm +
+            # residual + LeakyReLU as one fused HIP op with a HIP backward (wfa.NormActFn)
+            slope = self.lrelu.negative_slope
+            h = wfa.norm_act(self.conv1(inp), slope=slope, eps=self.norm1.eps)
+            out = self.conv2(h)
+            if self.downsample:
+                return wfa.norm_act(out, self.conv3(inp), slope, self.norm2.eps, self.norm3.eps,
+                                    normed_residual=True)
+            return wfa.norm_act(out, inp, slope, self.norm2.eps)
         out = self.lrelu(self.norm1(self.conv1(inp)))
         out = self.norm2(self.conv2(out))
         res = self.norm3(self.conv3(inp)) if self.downsample else inp
         return self.lrelu(out + res)
+
+    def _train_ok(self, inp) -> bool:
+        return (inp.is_cuda and inp.dtype == torch.float32 and inp.dim() == 5
+                and inp.shape[1] % 4 == 0 and self.conv1.conv.out_channels % 4 == 0
+                and _in_ok(self.norm1) and _in_ok(self.norm2)
+                and (not self.downsample or _in_ok(self.norm3))
+                and type(self.lrelu) is nn.LeakyReLU and self.lrelu.negative_slope > 0)
 
 
 class UnetBasicBlock(nn.Module):
@@ -169,6 +186,12 @@ class UnetBasicBlock(nn.Module):
             out, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
                                     norm_eps=self.norm2.eps)
             return ops.norm_act(out, s2, slope=slope, out=out)
+        if (inp.is_cuda and inp.dtype == torch.float32 and inp.dim() == 5
+                and self.conv1.conv.out_channels % 4 == 0 and _in_ok(self.norm1)
+                and _in_ok(self.norm2) and self.lrelu.negative_slope > 0):
+            slope = self.lrelu.negative_slope  # training: fused HIP norm + LeakyReLU
+            h = wfa.norm_act(self.conv1(inp), slope=slope, eps=self.norm1.eps)
+            return wfa.norm_act(self.conv2(h), slope=slope, eps=self.norm2.eps)
         out = self.lrelu(self.norm1(self.conv1(inp)))
         return self.lrelu(self.norm2(self.conv2(out)))
 

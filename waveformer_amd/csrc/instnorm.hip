@@ -99,9 +99,170 @@ __global__ __launch_bounds__(256) void norm_act_kernel(
   }
 }
 
+// ---- backward of y = act((a - mean_a) * rstd_a + r'), act = LeakyReLU(slope) (training of
+// UnetResBlock / UnetBasicBlock).  dz = dy * (y > 0 ? 1 : slope) -- the sign of y is the sign
+// of the pre-activation for slope > 0, as the in-place LeakyReLU's own backward uses it.
+// Pass 1: per (b, c) the sums of dz, dz * xhat_a and (normed residual) dz * xhat_r, fp64 per
+// workgroup, one fp64 atomic per channel, moment and workgroup.  Pass 2 (elementwise):
+//   da = rstd_a * (dz - S0 / P - xhat_a * S1 / P)
+//   dr = rstd_r * (dz - S0 / P - xhat_r * S2 / P)   (normed residual)  |  dz  (plain residual)
+struct NaBwd {
+  const float* dy; int64_t ldd;
+  const float* y; int64_t ldy;
+  const float* a; int64_t lda;
+  const float* sa;           // (B, 2, C) {mean, rstd}
+  const float* r; int64_t ldr;
+  const float* sr;           // (B, 2, C) or nullptr
+  double* acc;               // (B, C, 3)
+  float* da; int64_t ldda;
+  float* dr; int64_t lddr;   // nullptr: no residual gradient wanted
+  int C;
+  int64_t P;
+  float slope;
+};
+
+__global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(NaBwd k, int64_t chunk) {
+  extern __shared__ double red3[];  // [R][C4][12]
+  const int C4 = k.C >> 2;
+  const int R = 256 / C4;
+  const int tid = threadIdx.x;
+  const int row = tid / C4, g = tid - row * C4;
+  const int b = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * chunk;
+  const int64_t p1 = min(k.P, p0 + chunk);
+  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  if (row < R) {
+    const int c = 4 * g;
+    const f32x4 ma = *reinterpret_cast<const f32x4*>(k.sa + (int64_t)(2 * b) * k.C + c);
+    const f32x4 ra = *reinterpret_cast<const f32x4*>(k.sa + (int64_t)(2 * b + 1) * k.C + c);
+    f32x4 mr = {0, 0, 0, 0}, rr = {0, 0, 0, 0};
+    if (k.sr) {
+      mr = *reinterpret_cast<const f32x4*>(k.sr + (int64_t)(2 * b) * k.C + c);
+      rr = *reinterpret_cast<const f32x4*>(k.sr + (int64_t)(2 * b + 1) * k.C + c);
+    }
+    for (int64_t p = p0 + row; p < p1; p += R) {
+      const int64_t pos = (int64_t)b * k.P + p;
+      const f32x4 dy = *reinterpret_cast<const f32x4*>(k.dy + pos * k.ldd + c);
+      const f32x4 y = *reinterpret_cast<const f32x4*>(k.y + pos * k.ldy + c);
+      const f32x4 xa = (*reinterpret_cast<const f32x4*>(k.a + pos * k.lda + c) - ma) * ra;
+      f32x4 xr = {0, 0, 0, 0};
+      if (k.sr) xr = (*reinterpret_cast<const f32x4*>(k.r + pos * k.ldr + c) - mr) * rr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double dz = (double)(y[j] > 0.f ? dy[j] : dy[j] * k.slope);
+        s0[j] += dz;
+        s1[j] += dz * (double)xa[j];
+        s2[j] += dz * (double)xr[j];
+      }
+    }
+    double* rd = red3 + ((int64_t)row * C4 + g) * 12;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      rd[j] = s0[j];
+      rd[4 + j] = s1[j];
+      rd[8 + j] = s2[j];
+    }
+  }
+  __syncthreads();
+  const int nm = k.sr ? 3 : 2;
+  for (int i = tid; i < k.C * nm; i += blockDim.x) {
+    const int c = i / nm, mom = i - c * nm;
+    const int gg = c >> 2, j = c & 3;
+    double t = 0;
+    for (int rr2 = 0; rr2 < R; ++rr2) t += red3[((int64_t)rr2 * C4 + gg) * 12 + 4 * mom + j];
+    atomicAdd(k.acc + ((int64_t)b * k.C + c) * 3 + mom, t);
+  }
+}
+
+__global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(NaBwd k, int64_t total) {
+  const int C4 = k.C >> 2;
+  const double invP = 1.0 / (double)k.P;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pos = i / C4;
+    const int c = 4 * (int)(i - pos * C4);
+    const int b = (int)(pos / k.P);
+    const f32x4 ma = *reinterpret_cast<const f32x4*>(k.sa + (int64_t)(2 * b) * k.C + c);
+    const f32x4 ra = *reinterpret_cast<const f32x4*>(k.sa + (int64_t)(2 * b + 1) * k.C + c);
+    const f32x4 dy = *reinterpret_cast<const f32x4*>(k.dy + pos * k.ldd + c);
+    const f32x4 y = *reinterpret_cast<const f32x4*>(k.y + pos * k.ldy + c);
+    const f32x4 xa = (*reinterpret_cast<const f32x4*>(k.a + pos * k.lda + c) - ma) * ra;
+    const double* ac = k.acc + ((int64_t)b * k.C + c) * 3;
+    f32x4 dz, da, dr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      dz[j] = y[j] > 0.f ? dy[j] : dy[j] * k.slope;
+      const float m0 = (float)(ac[3 * j] * invP), m1 = (float)(ac[3 * j + 1] * invP);
+      da[j] = ra[j] * (dz[j] - m0 - xa[j] * m1);
+    }
+    *reinterpret_cast<f32x4*>(k.da + pos * k.ldda + c) = da;
+    if (k.dr) {
+      if (k.sr) {
+        const f32x4 mr = *reinterpret_cast<const f32x4*>(k.sr + (int64_t)(2 * b) * k.C + c);
+        const f32x4 rr = *reinterpret_cast<const f32x4*>(k.sr + (int64_t)(2 * b + 1) * k.C + c);
+        const f32x4 xr = (*reinterpret_cast<const f32x4*>(k.r + pos * k.ldr + c) - mr) * rr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float m0 = (float)(ac[3 * j] * invP), m2 = (float)(ac[3 * j + 2] * invP);
+          dr[j] = rr[j] * (dz[j] - m0 - xr[j] * m2);
+        }
+      } else {
+        dr = dz;
+      }
+      *reinterpret_cast<f32x4*>(k.dr + pos * k.lddr + c) = dr;
+    }
+  }
+}
+
 }  // namespace wf
 
 using namespace wf;
+
+extern "C" int64_t wf_norm_act_bwd_workspace_bytes(int64_t B, int64_t C) {
+  return B * C * 3 * (int64_t)sizeof(double);
+}
+
+extern "C" int wf_norm_act_bwd_cl(const float* dy, int64_t ldd, const float* y, int64_t ldy,
+                                  const float* a, int64_t lda, const float* stats_a,
+                                  const float* r, int64_t ldr, const float* stats_r,
+                                  float* da, int64_t ldda, float* dr, int64_t lddr, int64_t B,
+                                  int64_t C, int64_t P, float slope, void* workspace,
+                                  void* stream) {
+  WF_REQUIRE(B >= 1 && P >= 1, "empty tensor");
+  WF_REQUIRE(C >= 4 && C % 4 == 0 && C <= 1024, "C must be a multiple of 4 in [4, 1024]");
+  WF_REQUIRE(ldd >= C && ldy >= C && lda >= C && ldda >= C && ldd % 4 == 0 && ldy % 4 == 0 &&
+             lda % 4 == 0 && ldda % 4 == 0 && (!dr || (lddr >= C && lddr % 4 == 0)) &&
+             (!stats_r || (r && ldr >= C && ldr % 4 == 0)),
+             "every ld must be >= C and a multiple of 4");
+  WF_REQUIRE_PTR(dy);
+  WF_REQUIRE_PTR(y);
+  WF_REQUIRE_PTR(a);
+  WF_REQUIRE_PTR(stats_a);
+  WF_REQUIRE_PTR(da);
+  WF_REQUIRE_PTR(workspace);
+  NaBwd k{dy, ldd, y, ldy, a, lda, stats_a, r, ldr, stats_r,
+          reinterpret_cast<double*>(workspace), da, ldda, dr, lddr, (int)C, P, slope};
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(k.acc, 0, (size_t)wf_norm_act_bwd_workspace_bytes(B, C), s) != hipSuccess)
+    return check_launch("wf_norm_act_bwd_cl (memset)");
+  const int C4 = (int)(C / 4);
+  const int R = 256 / C4;
+  int64_t chunks = cdiv(1024, B);
+  int64_t chunk = cdiv(P, chunks);
+  if (chunk < 4 * R) chunk = 4 * R;
+  chunks = cdiv(P, chunk);
+  const size_t lds = (size_t)R * C4 * 12 * sizeof(double);
+  hipLaunchKernelGGL(norm_act_bwd_reduce_kernel, dim3((unsigned)chunks, (unsigned)B), dim3(256),
+                     lds, s, k, chunk);
+  int rc = check_launch("wf_norm_act_bwd_cl (reduce)");
+  if (rc) return rc;
+  const int64_t total = B * P * C4;
+  int64_t blocks = cdiv(total, 256);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(norm_act_bwd_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, k,
+                     total);
+  return check_launch("wf_norm_act_bwd_cl (apply)");
+}
 
 extern "C" int64_t wf_instnorm_workspace_bytes(int64_t B, int64_t C) {
   return B * C * 2 * (int64_t)sizeof(double);
