@@ -49,7 +49,7 @@ struct Conv3Args {
                       // InstanceNorm statistics of the output, fused into the epilogue
 };
 
-template <int CO_T, int NT, int P>
+template <int CO_T, int NT, int P, bool PIPE = false>
 __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   constexpr int TX = 16 * NT, TY = 4, HX = TX + 2, HY = TY + 2;
@@ -212,8 +212,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
         }
       }
       // keep the next step's fragment reads from being hoisted over these MFMAs (VGPRs: the
-      // next chunk's prefetch registers are live across the whole loop)
-      __builtin_amdgcn_sched_barrier(0);
+      // next chunk's prefetch registers are live across the whole loop); without the split's
+      // lo operands there is room to read one step ahead (WF_CONV_PIPE A/B)
+      if (SPLIT || !PIPE) __builtin_amdgcn_sched_barrier(0);
     }
   }
 
@@ -324,9 +325,12 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   dim3 grid((unsigned)a.nblocks, (unsigned)(a.Cout / (16 * CO_T)), (unsigned)a.ksplit);
   const bool post_stats = a.stats && a.ksplit > 1;  // partial outputs: a separate pass below
   {
+    static const bool pipe = getenv("WF_CONV_PIPE") != nullptr;
     auto kern = prec == PREC_SPLIT  ? conv3d_k3_kernel<CO_T, NT, PREC_SPLIT>
-                : prec == PREC_FP16 ? conv3d_k3_kernel<CO_T, NT, PREC_FP16>
-                                    : conv3d_k3_kernel<CO_T, NT, PREC_BF16>;
+                : prec == PREC_FP16 ? (pipe ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, true>
+                                            : conv3d_k3_kernel<CO_T, NT, PREC_FP16>)
+                                    : (pipe ? conv3d_k3_kernel<CO_T, NT, PREC_BF16, true>
+                                            : conv3d_k3_kernel<CO_T, NT, PREC_BF16>);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
