@@ -47,6 +47,7 @@ struct Conv3Args {
                       // epilogue atomically adds into a zeroed output (small grids only)
   double* stats;      // (B, Cout, 2) fp64 {sum, sum of squares} accumulator or nullptr: the
                       // InstanceNorm statistics of the output, fused into the epilogue
+  int zfirst;         // tile order: z fastest (1) or x fastest (0)
 };
 
 template <int CO_T, int NT, int P, bool PIPE = false>
@@ -73,12 +74,25 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   // XCDs; give each XCD a contiguous run of tiles so z / y neighbours share its L2
   int64_t t = blockIdx.x;
   if ((a.nblocks & 7) == 0) t = (t & 7) * (a.nblocks >> 3) + (t >> 3);
-  const int tx = (int)(t % a.tiles_x);
-  t /= a.tiles_x;
-  const int ty = (int)(t % a.tiles_y);
-  t /= a.tiles_y;
-  const int z = (int)(t % a.D);
-  const int b = (int)(t / a.D);
+  int tx, ty, z, b;
+  if (a.zfirst) {
+    // z fastest: the workgroups an XCD runs together are consecutive z planes of one (y, x)
+    // column, so each input plane's halo is read by its three z neighbours out of that XCD's
+    // L2 instead of from HBM three times (large planes: 128^2 x 96 channels = 6 MB > 4 MB L2)
+    z = (int)(t % a.D);
+    t /= a.D;
+    tx = (int)(t % a.tiles_x);
+    t /= a.tiles_x;
+    ty = (int)(t % a.tiles_y);
+    b = (int)(t / a.tiles_y);
+  } else {
+    tx = (int)(t % a.tiles_x);
+    t /= a.tiles_x;
+    ty = (int)(t % a.tiles_y);
+    t /= a.tiles_y;
+    z = (int)(t % a.D);
+    b = (int)(t / a.D);
+  }
   const int x0 = tx * TX, y0 = ty * TY;
   const int co0 = blockIdx.y * (16 * CO_T);
 
@@ -324,6 +338,8 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   }
   dim3 grid((unsigned)a.nblocks, (unsigned)(a.Cout / (16 * CO_T)), (unsigned)a.ksplit);
   const bool post_stats = a.stats && a.ksplit > 1;  // partial outputs: a separate pass below
+  static const int zf = getenv("WF_CONV_ZFIRST") ? atoi(getenv("WF_CONV_ZFIRST")) : 1;
+  a.zfirst = zf;
   {
     static const bool pipe = getenv("WF_CONV_PIPE") != nullptr;
     auto kern = prec == PREC_SPLIT  ? conv3d_k3_kernel<CO_T, NT, PREC_SPLIT>
