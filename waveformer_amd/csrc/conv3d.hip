@@ -50,10 +50,13 @@ struct Conv3Args {
   int zfirst;         // tile order: z fastest (1) or x fastest (0)
 };
 
-template <int CO_T, int NT, int P, bool PIPE = false>
+// RW output rows per wave (wave w: rows w, w + 4, ...): RW = 2 halves the weight-fragment LDS
+// reads per MFMA and the halo staging per output (non-split modes; the split's registers
+// do not allow it)
+template <int CO_T, int NT, int P, bool PIPE = false, int RW = 1>
 __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
-  constexpr int TX = 16 * NT, TY = 4, HX = TX + 2, HY = TY + 2;
+  constexpr int TX = 16 * NT, TY = 4 * RW, HX = TX + 2, HY = TY + 2;
   constexpr int NPOS = 3 * HY * HX;
   constexpr int PS = kConvCC;                       // bf16 per position per plane
   constexpr int NPL = SPLIT ? 2 : 1;                 // operand planes staged (lo only for SPLIT)
@@ -96,11 +99,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   const int x0 = tx * TX, y0 = ty * TY;
   const int co0 = blockIdx.y * (16 * CO_T);
 
-  f32x4 acc[CO_T][NT];
+  f32x4 acc[RW][CO_T][NT];
 #pragma unroll
-  for (int m = 0; m < CO_T; ++m)
+  for (int r = 0; r < RW; ++r)
 #pragma unroll
-    for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0, 0, 0, 0};
+    for (int m = 0; m < CO_T; ++m)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[r][m][n] = f32x4{0, 0, 0, 0};
 
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   const int ch_begin = (int)(((int64_t)blockIdx.z * a.nch) / a.ksplit);
@@ -200,7 +205,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
     if (ch + 1 < ch_end) fetch(ch + 1);
 #pragma unroll
     for (int s = 0; s < kConvKS; ++s) {
-      bf16x8 bh[NT], bl[NT], wh[CO_T], wl[CO_T];
+      bf16x8 wh[CO_T], wl[CO_T];
 #pragma unroll
       for (int m = 0; m < CO_T; ++m) {
         wh[m] = *reinterpret_cast<const bf16x8*>(lw + ((s * NPL + 0) * CO_T + m) * 1024);
@@ -208,21 +213,26 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
                       : zero8;
       }
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        bh[n] = *reinterpret_cast<const bf16x8*>(lb + boff[s] + 16 * n * PS * 2);
-        bl[n] = SPLIT ? *reinterpret_cast<const bf16x8*>(lb + boff[s] + 16 * n * PS * 2 +
-                                                           NPOS * PS * 2)
-                      : zero8;
-      }
+      for (int r = 0; r < RW; ++r) {
+        bf16x8 bh[NT], bl[NT];
+        const uint32_t ro = (uint32_t)(4 * r * HX * PS * 2);  // row w + 4 r of the halo
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
+        for (int n = 0; n < NT; ++n) {
+          bh[n] = *reinterpret_cast<const bf16x8*>(lb + boff[s] + ro + 16 * n * PS * 2);
+          bl[n] = SPLIT ? *reinterpret_cast<const bf16x8*>(lb + boff[s] + ro + 16 * n * PS * 2 +
+                                                             NPOS * PS * 2)
+                        : zero8;
+        }
 #pragma unroll
-        for (int m = 0; m < CO_T; ++m) {
-          if (SPLIT) {
-            acc[m][n] = mma32<P>(wh[m], bl[n], acc[m][n]);
-            acc[m][n] = mma32<P>(wl[m], bh[n], acc[m][n]);
+        for (int n = 0; n < NT; ++n) {
+#pragma unroll
+          for (int m = 0; m < CO_T; ++m) {
+            if (SPLIT) {
+              acc[r][m][n] = mma32<P>(wh[m], bl[n], acc[r][m][n]);
+              acc[r][m][n] = mma32<P>(wl[m], bh[n], acc[r][m][n]);
+            }
+            acc[r][m][n] = mma32<P>(wh[m], bh[n], acc[r][m][n]);
           }
-          acc[m][n] = mma32<P>(wh[m], bh[n], acc[m][n]);
         }
       }
       // keep the next step's fragment reads from being hoisted over these MFMAs (VGPRs: the
@@ -236,20 +246,23 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   // lane's NT positions, then the 16 lanes of its row (DPP), then the 4 waves (LDS), then one
   // fp64 atomic per (channel, moment) per workgroup
   if (a.stats && a.ksplit == 1) {
-    const bool rowok = y0 + wid < a.H;
     f32x4 ps[CO_T], pq[CO_T];
 #pragma unroll
     for (int m = 0; m < CO_T; ++m) {
       ps[m] = f32x4{0, 0, 0, 0};
       pq[m] = f32x4{0, 0, 0, 0};
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        const bool ok = rowok && x0 + 16 * n + l15 < a.W;
-        f32x4 v = acc[m][n];
-        if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + co0 + 16 * m + 4 * g4);
-        if (ok) {
-          ps[m] += v;
-          pq[m] += v * v;
+      for (int r = 0; r < RW; ++r) {
+        const bool rowok = y0 + wid + 4 * r < a.H;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const bool ok = rowok && x0 + 16 * n + l15 < a.W;
+          f32x4 v = acc[r][m][n];
+          if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + co0 + 16 * m + 4 * g4);
+          if (ok) {
+            ps[m] += v;
+            pq[m] += v * v;
+          }
         }
       }
 #pragma unroll
@@ -280,24 +293,28 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
     }
   }
 
-  // ---- epilogue: acc[m][n][i] = out[(z, y0 + wid, x0 + 16 n + l15)][co0 + 16 m + 4 g4 + i]
-  const int gy = y0 + wid;
-  if (gy >= a.H) return;
+  // ---- epilogue: acc[r][m][n][i] = out[(z, y0 + wid + 4 r, x0 + 16 n + l15)]
+  //                                      [co0 + 16 m + 4 g4 + i]
 #pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const int gx = x0 + 16 * n + l15;
-    if (gx >= a.W) continue;
-    float* o = a.out + (((int64_t)(b * a.D + z) * a.H + gy) * a.W + gx) * a.ldo;
+  for (int r = 0; r < RW; ++r) {
+    const int gy = y0 + wid + 4 * r;
+    if (gy >= a.H) break;
 #pragma unroll
-    for (int m = 0; m < CO_T; ++m) {
-      const int co = co0 + 16 * m + 4 * g4;
-      f32x4 v = acc[m][n];
-      if (a.bias && blockIdx.z == 0) v += *reinterpret_cast<const f32x4*>(a.bias + co);
-      if (a.ksplit > 1) {
+    for (int n = 0; n < NT; ++n) {
+      const int gx = x0 + 16 * n + l15;
+      if (gx >= a.W) continue;
+      float* o = a.out + (((int64_t)(b * a.D + z) * a.H + gy) * a.W + gx) * a.ldo;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) atomicAdd(o + co + j, v[j]);
-      } else {
-        *reinterpret_cast<f32x4*>(o + co) = v;
+      for (int m = 0; m < CO_T; ++m) {
+        const int co = co0 + 16 * m + 4 * g4;
+        f32x4 v = acc[r][m][n];
+        if (a.bias && blockIdx.z == 0) v += *reinterpret_cast<const f32x4*>(a.bias + co);
+        if (a.ksplit > 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) atomicAdd(o + co + j, v[j]);
+        } else {
+          *reinterpret_cast<f32x4*>(o + co) = v;
+        }
       }
     }
   }
@@ -313,19 +330,19 @@ __global__ void zero_cl_kernel(float* __restrict__ out, int64_t ldo, int C, int6
   }
 }
 
-template <int CO_T, int NT>
+template <int CO_T, int NT, int RW = 1>
 static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   Conv3Args a = a0;
   constexpr int TX = 16 * NT;
   a.tiles_x = (int)cdiv(a.W, TX);
-  a.tiles_y = (int)cdiv(a.H, 4);
+  a.tiles_y = (int)cdiv(a.H, 4 * RW);
   a.nblocks = (int64_t)a.B * a.D * a.tiles_y * a.tiles_x;
   if (a.nblocks >= ((int64_t)1 << 31)) return fail(WF_E_SHAPE, "wf_conv3d_k3_fwd: too many tiles");
   // operand planes staged: hi + lo for the split, hi only otherwise (half the LDS: twice the
   // workgroups per CU for bf16 / fp16)
   const size_t npl = prec == PREC_SPLIT ? 2 : 1;
-  const size_t lds = (npl * 3 * 6 * (TX + 2) * kConvCC + (size_t)kConvKS * npl * CO_T * 512) *
-                     sizeof(uint16_t);
+  const size_t lds = (npl * 3 * (4 * RW + 2) * (TX + 2) * kConvCC +
+                      (size_t)kConvKS * npl * CO_T * 512) * sizeof(uint16_t);
   // small grids (the 8^3 / 16^3 decoder convs): split the Cin chunks over blockIdx.z so the
   // launch covers the 256 CUs; partial sums meet in the zeroed output through fp32 atomics
   const int64_t wgs = a.nblocks * (a.Cout / (16 * CO_T));
@@ -341,12 +358,9 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   static const int zf = getenv("WF_CONV_ZFIRST") ? atoi(getenv("WF_CONV_ZFIRST")) : 1;
   a.zfirst = zf;
   {
-    static const bool pipe = getenv("WF_CONV_PIPE") != nullptr;
-    auto kern = prec == PREC_SPLIT  ? conv3d_k3_kernel<CO_T, NT, PREC_SPLIT>
-                : prec == PREC_FP16 ? (pipe ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, true>
-                                            : conv3d_k3_kernel<CO_T, NT, PREC_FP16>)
-                                    : (pipe ? conv3d_k3_kernel<CO_T, NT, PREC_BF16, true>
-                                            : conv3d_k3_kernel<CO_T, NT, PREC_BF16>);
+    auto kern = prec == PREC_SPLIT  ? conv3d_k3_kernel<CO_T, NT, PREC_SPLIT, false, 1>
+                : prec == PREC_FP16 ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, false, RW>
+                                    : conv3d_k3_kernel<CO_T, NT, PREC_BF16, false, RW>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
@@ -444,6 +458,11 @@ extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_p
   a.stats = stats_acc;
   hipStream_t s = (hipStream_t)stream;
   const bool co3 = Cout % 48 == 0;
+  // two output rows per wave (WF_CONV_RW=2, non-split modes, W > 32): measured slower, the
+  // larger halo's prefetch registers spill (96->48 at 128^3 fp16: 1.82 vs 1.73 ms)
+  static const int rw = getenv("WF_CONV_RW") ? atoi(getenv("WF_CONV_RW")) : 1;
+  if (W > 32 && precision != PREC_SPLIT && rw == 2 && co3)
+    return launch_conv3<3, 4, 2>(a, precision, s);
   if (W > 32) return co3 ? launch_conv3<3, 4>(a, precision, s) : launch_conv3<1, 4>(a, precision, s);
   if (W > 16) return co3 ? launch_conv3<3, 2>(a, precision, s) : launch_conv3<1, 2>(a, precision, s);
   return co3 ? launch_conv3<3, 1>(a, precision, s) : launch_conv3<1, 1>(a, precision, s);
