@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(mrun, tmax);
-    const float alpha = exp2f(mrun - mnew);  // mrun = -inf on the first tile -> 0
+    const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);  // mrun = -inf on the first tile -> 0
     mrun = mnew;
     float psum = 0.f;
     bf16x4 pf[NKT], pfl[NKT];
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
     for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(s[kt][i] - mnew);
+        const float p = __builtin_amdgcn_exp2f(s[kt][i] - mnew);
         psum += p;
         const uint16_t ph = op_cvt<P>(p);
         pf[kt][i] = (short)ph;
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(mrun, tmax);
-    const float alpha = exp2f(mrun - mnew);
+    const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
     mrun = mnew;
     float psum = 0.f;
     bf16x4 pf[NKT], pfl[NKT];
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
     for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(s[kt][i] - mnew);
+        const float p = __builtin_amdgcn_exp2f(s[kt][i] - mnew);
         psum += p;
         const uint16_t ph = op_cvt<P>(p);
         pf[kt][i] = (short)ph;
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mnew = fmaxf(mrun, tmax);
-      const float alpha = exp2f(mrun - mnew);
+      const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
       mrun = mnew;
       float psum = 0.f;
       bf16x4 ph[4], pl[4];
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(s[kt][i] - mnew);
+          const float p = __builtin_amdgcn_exp2f(s[kt][i] - mnew);
           psum += p;
           const uint16_t hb = op_cvt<P>(p);
           ph[kt][i] = (short)hb;

@@ -356,8 +356,12 @@ int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s) {
   // chunks until the grid has ~2 workgroups per CU (the K loop is a serial chain per workgroup)
   auto blocks = [&](int c) { return cdiv(g.M, 64 * (c >= 24 ? 1 : 2)) * (tiles / c); };
   int nt = 0;
+  // with fp32 activations (PREC_SPLIT / PREC_FP16) NT = 12 / 24 need 248-256 VGPRs: one wave
+  // per SIMD and nothing to hide the A stream's latency -- at most 8 column tiles (188 VGPRs,
+  // two waves) and the A rows re-read per chunk from L2 instead
+  const int ntmax = (g.epi != EPI_LN_GELU && store32(g.prec) && !g.a_bf16) ? 8 : 24;
   for (int c : cand) {
-    if (tiles % c != 0) continue;
+    if (tiles % c != 0 || c > ntmax) continue;
     if (g.epi == EPI_LN_GELU && c != tiles) continue;  // LayerNorm needs the full row
     if (nt == 0 || (g.epi != EPI_LN_GELU && blocks(nt) < 512 && c >= 3)) nt = c;
     if (blocks(nt) >= 512) break;

@@ -26,6 +26,9 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t Wl[];  // [NB][NT*16][KP]
   const int K = g.K, N = g.N;
   const int M = (int)g.M;
+  // LN+GELU epilogue call sites (CCF_FFN pwconv) load with given stats or none
+  const int a_ln = EPI == EPI_LN_GELU ? (g.a_ln == LN_GIVEN ? LN_GIVEN : LN_NONE) : g.a_ln;
+  const int a_gelu = EPI == EPI_LN_GELU ? 0 : g.a_gelu;
   const int K32 = (K + 31) & ~31;
   const int KP = K32 + 8;
   constexpr int NCOL = NT * 16;
@@ -59,7 +62,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
   float* elw = ebias + NCOL;
   float* elb = elw + NCOL;
   for (int i = tid; i < K32; i += blockDim.x) {
-    const bool ok = g.a_ln != LN_NONE && i < K;
+    const bool ok = a_ln != LN_NONE && i < K;
     lnw[i] = ok ? g.a_ln_w[i] : 0.f;
     lnb[i] = ok ? g.a_ln_b[i] : 0.f;
   }
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
   float vn[8];
   load8f<ABF16>(g.a_src, rm.offset(g, min(8 * g4, K - 8)), vn);
   float gmean = 0.f, grstd = 1.f;
-  if (g.a_ln == LN_GIVEN) {
+  if (a_ln == LN_GIVEN) {
     gmean = g.a_stats[2 * arow_c];
     grstd = g.a_stats[2 * arow_c + 1];
   }
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
     const int arow_n = min((tile + stride) * 16 + l15, M - 1);
     const RowMapper<MAP> rmn(g, arow_n);
     float mean = gmean, rstd = grstd;
-    if (g.a_ln == LN_COMPUTE) {  // lanes l15, l15+16, l15+32, l15+48 share the row
+    if (a_ln == LN_COMPUTE) {  // lanes l15, l15+16, l15+32, l15+48 share the row
       float s = 0.f;
       for (int ch = g4; ch < K / 8; ch += 4) {
         float v[8];
@@ -116,7 +119,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
       q += __shfl_xor(q, 16, 64);
       q += __shfl_xor(q, 32, 64);
       rstd = rsqrtf(q / (float)K + g.a_eps);
-    } else if (g.a_ln == LN_PARTIAL) {  // combine the producer's per-group {mean, M2}
+    } else if (a_ln == LN_PARTIAL) {  // combine the producer's per-group {mean, M2}
       const int np = g.a_np;
       const float* ps = g.a_stats + (int64_t)arow_c * np * 2;
       float s = 0.f;
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
       const int64_t noff = k0 + 32 < K32 ? rm.offset(g, min(k + 32, K - 8))
                                          : rmn.offset(g, min(8 * g4, K - 8));
       load8f<ABF16>(g.a_src, noff, vn);
-      if (g.a_ln != LN_NONE) {
+      if (a_ln != LN_NONE) {
         const f32x4 w0 = *reinterpret_cast<const f32x4*>(lnw + k);
         const f32x4 w1 = *reinterpret_cast<const f32x4*>(lnw + k + 4);
         const f32x4 b0 = *reinterpret_cast<const f32x4*>(lnb + k);
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (v[j] - mean) * rstd * wv[j] + bv[j];
       }
-      if (g.a_gelu) {
+      if (a_gelu) {
         gelu_erf8(v);
       }
       bf16x8 ah, al;
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
       }
     }
 
-    if (g.a_ln == LN_GIVEN) {  // next tile's stats, in flight through the epilogue
+    if (a_ln == LN_GIVEN) {  // next tile's stats, in flight through the epilogue
       gmean = g.a_stats[2 * arow_n];
       grstd = g.a_stats[2 * arow_n + 1];
     }
@@ -246,8 +249,12 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
           v = xr + v * bs;         // bare CCF_FFN.forward: x + x_out
         }
       }
-      if (rv && col < N) {
-        if (g.out_bf16) {
+      // LN+GELU (CCF_FFN pwconv): the chunk is the whole row and the storage type follows
+      // the precision, so the store needs no column test and no runtime type branch
+      const bool cv = EPI == EPI_LN_GELU ? true : col < N;
+      const bool obf = EPI == EPI_LN_GELU ? P == PREC_BF16 : g.out_bf16 != 0;
+      if (rv && cv) {
+        if (obf) {
           bf16x4 o;
           o[0] = (short)f2bf(v.x);
           o[1] = (short)f2bf(v.y);
@@ -303,6 +310,10 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
   const bool known = (g.a_map == MAP_WINDOW && g.epi == EPI_STORE) ||
                      (g.a_map == MAP_IDENTITY) || (g.a_map == MAP_MERGE && g.epi == EPI_STORE);
   if (!known) return 0;
+  // the LN+GELU instantiations are specialised to the CCF_FFN pwconv's loader and storage
+  if (g.epi == EPI_LN_GELU && ((g.a_ln != LN_GIVEN && g.a_ln != LN_NONE) || g.a_gelu ||
+                               (g.out_bf16 != 0) != (g.prec == PREC_BF16 || g.a_bf16 != 0)))
+    return 0;
   const bool split = g.prec == PREC_SPLIT;
   const int K32 = (g.K + 31) & ~31;
   const size_t per_col = (size_t)(split ? 2 : 1) * (K32 + 8) * 2;
