@@ -2,7 +2,7 @@
 // LDS whole (PatchMerging 8C -> 2C, the CCF_FFN fc of stages 2-4, stage 3/4 qkv/pw).
 //
 // out[m, n] = epilogue( sum_k A[m, k] * Wt[n, k] )
-//   * workgroup = 4 waves x RT row tiles of 16 rows (64 * RT rows) x one column chunk of
+//   * workgroup = 8 waves x one row tile of 16 rows (128 rows) x one column chunk of
 //     NC = NT * 16 output channels (grid.y walks the chunks);
 //   * the weight chunk streams through LDS 32 k at a time, double buffered: the next k step's
 //     [NC][32] bf16 hi (+ lo) slice is loaded into registers while the MFMAs of the current
@@ -24,14 +24,18 @@ constexpr int KC_KP = KC_BK + 8;  // LDS row stride in bf16 (16 B pad: conflict-
 
 template <int NT>
 struct KcCfg {
-  static constexpr int RT = NT >= 24 ? 1 : 2;  // accumulators: RT * NT * 4 <= 96 VGPRs
+  // one 16-row tile per wave and 8 waves per workgroup (128 rows): the accumulators stay
+  // at NT * 4 VGPRs, so NT <= 8 fits four waves per SIMD to hide the A stream and the
+  // per-step barrier (4 waves x 2 tiles: 168-188 VGPRs, two waves per SIMD, ~2x slower)
+  static constexpr int RT = 1;
+  static constexpr int WAVES = 8, NTHR = 64 * WAVES, ROWS = 16 * RT * WAVES;
   static constexpr int NC = NT * 16;
   static constexpr int WITEMS = NC * (KC_BK / 8);  // 16-byte pieces per plane per k step
-  static constexpr int WPT = (WITEMS + 255) / 256;  // per thread
+  static constexpr int WPT = (WITEMS + NTHR - 1) / NTHR;  // per thread
 };
 
 template <int NT, int P, int MAP, int EPI, bool ABF16>
-__global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
+__global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
   typedef KcCfg<NT> C;
   constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   constexpr int RT = C::RT, NC = C::NC, NPL = SPLIT ? 2 : 1;
@@ -42,14 +46,14 @@ __global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
   const int c0 = blockIdx.y * NC;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l15 = lane & 15, g4 = lane >> 4;
-  const int rbase = blockIdx.x * (64 * RT) + wid * (16 * RT);
+  const int rbase = blockIdx.x * C::ROWS + wid * (16 * RT);
 
   // ---- weight staging: piece i -> (column i / 4, k-octet i % 4) of the step's slice
   bf16x8 wst[NPL][C::WPT];
   auto wfetch = [&](int ks) {
 #pragma unroll
     for (int j = 0; j < C::WPT; ++j) {
-      const int i = min(j * 256 + tid, C::WITEMS - 1);
+      const int i = min(j * C::NTHR + tid, C::WITEMS - 1);
       const int n = c0 + (i >> 2), k = ks * KC_BK + 8 * (i & 3);
       const bool ok = n < N && k < K;
       const int64_t off = (int64_t)min(n, N - 1) * K + min(k, K - 8);
@@ -65,7 +69,7 @@ __global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
   auto wcommit = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < C::WPT; ++j) {
-      const int i = j * 256 + tid;
+      const int i = j * C::NTHR + tid;
       if (i < C::WITEMS) {
 #pragma unroll
         for (int pl = 0; pl < NPL; ++pl)
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(256) void gemm_kc_kernel(GemmArgs g) {
   float* lnw = reinterpret_cast<float*>(Wl + (size_t)2 * NPL * NC * KC_KP);
   float* lnb = lnw + nks * KC_BK;
   if (g.a_ln != LN_NONE) {
-    for (int i = tid; i < nks * KC_BK; i += 256) {
+    for (int i = tid; i < nks * KC_BK; i += C::NTHR) {
       lnw[i] = i < K ? g.a_ln_w[i] : 0.f;
       lnb[i] = i < K ? g.a_ln_b[i] : 0.f;
     }
@@ -328,8 +332,8 @@ static void go_kc(const GemmArgs& g, hipStream_t s) {
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const dim3 grid((unsigned)cdiv(g.M, 64 * C::RT), (unsigned)(g.N / C::NC));
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g);
+  const dim3 grid((unsigned)cdiv(g.M, C::ROWS), (unsigned)(g.N / C::NC));
+  hipLaunchKernelGGL(kern, grid, dim3(C::NTHR), lds, s, g);
 }
 
 template <int MAP, int EPI>
@@ -354,11 +358,11 @@ int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s) {
   static const int cand[] = {24, 12, 8, 6, 4, 3, 2};
   // widest column chunk that divides N (fewest re-reads of A); then, for small M, narrower
   // chunks until the grid has ~2 workgroups per CU (the K loop is a serial chain per workgroup)
-  auto blocks = [&](int c) { return cdiv(g.M, 64 * (c >= 24 ? 1 : 2)) * (tiles / c); };
+  auto blocks = [&](int c) { return cdiv(g.M, 128) * (tiles / c); };
   int nt = 0;
-  // with fp32 activations (PREC_SPLIT / PREC_FP16) NT = 12 / 24 need 248-256 VGPRs: one wave
-  // per SIMD and nothing to hide the A stream's latency -- at most 8 column tiles (188 VGPRs,
-  // two waves) and the A rows re-read per chunk from L2 instead
+  // with fp32 activations (PREC_SPLIT / PREC_FP16) NT = 12 / 24 need 150-210 VGPRs (two or
+  // three waves per SIMD) -- at most 8 column tiles (<= 136 VGPRs) and the A rows re-read per
+  // chunk from L2 instead
   const int ntmax = (g.epi != EPI_LN_GELU && store32(g.prec) && !g.a_bf16) ? 8 : 24;
   for (int c : cand) {
     if (tiles % c != 0 || c > ntmax) continue;
