@@ -47,7 +47,7 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_fused_kernel" if os.environ.get("WF_FFN_FUSED")
               else "ffn_dwfc_kernel" if os.environ.get("WF_FFN_DWFC_CLASSIC")
               else "ffn_dwfc_ws_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
-              "window_attention": "attn_core_kernel",
+              "window_attention": "attn_tbl_kernel",
               "msfuse": "msfuse", "proj_out": "proj_out"}
 
 
