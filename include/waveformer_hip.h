@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 10
+#define WF_ABI_VERSION 11
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
@@ -75,6 +75,11 @@ int wf_split_f32_to_bf16x2_multi(const int64_t* table_dev, int64_t n, int64_t to
 int wf_cast_f32_to_f16x2(const float* in, uint16_t* out, int64_t n, void* stream);
 int wf_cast_f32_to_f16x2_multi(const int64_t* table_dev, int64_t n, int64_t total,
                                void* stream);
+
+/* Test support, not a reference op: `blocks` workgroups that each fill `lds_bytes` of LDS
+ * with a NaN pattern and exit, so the next workgroups on those CUs start on garbage LDS (a
+ * kernel that reads LDS it did not write then shows it).                                  */
+int wf_debug_poison_lds(int64_t blocks, int lds_bytes, void* stream);
 
 /* ---- a10: PatchEmbed -------------------------------------------------------------- */
 /* Replaces monai PatchEmbed.proj = Conv3d(Cin, Cout, k=2, s=2) as called at

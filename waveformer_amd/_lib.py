@@ -30,6 +30,7 @@ SIGNATURES = {
     "wf_split_f32_to_bf16x2_multi": (_I, [_P, _I64, _I64, _P]),
     "wf_cast_f32_to_f16x2": (_I, [_P, _P, _I64, _P]),
     "wf_cast_f32_to_f16x2_multi": (_I, [_P, _I64, _I64, _P]),
+    "wf_debug_poison_lds": (_I, [_I64, _I, _P]),
     "wf_patch_embed_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwt3d_haar_fwd": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
@@ -105,7 +106,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 _lock = threading.Lock()
 _lib = None
 _err = None

@@ -78,9 +78,26 @@ __global__ void cast_f16x2_kernel(const float* __restrict__ in, uint16_t* __rest
   }
 }
 
+// Test support: fill `words` of LDS with a quiet-NaN pattern (volatile: the stores are kept)
+__global__ __launch_bounds__(256) void poison_lds_kernel(int words) {
+  extern __shared__ uint32_t pl[];
+  volatile uint32_t* v = pl;
+  for (int i = threadIdx.x; i < words; i += blockDim.x) v[i] = 0x7fc00000u | (uint32_t)(i & 0xffff);
+}
+
 }  // namespace wf
 
 extern "C" int wf_abi_version(void) { return WF_ABI_VERSION; }
+
+extern "C" int wf_debug_poison_lds(int64_t blocks, int lds_bytes, void* stream) {
+  WF_REQUIRE(blocks >= 1 && blocks <= (1 << 20), "blocks out of range");
+  WF_REQUIRE(lds_bytes >= 4 && lds_bytes <= 160 * 1024, "lds_bytes out of range");
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wf::poison_lds_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  hipLaunchKernelGGL(wf::poison_lds_kernel, dim3((unsigned)blocks), dim3(256), (size_t)lds_bytes,
+                     (hipStream_t)stream, lds_bytes / 4);
+  return wf::check_launch("wf_debug_poison_lds");
+}
 
 static int split_multi(const int64_t* table_dev, int64_t n, int64_t total, void* stream,
                        bool f16) {
