@@ -382,7 +382,11 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
   constexpr int NE = 384;                         // E threads
   constexpr int NLDE = (K::PP * K::NV + NE - 1) / NE;  // staged f32x4 per E thread (8)
   constexpr int H2F = K::NPOS * K::HS;            // one h2 tile (floats)
-  constexpr int LNL = 8, LNC = HID / LNL;         // LN2: 8 lanes x 24 channels per position
+  // LN2 + GELU of an h2 tile: 16 lanes x 12 channels per position; positions 0..15 by the D
+  // waves 0..3 in their phase 1 (they idle there otherwise: per plane the D waves' scatter is
+  // ~2.8k cycles of work against ~5.3k for the E waves, measured with s_memtime probes),
+  // positions 16..31 by the E waves 0..3
+  constexpr int LNL = 16, LNC = HID / LNL;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* planes = lds;                                  // [2][PP][HID]
   float* h2b = lds + 2 * K::PLANE_F;                     // [2][NPOS][HS]
@@ -426,6 +430,52 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
   const int64_t plane_elems = (int64_t)H * W * HID;
   const float bs = a.bscale ? a.bscale[b] : 1.f;
 
+  // LN2 + GELU + the bf16 hi / lo split of one h2 tile row, rewritten in place (the row's
+  // lanes are one 16-lane group of a wave: all reads precede the cross-lane reductions, which
+  // precede every write)
+  auto ln2_row = [&](float* h2t, int pos, int g) {
+    float* row = h2t + pos * K::HS;
+    float v[LNC];
+#pragma unroll
+    for (int j = 0; j < LNC / 4; ++j) {
+      const f32x4 u = *reinterpret_cast<const f32x4*>(row + g * LNC + 4 * j);
+      v[4 * j] = u.x;
+      v[4 * j + 1] = u.y;
+      v[4 * j + 2] = u.z;
+      v[4 * j + 3] = u.w;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < LNC; ++j) sm += v[j];
+    const float mean = group_sum<LNL>(sm) * (1.f / HID);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < LNC; ++j) {
+      const float d = v[j] - mean;
+      q += d * d;
+    }
+    const float rstd = rsqrtf(group_sum<LNL>(q) * (1.f / HID) + a.eps2);
+    const float nmr = -mean * rstd;
+    uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
+#pragma unroll
+    for (int j = 0; j < LNC / 4; ++j) {
+      const int c = g * LNC + 4 * j;
+      const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + c);
+      const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + c);
+      const f32x4 y = gelu_half4((f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]} *
+                                  rstd + nmr) * lw4 + lb4);
+      bf16x4 hi4, lo4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint16_t hb = op_cvt<P>(y[e]);
+        hi4[e] = (short)hb;
+        lo4[e] = op_lo<P>(y[e], hb);
+      }
+      *reinterpret_cast<bf16x4*>(rowh + c) = hi4;
+      if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + c) = lo4;
+    }
+  };
+
   if (isD) {
     // ================================ D waves: depthwise scatter ==========================
     const int cp = tid % NPAIR, xg = tid / NPAIR;  // columns xg and xg + 4
@@ -468,6 +518,12 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
       const bool live = p <= z1;
       const float* cur = planes + ((p - z0 + 1) & 1) * K::PLANE_F;
       const bool dscat = !(a.dbg & 1);  // timing experiments only (WF_FFN_DBG)
+      const int zl = p - 2;  // the h2 tile the E waves' fc takes in this iteration
+      if (zl >= z0 && zl < z1 && tid < 16 * LNL && !(a.dbg & 2)) {
+        int ltid = tid;
+        asm volatile("" : "+v"(ltid));
+        ln2_row(h2b + ((zl - z0) & 1) * H2F, ltid / LNL, ltid % LNL);
+      }
       if (live && dscat) rows(cur, 0, a.ws_split);
       __syncthreads();  // 1 -> 2
       if (live) {
@@ -574,47 +630,7 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
     if (epi && ewid < 4 && !(a.dbg & 2)) {
       int ltid = et;
       asm volatile("" : "+v"(ltid));
-      const int pos = ltid / LNL, g = ltid % LNL;
-      float* row = h2t + pos * K::HS;
-      float v[LNC];
-#pragma unroll
-      for (int j = 0; j < LNC / 4; ++j) {
-        const f32x4 u = *reinterpret_cast<const f32x4*>(row + g * LNC + 4 * j);
-        v[4 * j] = u.x;
-        v[4 * j + 1] = u.y;
-        v[4 * j + 2] = u.z;
-        v[4 * j + 3] = u.w;
-      }
-      float sm = 0.f;
-#pragma unroll
-      for (int j = 0; j < LNC; ++j) sm += v[j];
-      const float mean = group_sum<LNL>(sm) * (1.f / HID);
-      float q = 0.f;
-#pragma unroll
-      for (int j = 0; j < LNC; ++j) {
-        const float d = v[j] - mean;
-        q += d * d;
-      }
-      const float rstd = rsqrtf(group_sum<LNL>(q) * (1.f / HID) + a.eps2);
-      const float nmr = -mean * rstd;
-      uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
-#pragma unroll
-      for (int j = 0; j < LNC / 4; ++j) {
-        const int c = g * LNC + 4 * j;
-        const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + c);
-        const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + c);
-        const f32x4 y = gelu_half4((f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]} *
-                                    rstd + nmr) * lw4 + lb4);
-        bf16x4 hi4, lo4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint16_t hb = op_cvt<P>(y[e]);
-          hi4[e] = (short)hb;
-          lo4[e] = op_lo<P>(y[e], hb);
-        }
-        *reinterpret_cast<bf16x4*>(rowh + c) = hi4;
-        if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + c) = lo4;
-      }
+      ln2_row(h2t, 16 + ltid / LNL, ltid % LNL);
     }
     __syncthreads();  // 1 -> 2: LN rows of tile (p-2) visible
     // ---- phase 2: commit plane p+1 into the free buffer (D is done with plane p-1 since the
