@@ -2,9 +2,115 @@
 // (a10, quirk Q5).  All three are HBM-streaming row kernels over channel-last data.
 #include <math.h>
 
+#include <algorithm>
+
 #include "rowgroup.hpp"
 
 namespace wf {
+
+// ---------------------------------------------------------------------------------------
+// PatchEmbed, streaming variant (Cin = 4, Cout % 4 == 0, W % 2 == 0: the encoder's 4 -> 48
+// stem): a persistent workgroup walks groups of R output rows; the next group's 2x2 input
+// rows are loaded into registers (8 float4 per thread at R = 4) while the current group is
+// computed out of LDS, then written to the other LDS buffer -- the input stream never waits
+// on a barrier-separated load phase (the one-shot kernel above: 282 us at B = 8, 2.4 TB/s).
+// ---------------------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(256) void patch_embed_stream_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ out, int Cout, int D, int H, int W, int64_t ngroups) {
+  constexpr int CIN = 4, NK = CIN * 8;
+  extern __shared__ __attribute__((aligned(16))) float slab[];  // [2][R][Cin][dz][dy][2W]
+  const int W2 = 2 * W, H2 = 2 * H, D2 = 2 * D;
+  const int rowf = CIN * 4 * W2;            // floats per output row
+  const int per = rowf >> 2;                // float4 per output row
+  const int gper = R * per;                 // float4 per group
+  const int NLD = (gper + 255) / 256;       // <= 8 at W = 64, R = 4 (host-checked)
+  const int nyb = H / R;                    // H % R == 0 (host-checked)
+  const int tid = threadIdx.x;
+  float* buf0 = slab;
+  float* buf1 = slab + R * rowf;
+
+  // thread = (4-channel group, x group): weights as channel pairs, packed FMAs (as above)
+  const int C4 = Cout >> 2;
+  const int XG = blockDim.x / C4;
+  const int cq = tid % C4, xg = tid / C4;
+  const bool act = xg < XG;
+  const int c0 = 4 * (act ? cq : 0);
+  f32x2 wa[NK], wb[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    wa[k] = f32x2{w[(int64_t)(c0 + 0) * NK + k], w[(int64_t)(c0 + 1) * NK + k]};
+    wb[k] = f32x2{w[(int64_t)(c0 + 2) * NK + k], w[(int64_t)(c0 + 3) * NK + k]};
+  }
+  const f32x2 ba = bias ? f32x2{bias[c0], bias[c0 + 1]} : f32x2{0.f, 0.f};
+  const f32x2 bb = bias ? f32x2{bias[c0 + 2], bias[c0 + 3]} : f32x2{0.f, 0.f};
+
+  f32x4 stg[8];
+  auto fetch = [&](int64_t grp) {
+    const int y0 = (int)(grp % nyb) * R;
+    const int64_t r = grp / nyb;
+    const int z = (int)(r % D), b = (int)(r / D);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = min(j * 256 + tid, gper - 1);
+      const int rr = i / per, jj = i - rr * per;
+      const int x4 = jj % (W2 >> 2), t = jj / (W2 >> 2);
+      const int dy = t & 1, dz = (t >> 1) & 1, ci = t >> 2;
+      if (j < NLD)
+        stg[j] = reinterpret_cast<const f32x4*>(
+            x + ((((int64_t)b * CIN + ci) * D2 + 2 * z + dz) * H2 + 2 * (y0 + rr) + dy) * W2)[x4];
+    }
+  };
+  auto commit = [&](float* dst) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = j * 256 + tid;
+      if (j < NLD && i < gper) reinterpret_cast<f32x4*>(dst)[i] = stg[j];
+    }
+  };
+  auto compute = [&](const float* src, int64_t grp) {
+    if (!act) return;
+    const int y0 = (int)(grp % nyb) * R;
+    const int64_t r = grp / nyb;
+    const int z = (int)(r % D), b = (int)(r / D);
+#pragma unroll 1
+    for (int rr = 0; rr < R; ++rr) {
+      const float* sl = src + rr * rowf;
+      float* orow = out + (((int64_t)b * D + z) * H + y0 + rr) * W * (int64_t)Cout;
+      for (int xo = xg; xo < W; xo += XG) {
+        f32x2 a0 = ba, a1 = bb;
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float2 v = *reinterpret_cast<const float2*>(sl + (ci * 4 + q) * W2 + 2 * xo);
+            const int k = ci * 8 + 2 * q;
+            a0 = wa[k] * v.x + a0;
+            a1 = wb[k] * v.x + a1;
+            a0 = wa[k + 1] * v.y + a0;
+            a1 = wb[k + 1] * v.y + a1;
+          }
+        *reinterpret_cast<f32x4*>(orow + (int64_t)xo * Cout + c0) = f32x4{a0.x, a0.y, a1.x, a1.y};
+      }
+    }
+  };
+
+  int64_t g = blockIdx.x;
+  if (g >= ngroups) return;
+  fetch(g);
+  commit(buf0);
+  __syncthreads();
+  int cur = 0;
+  for (; g < ngroups; g += gridDim.x) {
+    const int64_t gn = g + gridDim.x;
+    if (gn < ngroups) fetch(gn);        // next group's input in flight during this compute
+    compute(cur ? buf1 : buf0, g);
+    if (gn < ngroups) commit(cur ? buf0 : buf1);
+    __syncthreads();                    // next buffer written, current buffer free
+    cur ^= 1;
+  }
+}
 
 // ---------------------------------------------------------------------------------------
 // PatchEmbed: Conv3d(Cin, Cout, k=2, s=2) on NCDHW input -> channel-last output.
@@ -400,6 +506,21 @@ extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* b
   WF_REQUIRE(Cout <= 256, "PatchEmbed: at most 256 output channels");
   const size_t row_lds = (size_t)Cin * 8 * W * sizeof(float);
   WF_REQUIRE(row_lds <= 64 * 1024, "PatchEmbed row tile exceeds 64 KB of LDS");
+  static const bool one_shot = getenv("WF_PE_ONESHOT") != nullptr;  // A/B: the kernel below
+  if (!one_shot && Cin == 4 && Cout % 4 == 0 && Cout <= 256 && H % 4 == 0 &&
+      4 * (int64_t)Cin * 8 * W / 4 <= 8 * 256) {
+    constexpr int R = 4;
+    const int64_t ngroups = B * D * (H / R);
+    const size_t lds = 2 * R * row_lds;
+    const int64_t blocks = std::min<int64_t>(ngroups, 256 * 2);  // 2 persistent per CU (LDS)
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(patch_embed_stream_kernel<R>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(patch_embed_stream_kernel<R>, dim3((unsigned)blocks), dim3(256), lds,
+                       (hipStream_t)stream, x, w, bias, out, (int)Cout, (int)D, (int)H, (int)W,
+                       ngroups);
+    return check_launch("wf_patch_embed_fwd");
+  }
   // rows per workgroup: up to 4 within 32 KB of LDS, while the grid keeps >= 2048 workgroups
   static const int rmax = getenv("WF_PE_ROWS") ? atoi(getenv("WF_PE_ROWS")) : 4;
   int R = 1;
