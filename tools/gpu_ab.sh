@@ -9,5 +9,5 @@ for so in "$@"; do
   n=$(basename $so .so)
   WAVEFORMER_HIP_LIB=$PWD/$so timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_$n -o run -- python $DRV > gpurun_out/${TAG}_$n.log 2>&1 || { tail -20 gpurun_out/${TAG}_$n.log; exit 1; }
   echo "== $n"; tail -2 gpurun_out/${TAG}_$n.log
-  f=$(ls gpurun_out/${TAG}_$n/*kernel_trace.csv | head -1); python tools/kstats.py $f 8
+  f=$(ls gpurun_out/${TAG}_$n/*kernel_trace.csv | head -1); python tools/kstats.py $f ${NK:-8}
 done

@@ -18,6 +18,10 @@
 // so each call site compiles to straight-line code with 32-bit index math.
 #include "gemm_common.hpp"
 
+#ifndef W2STAGE
+#define W2STAGE 1
+#endif
+
 namespace wf {
 
 template <int NT, int P, int MAP, int EPI, bool ABF16>
@@ -61,6 +65,11 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
   float* ebias = lnb + K32;
   float* elw = ebias + NCOL;
   float* elb = elw + NCOL;
+  // fp32 W2 output restaged per wave in LDS so each store instruction writes 1 KB of the
+  // tile's 16 contiguous rows (the accumulator layout writes 16 rows x 64 B per instruction)
+  constexpr bool STAGE = W2STAGE && EPI == EPI_LN_GELU && P != PREC_BF16;
+  constexpr int OST = NCOL + 4;  // staged row stride in floats (16-B pad)
+  float* ostg = elb + NCOL + (STAGE ? (threadIdx.x >> 6) * 16 * OST : 0);
   for (int i = tid; i < K32; i += blockDim.x) {
     const bool ok = a_ln != LN_NONE && i < K;
     lnw[i] = ok ? g.a_ln_w[i] : 0.f;
@@ -70,8 +79,8 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
     const int n = c0 + i;
     ebias[i] = (g.bias && n < N) ? g.bias[n] : 0.f;
     const bool e = EPI == EPI_LN_GELU && n < N;
-    elw[i] = e ? g.e_ln_w[n] : 0.f;
-    elb[i] = e ? g.e_ln_b[n] : 0.f;
+    elw[i] = e ? 0.5f * g.e_ln_w[n] : 0.f;  // half: the epilogue feeds gelu_half2
+    elb[i] = e ? 0.5f * g.e_ln_b[n] : 0.f;
   }
   __syncthreads();
 
@@ -83,8 +92,19 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
   int tile = blockIdx.x * nwaves + wid;
   int arow_c = min(tile * 16 + l15, M - 1);
   RowMapper<MAP> rm(g, arow_c);
-  float vn[8];
+  // LN + GELU (CCF_FFN pwconv, K <= 64): BOTH k steps of the next tile are loaded at the top of
+  // the current one, ahead of its epilogue stores.  vmcnt counts stores too and retires in
+  // order, so a load issued after a tile's 12 stores could only be waited for together with
+  // them: the one-step prefetch made every tile wait out the previous tile's write latency
+  // (without the stores the kernel ran 341 instead of 567 us at B = 8)
+  constexpr bool W2 = EPI == EPI_LN_GELU;
+  // output descriptor of the W2 stores: M rows of ldo elements (host: < 2^31 bytes)
+  const bool obf_ = EPI == EPI_LN_GELU ? P == PREC_BF16 : false;
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      g.out, 0, W2 ? (int)((int64_t)M * g.ldo * (obf_ ? 2 : 4)) : 0, 0x00020000);
+  float vn[8], vn1[8];
   load8f<ABF16>(g.a_src, rm.offset(g, min(8 * g4, K - 8)), vn);
+  if (W2) load8f<ABF16>(g.a_src, rm.offset(g, min(32 + 8 * g4, K - 8)), vn1);
   float gmean = 0.f, grstd = 1.f;
   if (a_ln == LN_GIVEN) {
     gmean = g.a_stats[2 * arow_c];
@@ -142,17 +162,10 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0, 0, 0, 0};
 
-    // k loop with a one-step register prefetch of the A fragment (last step: the next tile's)
-#pragma unroll 1
-    for (int k0 = 0; k0 < K32; k0 += 32) {
+    // one 32-deep k step on the A fragment v (LayerNorm / GELU / split in the loader)
+    auto kstep = [&](int k0, float* v) {
       const int k = k0 + 8 * g4;
       const bool kv = k < K;
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = vn[j];
-      const int64_t noff = k0 + 32 < K32 ? rm.offset(g, min(k + 32, K - 8))
-                                         : rmn.offset(g, min(8 * g4, K - 8));
-      load8f<ABF16>(g.a_src, noff, vn);
       if (a_ln != LN_NONE) {
         const f32x4 w0 = *reinterpret_cast<const f32x4*>(lnw + k);
         const f32x4 w1 = *reinterpret_cast<const f32x4*>(lnw + k + 4);
@@ -191,9 +204,38 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
         // occupancy): a scheduling fence every 3 tiles
         if (t % 3 == 2) __builtin_amdgcn_sched_barrier(0);
       }
+    };
+
+    if constexpr (W2) {
+      float v0[8], v1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v0[j] = vn[j];
+        v1[j] = vn1[j];
+      }
+      load8f<ABF16>(g.a_src, rmn.offset(g, min(8 * g4, K - 8)), vn);
+      load8f<ABF16>(g.a_src, rmn.offset(g, min(32 + 8 * g4, K - 8)), vn1);
+      if (a_ln == LN_GIVEN) {
+        gmean = g.a_stats[2 * arow_n];
+        grstd = g.a_stats[2 * arow_n + 1];
+      }
+      kstep(0, v0);
+      if (K32 > 32) kstep(32, v1);
+    } else {
+      // k loop with a one-step register prefetch of the A fragment (last step: the next tile's)
+#pragma unroll 1
+      for (int k0 = 0; k0 < K32; k0 += 32) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = vn[j];
+        const int64_t noff = k0 + 32 < K32 ? rm.offset(g, min(k0 + 32 + 8 * g4, K - 8))
+                                           : rmn.offset(g, min(8 * g4, K - 8));
+        load8f<ABF16>(g.a_src, noff, vn);
+        kstep(k0, v);
+      }
     }
 
-    if (a_ln == LN_GIVEN) {  // next tile's stats, in flight through the epilogue
+    if (!W2 && a_ln == LN_GIVEN) {  // next tile's stats, in flight through the epilogue
       gmean = g.a_stats[2 * arow_n];
       grstd = g.a_stats[2 * arow_n + 1];
     }
@@ -206,18 +248,23 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
     for (int t = 0; t < NT; ++t) acc[t] += *reinterpret_cast<const f32x4*>(ebias + t * 16 + 4 * g4);
     float rm_ = 0.f, rs_ = 1.f, bs = 1.f;
     if (EPI == EPI_LN_GELU) {  // full row in this wave (NCOL == N): the 4 lanes of a position
-      float s = 0.f;
+      // moments on packed pairs straight off the accumulator registers (v_pk_add / v_pk_fma
+      // on .xy / .zw: no repacking moves, half the instructions of per-element scalar code)
+      f32x2 s2 = {0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < NT; ++t) s += (acc[t].x + acc[t].y) + (acc[t].z + acc[t].w);
+      for (int t = 0; t < NT; ++t) s2 += lo2(acc[t]) + hi2(acc[t]);
+      float s = s2.x + s2.y;
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
       rm_ = s / (float)N;
-      float q = 0.f;
+      f32x2 q2 = {0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const f32x4 d = acc[t] - rm_;
-        q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+        const f32x2 d0 = lo2(acc[t]) - rm_, d1 = hi2(acc[t]) - rm_;
+        q2 = d0 * d0 + q2;
+        q2 = d1 * d1 + q2;
       }
+      float q = q2.x + q2.y;
       q += __shfl_xor(q, 16, 64);
       q += __shfl_xor(q, 32, 64);
       rs_ = rsqrtf(q / (float)N + g.e_eps);
@@ -234,10 +281,15 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
       const int colc = min(col, N - 4);
       f32x4 v = acc[t];
       if (EPI == EPI_LN_GELU) {
+        // elw / elb hold HALF the LayerNorm affine (staged x 0.5, exact): the normalised
+        // value comes out as GELU's half input; (v - mean) * rstd as one FMA per pair
         const f32x4 lw = *reinterpret_cast<const f32x4*>(elw + t * 16 + 4 * g4);
         const f32x4 lb = *reinterpret_cast<const f32x4*>(elb + t * 16 + 4 * g4);
-        v = (v - rm_) * rs_ * lw + lb;
-        v = gelu_erf4(v);
+        const float nb = -rm_ * rs_;
+        const f32x2 u0 = lo2(v) * rs_ + nb, u1 = hi2(v) * rs_ + nb;
+        const f32x2 h0 = gelu_half2(u0 * lo2(lw) + lo2(lb));
+        const f32x2 h1 = gelu_half2(u1 * hi2(lw) + hi2(lb));
+        v = f32x4{h0.x, h0.y, h1.x, h1.y};
       } else if (EPI == EPI_RESID) {
         const f32x4 xr = *reinterpret_cast<const f32x4*>(g.r_x + (int64_t)rowc * N + colc);
         if (g.r_stats) {
@@ -253,7 +305,24 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
       // the precision, so the store needs no column test and no runtime type branch
       const bool cv = EPI == EPI_LN_GELU ? true : col < N;
       const bool obf = EPI == EPI_LN_GELU ? P == PREC_BF16 : g.out_bf16 != 0;
-      if (rv && cv) {
+      if constexpr (W2) {
+        // range-checked buffer store (rows >= M dropped by the descriptor): no exec branch,
+        // so the compiler can count these stores and wait for the next tile's loads only
+        if (obf) {
+          bf16x4 o;
+          o[0] = (short)f2bf(v.x);
+          o[1] = (short)f2bf(v.y);
+          o[2] = (short)f2bf(v.z);
+          o[3] = (short)f2bf(v.w);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), orsrc,
+                                                (int)((row * g.ldo + col) * 2), 0, 0);
+        } else if (STAGE) {
+          *reinterpret_cast<f32x4*>(ostg + l15 * OST + t * 16 + 4 * g4) = v;
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), orsrc,
+                                                 (int)((row * g.ldo + col) * 4), 0, 0);
+        }
+      } else if (rv && cv) {
         if (obf) {
           bf16x4 o;
           o[0] = (short)f2bf(v.x);
@@ -266,6 +335,24 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
         }
       }
       if (t % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // bound load hoisting (VGPRs)
+    }
+    if constexpr (STAGE) {
+      // one wave's LDS operations complete in issue order; the fences only keep the compiler
+      // from moving the lanes' exchange
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr int RC = NCOL / 4;  // 16-B chunks per row
+#pragma unroll
+      for (int j = 0; j < 16 * RC / 64; ++j) {
+        const int c = j * 64 + lane, r = c / RC, c4 = c - r * RC;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ostg + r * OST + 4 * c4);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), orsrc,
+                                               (int)(((tile * 16 + r) * g.ldo + 4 * c4) * 4), 0, 0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     arow_c = arow_n;
     rm = rmn;
@@ -311,7 +398,8 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
                      (g.a_map == MAP_IDENTITY) || (g.a_map == MAP_MERGE && g.epi == EPI_STORE);
   if (!known) return 0;
   // the LN+GELU instantiations are specialised to the CCF_FFN pwconv's loader and storage
-  if (g.epi == EPI_LN_GELU && ((g.a_ln != LN_GIVEN && g.a_ln != LN_NONE) || g.a_gelu ||
+  const int64_t out_bytes = g.M * g.ldo * ((g.prec == PREC_BF16 || g.a_bf16) ? 2 : 4);
+  if (g.epi == EPI_LN_GELU && (g.K > 64 || out_bytes >= ((int64_t)1 << 31) || (g.a_ln != LN_GIVEN && g.a_ln != LN_NONE) || g.a_gelu ||
                                (g.out_bf16 != 0) != (g.prec == PREC_BF16 || g.a_bf16 != 0)))
     return 0;
   const bool split = g.prec == PREC_SPLIT;
@@ -329,7 +417,10 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
     }
   }
   if (nt == 0) return 0;
-  const size_t lds = (size_t)nt * 16 * per_col + (size_t)(2 * K32 + 3 * nt * 16) * 4;
+  size_t lds = (size_t)nt * 16 * per_col + (size_t)(2 * K32 + 3 * nt * 16) * 4;
+  if (W2STAGE && g.epi == EPI_LN_GELU && g.prec != PREC_BF16 && !g.a_bf16)  // output staging
+    lds += (size_t)8 * 16 * (nt * 16 + 4) * 4;
+  if (lds > 160 * 1024) return 0;
   const int chunks = tiles / nt;
   if (single_chunk_only && chunks > 1) return 0;
   const int64_t ntiles = (g.M + 15) / 16;

@@ -28,6 +28,8 @@ int check_launch(const char* what);
 // vector types
 // ---------------------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -59,6 +61,9 @@ __device__ __forceinline__ float gelu_erf(float x) {
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// the register pairs of an f32x4 (operands of v_pk_*_f32 without repacking)
+__device__ __forceinline__ f32x2 lo2(f32x4 v) { return __builtin_shufflevector(v, v, 0, 1); }
+__device__ __forceinline__ f32x2 hi2(f32x4 v) { return __builtin_shufflevector(v, v, 2, 3); }
 // GELU on a pair given HALF its input, hx = x / 2:  GELU(x) = x Phi(x) = hx + |hx| erf(sqrt2 |hx|)
 // (no sign restore: x erf(x / sqrt2) = |x| erf(|x| / sqrt2)).  erf by Abramowitz & Stegun 7.1.26
 // as in gelu_erf, with the polynomial's coefficients negated so 1 - p e is one FMA, and the
