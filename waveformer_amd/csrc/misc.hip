@@ -15,7 +15,12 @@ namespace wf {
 // computed out of LDS, then written to the other LDS buffer -- the input stream never waits
 // on a barrier-separated load phase (the one-shot kernel above: 282 us at B = 8, 2.4 TB/s).
 // ---------------------------------------------------------------------------------------
-template <int R>
+// XI = ceil(W / XG) output positions per thread and row, unrolled: with the outputs leaving
+// through range-checked buffer stores (out-of-range x / idle lanes get an offset past the
+// descriptor), every lane issues the same R * XI stores per group, so the wait for the next
+// group's fetch can leave them in flight (vmcnt(R * XI)) instead of draining every store
+// (vmcnt(0)) as the exec-masked store loop forced.  The output must stay below 2^31 bytes.
+template <int R, int XI>
 __global__ __launch_bounds__(256) void patch_embed_stream_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ out, int Cout, int D, int H, int W, int64_t ngroups) {
@@ -69,29 +74,36 @@ __global__ __launch_bounds__(256) void patch_embed_stream_kernel(
       if (j < NLD && i < gper) reinterpret_cast<f32x4*>(dst)[i] = stg[j];
     }
   };
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      out, 0, (int)((int64_t)ngroups * R * W * Cout * 4), 0x00020000);
   auto compute = [&](const float* src, int64_t grp) {
-    if (!act) return;
     const int y0 = (int)(grp % nyb) * R;
-    const int64_t r = grp / nyb;
-    const int z = (int)(r % D), b = (int)(r / D);
+    const int r = (int)(grp / nyb);
+    const int z = r % D, b = r / D;
 #pragma unroll 1
     for (int rr = 0; rr < R; ++rr) {
       const float* sl = src + rr * rowf;
-      float* orow = out + (((int64_t)b * D + z) * H + y0 + rr) * W * (int64_t)Cout;
-      for (int xo = xg; xo < W; xo += XG) {
+      const int orow = ((b * D + z) * H + y0 + rr) * W;
+#pragma unroll
+      for (int i = 0; i < XI; ++i) {
+        const int xo = xg + i * XG;
+        const bool ok = act && xo < W;
+        const int xc = ok ? xo : 0;
         f32x2 a0 = ba, a1 = bb;
 #pragma unroll
         for (int ci = 0; ci < CIN; ++ci)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float2 v = *reinterpret_cast<const float2*>(sl + (ci * 4 + q) * W2 + 2 * xo);
+            const float2 v = *reinterpret_cast<const float2*>(sl + (ci * 4 + q) * W2 + 2 * xc);
             const int k = ci * 8 + 2 * q;
             a0 = wa[k] * v.x + a0;
             a1 = wb[k] * v.x + a1;
             a0 = wa[k + 1] * v.y + a0;
             a1 = wb[k + 1] * v.y + a1;
           }
-        *reinterpret_cast<f32x4*>(orow + (int64_t)xo * Cout + c0) = f32x4{a0.x, a0.y, a1.x, a1.y};
+        const int off = ok ? ((orow + xo) * Cout + c0) * 4 : 0x7fffffff;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, f32x4{a0.x, a0.y, a1.x, a1.y}), orsrc, off, 0, 0);
       }
     }
   };
@@ -513,13 +525,21 @@ extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* b
     const int64_t ngroups = B * D * (H / R);
     const size_t lds = 2 * R * row_lds;
     const int64_t blocks = std::min<int64_t>(ngroups, 256 * 2);  // 2 persistent per CU (LDS)
-    if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(patch_embed_stream_kernel<R>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(patch_embed_stream_kernel<R>, dim3((unsigned)blocks), dim3(256), lds,
-                       (hipStream_t)stream, x, w, bias, out, (int)Cout, (int)D, (int)H, (int)W,
-                       ngroups);
-    return check_launch("wf_patch_embed_fwd");
+    const int xg = 256 / (int)(Cout / 4);
+    const int64_t xi = cdiv(W, xg);
+    void (*k)(const float*, const float*, const float*, float*, int, int, int, int, int64_t) =
+        xi == 1 ? patch_embed_stream_kernel<R, 1> : xi == 2 ? patch_embed_stream_kernel<R, 2>
+      : xi == 3 ? patch_embed_stream_kernel<R, 3> : xi == 4 ? patch_embed_stream_kernel<R, 4>
+      : xi == 5 ? patch_embed_stream_kernel<R, 5> : xi == 6 ? patch_embed_stream_kernel<R, 6>
+                : nullptr;
+    if (k && B * D * H * W * Cout * 4 < ((int64_t)1 << 31) - 16) {
+      if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, x, w,
+                         bias, out, (int)Cout, (int)D, (int)H, (int)W, ngroups);
+      return check_launch("wf_patch_embed_fwd");
+    }
   }
   // rows per workgroup: up to 4 within 32 KB of LDS, while the grid keeps >= 2048 workgroups
   static const int rmax = getenv("WF_PE_ROWS") ? atoi(getenv("WF_PE_ROWS")) : 4;
