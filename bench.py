@@ -468,7 +468,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        # RCCL ("nccl") between the GPUs of a node; WF_BENCH_BACKEND=gloo rehearses the
+        # multi-rank path with several ranks sharing fewer GPUs (rank -> LOCAL_RANK % GPUs)
+        dist.init_process_group(os.environ.get("WF_BENCH_BACKEND", "nccl"), init_method="env://")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from waveformer_amd import _lib, ops
