@@ -44,26 +44,57 @@ __global__ void split_f32_bf16x2_kernel(const float* __restrict__ in, uint16_t* 
 // source pointers, then n destination pointers, all in device memory.  Destination d of
 // weight s holds its [2][numel] {hi, lo} planes, as wf_split_f32_to_bf16x2 writes them.
 template <bool F16>
-__global__ void split_multi_kernel(const int64_t* __restrict__ table, int n, int64_t total) {
+__device__ __forceinline__ void split_one(float v, uint16_t& h, uint16_t& l) {
+  if (F16) {
+    h = f2h(v);
+    l = 0;
+  } else {
+    h = f2bf(v);
+    l = f2bf(v - bf2f(h));
+  }
+}
+
+// A workgroup owns 1024 consecutive elements of the concatenated weights: their first segment
+// is found once (binary search, uniform), each thread walks forward from it for its 4
+// elements, which move as one float4 load + two 8-B stores when they sit in one segment at a
+// 4-aligned offset (every weight of the Python arena: numel % 8 == 0), element by element
+// otherwise.  (A per-element binary search over the table ran the launch at ~3 TB/s.)
+template <bool F16>
+__global__ __launch_bounds__(256) void split_multi_kernel(const int64_t* __restrict__ table,
+                                                          int n, int64_t total) {
   const int64_t* pre = table;
   const float* const* src = reinterpret_cast<const float* const*>(table + n + 1);
   uint16_t* const* dst = reinterpret_cast<uint16_t* const*>(table + 2 * n + 1);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    int lo = 0, hi = n - 1;  // last segment with pre[s] <= i
+  for (int64_t base = (int64_t)blockIdx.x * 1024; base < total; base += (int64_t)gridDim.x * 1024) {
+    int lo = 0, hi = n - 1;  // last segment with pre[s] <= base
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (pre[mid] <= i) lo = mid; else hi = mid - 1;
+      if (pre[mid] <= base) lo = mid; else hi = mid - 1;
     }
-    const int64_t j = i - pre[lo], m = pre[lo + 1] - pre[lo];
-    const float v = src[lo][j];
-    if (F16) {
-      dst[lo][j] = f2h(v);
-      dst[lo][m + j] = 0;
+    const int64_t i = base + 4 * (int64_t)threadIdx.x;
+    if (i >= total) continue;
+    int sg = lo;
+    while (sg + 1 < n && pre[sg + 1] <= i) ++sg;
+    const int64_t j = i - pre[sg], m = pre[sg + 1] - pre[sg];
+    if (j + 4 <= m && (j & 3) == 0) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src[sg] + j);
+      uint16_t h[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split_one<F16>(v[e], h[e], l[e]);
+      *reinterpret_cast<uint2*>(dst[sg] + j) =
+          uint2{(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+      *reinterpret_cast<uint2*>(dst[sg] + m + j) =
+          uint2{(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
     } else {
-      const uint16_t h = f2bf(v);
-      dst[lo][j] = h;
-      dst[lo][m + j] = f2bf(v - bf2f(h));
+      for (int e = 0; e < 4 && i + e < total; ++e) {
+        const int64_t ie = i + e;
+        while (sg + 1 < n && pre[sg + 1] <= ie) ++sg;
+        const int64_t je = ie - pre[sg], me = pre[sg + 1] - pre[sg];
+        uint16_t hh, ll;
+        split_one<F16>(src[sg][je], hh, ll);
+        dst[sg][je] = hh;
+        dst[sg][me + je] = ll;
+      }
     }
   }
 }
@@ -104,8 +135,8 @@ static int split_multi(const int64_t* table_dev, int64_t n, int64_t total, void*
   WF_REQUIRE(n >= 0 && total >= 0, "negative count");
   if (n == 0 || total == 0) return WF_OK;
   WF_REQUIRE_PTR(table_dev);
-  int64_t blocks = wf::cdiv(total, 256);
-  if (blocks > 8192) blocks = 8192;
+  int64_t blocks = wf::cdiv(total, 1024);
+  if (blocks > 65535) blocks = 65535;
   if (f16)
     hipLaunchKernelGGL(wf::split_multi_kernel<true>, dim3((unsigned)blocks), dim3(256), 0,
                        (hipStream_t)stream, table_dev, (int)n, total);
