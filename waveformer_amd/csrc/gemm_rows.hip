@@ -18,10 +18,6 @@
 // so each call site compiles to straight-line code with 32-bit index math.
 #include "gemm_common.hpp"
 
-#ifndef W2STAGE
-#define W2STAGE 1
-#endif
-
 namespace wf {
 
 template <int NT, int P, int MAP, int EPI, bool ABF16>
@@ -67,7 +63,7 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
   float* elb = elw + NCOL;
   // fp32 W2 output restaged per wave in LDS so each store instruction writes 1 KB of the
   // tile's 16 contiguous rows (the accumulator layout writes 16 rows x 64 B per instruction)
-  constexpr bool STAGE = W2STAGE && EPI == EPI_LN_GELU && P != PREC_BF16;
+  constexpr bool STAGE = EPI == EPI_LN_GELU && P != PREC_BF16;
   constexpr int OST = NCOL + 4;  // staged row stride in floats (16-B pad)
   float* ostg = elb + NCOL + (STAGE ? (threadIdx.x >> 6) * 16 * OST : 0);
   for (int i = tid; i < K32; i += blockDim.x) {
@@ -418,7 +414,7 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
   }
   if (nt == 0) return 0;
   size_t lds = (size_t)nt * 16 * per_col + (size_t)(2 * K32 + 3 * nt * 16) * 4;
-  if (W2STAGE && g.epi == EPI_LN_GELU && g.prec != PREC_BF16 && !g.a_bf16)  // output staging
+  if (g.epi == EPI_LN_GELU && g.prec != PREC_BF16 && !g.a_bf16)  // output staging
     lds += (size_t)8 * 16 * (nt * 16 + 4) * 4;
   if (lds > 160 * 1024) return 0;
   const int chunks = tiles / nt;
