@@ -634,8 +634,7 @@ int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, 
   if (use_win && !f16 && hd == 16 && attn_win_lds(N, hd, split) <= 80 * 1024) {
     const size_t lds = attn_win_lds(N, hd, split);
     auto k = split ? attn_win_kernel<16, PREC_SPLIT> : attn_win_kernel<16, PREC_BF16>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    set_max_lds(reinterpret_cast<const void*>(k), (int)lds);
     hipLaunchKernelGGL(k, grid, dim3(256), lds, s, qkv, bias, out, lse, N, heads, sl2);
     return check_launch("attention core (window-resident)");
   }

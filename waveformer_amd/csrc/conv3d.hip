@@ -361,8 +361,7 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
     auto kern = prec == PREC_SPLIT  ? conv3d_k3_kernel<CO_T, NT, PREC_SPLIT, false, 1>
                 : prec == PREC_FP16 ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, false, RW>
                                     : conv3d_k3_kernel<CO_T, NT, PREC_BF16, false, RW>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
   }
   int rc = check_launch("wf_conv3d_k3_fwd");

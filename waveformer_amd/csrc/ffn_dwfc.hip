@@ -687,8 +687,7 @@ static int go_dwfc(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks) {
   void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_dwfc_kernel<C, HID, TY, TX, PREC_SPLIT, float>
                            : prec == PREC_FP16 ? ffn_dwfc_kernel<C, HID, TY, TX, PREC_FP16, float>
                                                : ffn_dwfc_kernel<C, HID, TY, TX, PREC_BF16, uint16_t>;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::LDS_BYTES);
+  set_max_lds(reinterpret_cast<const void*>(kern), (int)K::LDS_BYTES);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(K::NTH), K::LDS_BYTES, s, g);
   return check_launch("ffn_dwfc");
 }
@@ -713,8 +712,7 @@ static int go_dwfc_ws(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks
   void (*kern)(DwFcArgs) = prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>
                            : prec == PREC_FP16 ? ffn_dwfc_ws_kernel<PREC_FP16, float>
                                                : ffn_dwfc_ws_kernel<PREC_BF16, uint16_t>;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(K::NTH), lds, s, g);
   return check_launch("ffn_dwfc_ws");
 }

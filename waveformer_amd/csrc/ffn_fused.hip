@@ -462,8 +462,7 @@ int launch_ffn_fused(const DwFcArgs& a, int prec, hipStream_t s) {
   void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_fused_kernel<PREC_SPLIT>
                            : prec == PREC_FP16 ? ffn_fused_kernel<PREC_FP16>
                                                : ffn_fused_kernel<PREC_BF16>;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
+  set_max_lds(reinterpret_cast<const void*>(kern), (int)LDS_BYTES);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTH), LDS_BYTES, s, g);
   return check_launch("ffn_fused");
 }

@@ -334,8 +334,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
   const unsigned blocks = (unsigned)cdiv(g.M, BM);
   auto go = [&](auto kern) {
     if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, g);
   };
   if (split) {

@@ -330,8 +330,7 @@ static void go_kc(const GemmArgs& g, hipStream_t s) {
   const size_t lds = (size_t)2 * (split ? 2 : 1) * C::NC * KC_KP * 2 +
                      (g.a_ln != LN_NONE ? (size_t)2 * cdiv(g.K, KC_BK) * KC_BK * 4 : 0);
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
   const dim3 grid((unsigned)cdiv(g.M, C::ROWS), (unsigned)(g.N / C::NC));
   hipLaunchKernelGGL(kern, grid, dim3(C::NTHR), lds, s, g);
 }

@@ -367,8 +367,7 @@ static void go_rows(const GemmArgs& g, dim3 grid, size_t lds, hipStream_t s) {
   else
     kern = gemm_rows_kernel<NT, PREC_BF16, MAP, EPI, false>;
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
   hipLaunchKernelGGL(kern, grid, dim3(512), lds, s, g);
 }
 

@@ -534,8 +534,7 @@ extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* b
                 : nullptr;
     if (k && B * D * H * W * Cout * 4 < ((int64_t)1 << 31) - 16) {
       if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        set_max_lds(reinterpret_cast<const void*>(k), (int)lds);
       hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, x, w,
                          bias, out, (int)Cout, (int)D, (int)H, (int)W, ngroups);
       return check_launch("wf_patch_embed_fwd");

@@ -1,7 +1,20 @@
 // wf_api.hip -- error plumbing and small utilities of the C-ABI (include/waveformer_hip.h).
 #include "kernels.hpp"
 
+#include <mutex>
+#include <unordered_map>
+
 namespace wf {
+void set_max_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> done;
+  std::lock_guard<std::mutex> lock(mu);
+  int& cur = done[fn];
+  if (bytes > cur) {
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    cur = bytes;
+  }
+}
 
 static thread_local std::string g_last_error;
 
@@ -123,8 +136,7 @@ extern "C" int wf_abi_version(void) { return WF_ABI_VERSION; }
 extern "C" int wf_debug_poison_lds(int64_t blocks, int lds_bytes, void* stream) {
   WF_REQUIRE(blocks >= 1 && blocks <= (1 << 20), "blocks out of range");
   WF_REQUIRE(lds_bytes >= 4 && lds_bytes <= 160 * 1024, "lds_bytes out of range");
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wf::poison_lds_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  wf::set_max_lds(reinterpret_cast<const void*>(wf::poison_lds_kernel), lds_bytes);
   hipLaunchKernelGGL(wf::poison_lds_kernel, dim3((unsigned)blocks), dim3(256), (size_t)lds_bytes,
                      (hipStream_t)stream, lds_bytes / 4);
   return wf::check_launch("wf_debug_poison_lds");

@@ -14,6 +14,9 @@ namespace wf {
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int check_launch(const char* what);
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per kernel and size (not before every
+// launch: re-setting it while the same kernel is in flight on another queue is avoided)
+void set_max_lds(const void* fn, int bytes);
 
 #define WF_REQUIRE(cond, msg)                                              \
   do {                                                                     \
