@@ -374,7 +374,7 @@ def main_sliding(args, world, rank, dev):
         if rl:
             out["roofline"] = rl.get("conv3d_k3", next(iter(rl.values())))
             out["rooflines"] = rl
-        print(json.dumps(out), flush=True)
+        print(json.dumps(_stamp(out, args, world)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -401,7 +401,8 @@ def main_train(args, world, rank, dev):
     ddp = model
     if world > 1:
         ddp = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[dev.index], bucket_cap_mb=64, gradient_as_bucket_view=True)
+            model, device_ids=[dev.index], bucket_cap_mb=64, gradient_as_bucket_view=True,
+            find_unused_parameters=True)  # as the reference trainer (trainer.py:355-358)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-4)
     loss_fn = DiceCELoss(to_onehot_y=True, softmax=True)
     g = torch.Generator(device=dev).manual_seed(1 + rank)
@@ -456,24 +457,79 @@ def main_train(args, world, rank, dev):
             "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2),
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(_stamp(out, args, world)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
+def _stamp(out, args, world):
+    """The distinct GPUs behind the ranks; a gloo rehearsal that folds ranks onto fewer GPUs is
+    marked as such (its value is not an N-GPU number)."""
+    dv = getattr(args, "devices", world)
+    out["devices"] = dv
+    if dv < world:
+        out["rehearsal"] = f"{world} ranks on {dv} GPU(s) over {os.environ.get('WF_BENCH_BACKEND')}"
+    return out
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, n, port):
+    """The torch.distributed.run command that starts `n` ranks of this script with the same
+    arguments (one process per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_launch_ranks(args):
+    """`python bench.py --gpus N` from a plain shell (no WORLD_SIZE in the environment): start
+    the N ranks as ONE child process -- torch.distributed.run, the way the reference's own
+    launcher re-launches itself (light_training/launch.py:81-112) -- and return its exit code.
+    Rank 0's JSON line reaches our stdout directly (the child inherits it).  Nothing here has
+    touched the GPU: the ranks initialise their own devices.  None when this process is
+    already a rank or N == 1."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+    return subprocess.call(launcher_cmd(sys.argv[1:], args.gpus, _free_port()))
+
+
 def main():
     args = parse()
+    rc = maybe_launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: launch one rank "
+                         f"per GPU (or run `python bench.py --gpus N` and let it start them)")
+    backend = os.environ.get("WF_BENCH_BACKEND", "nccl")
     if world > 1:
         # RCCL ("nccl") between the GPUs of a node; WF_BENCH_BACKEND=gloo rehearses the
         # multi-rank path with several ranks sharing fewer GPUs (rank -> LOCAL_RANK % GPUs)
-        dist.init_process_group(os.environ.get("WF_BENCH_BACKEND", "nccl"), init_method="env://")
-    local = local % max(1, torch.cuda.device_count())
+        dist.init_process_group(backend, init_method="env://")
+    ngpu = torch.cuda.device_count()
+    if local >= ngpu:
+        if backend != "gloo":
+            raise SystemExit(f"bench.py: LOCAL_RANK {local} but only {ngpu} GPUs visible")
+        local = local % max(1, ngpu)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # distinct GPUs behind the ranks (a gloo rehearsal may fold several ranks onto one)
+    args.devices = world
+    if world > 1:
+        locs = [None] * world
+        dist.all_gather_object(locs, local)
+        args.devices = len(set(locs))
     from waveformer_amd import _lib, ops
     _lib.load()  # fail loudly without the HIP library
     ops.set_precision(args.precision)
@@ -608,7 +664,7 @@ def main():
                 out["parity"] = {"error": str(e)[:200]}
         if args.cpu_baseline and world == 1 and not full:
             out["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(out), flush=True)
+        print(json.dumps(_stamp(out, args, world)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

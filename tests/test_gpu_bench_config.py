@@ -76,6 +76,14 @@ def test_encoder128_b8_graph_replay_vs_b1_and_reference():
         assert abs(sums[2] - ref[2]) <= 10 * tol * math.sqrt(ref[1]), k
         assert C.rel_l2(sample, C.g(k + "__sample")) <= tol, k
 
+    # the graph replay against a second, eager B = 8 forward: bit-identical (same kernels, same
+    # launch shapes); on a mismatch the message names the tensor and the differing region, so
+    # the failing run itself says which side and where
+    with torch.no_grad():
+        eager = _flat(case, m(x))
+    for k, t in got.items():
+        assert torch.equal(t, eager[k]), f"graph replay vs eager B=8, {k}: {_region(t, eager[k])}"
+
     # every volume against its own B = 1 eager forward, full tensors
     worst = 0.0
     for b in range(B):
@@ -84,5 +92,18 @@ def test_encoder128_b8_graph_replay_vs_b1_and_reference():
         for k, t in got.items():
             e = _rel(t[b:b + 1], one[k])
             worst = max(worst, e)
-            assert e <= 1e-6, (b, k, e)
+            assert e <= 1e-6, (b, k, e, _region(t[b:b + 1], one[k]), _region(eager[k][b:b + 1], one[k]))
     print(f"B=8 graph vs B=1 eager: worst rel-L2 {worst:.3e}")
+
+
+def _region(a, b):
+    """Extent of the elements that differ between two (B, C, D, H, W) tensors: samples,
+    channel / z / y / x ranges, count, max difference."""
+    d = (a.double() - b.double()).abs()
+    nz = (d > 0).nonzero()
+    if nz.numel() == 0:
+        return "identical"
+    lo, hi = nz.min(0).values.tolist(), nz.max(0).values.tolist()
+    ax = "bczyx" if a.dim() == 5 else "".join(str(i) for i in range(a.dim()))
+    ext = ", ".join(f"{n} {l}-{h}" for n, l, h in zip(ax, lo, hi))
+    return f"{nz.shape[0]} elements, {ext}, max {d.max().item():.3e}"

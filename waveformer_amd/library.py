@@ -192,13 +192,17 @@ idwt3d.register_autograd(_idwt3d_bwd, setup_context=_idwt3d_setup)
 def window_attn(x: Tensor, ln_w: Optional[Tensor], ln_b: Optional[Tensor], eps: float,
                 wqkv: Tensor, bqkv: Optional[Tensor], table: Tensor, index: Tensor,
                 wproj: Tensor, bproj: Optional[Tensor], ws: int, heads: int, scale: float,
-                prec: int, train: bool) -> Tuple[Tensor, Tensor, Tensor]:
+                prec: int, train: bool, index_formula: bool = False
+                ) -> Tuple[Tensor, Tensor, Tensor]:
     """Attention over the ws^3 windows of a channel-last raster x (B, D1, H1, W1, C) ->
-    (out (B, D1, H1, W1, C), workspace, lse); workspace / lse are empty unless train."""
+    (out (B, D1, H1, W1, C), workspace, lse); workspace / lse are empty unless train.
+    index_formula: the caller vouches that `index` equals the reference's formula
+    (attention.py:40-56) -- Attention checks it at init and on load_state_dict -- so the
+    table-bias kernel may evaluate the formula itself instead of reading `index`."""
     C = x.shape[-1]
     ln = (ln_w, ln_b, eps) if ln_w is not None else None
     if not train:
-        bias = ops.attention_bias(table, index, ws, heads, C // heads)
+        bias = ops.attention_bias(table, index, ws, heads, C // heads, index_formula)
         out = ops.window_attention(x, wqkv, bqkv, bias, wproj, bproj, ws, heads, scale, ln,
                                    prec=prec)
         return out, _empty(x), _empty(x, torch.float32)
@@ -220,7 +224,7 @@ def window_attn(x: Tensor, ln_w: Optional[Tensor], ln_b: Optional[Tensor], eps: 
 
 @window_attn.register_fake
 def _(x, ln_w, ln_b, eps, wqkv, bqkv, table, index, wproj, bproj, ws, heads, scale, prec,
-      train):
+      train, index_formula=False):
     if not train:
         return torch.empty_like(x), _empty(x), _empty(x, torch.float32)
     B, D1, H1, W1, C = x.shape
@@ -231,7 +235,7 @@ def _(x, ln_w, ln_b, eps, wqkv, bqkv, table, index, wproj, bproj, ws, heads, sca
 
 def _attn_setup(ctx, inputs, output):
     (x, ln_w, ln_b, eps, wqkv, bqkv, table, index, wproj, bproj, ws, heads, scale, prec,
-     train) = inputs
+     train, _formula) = inputs
     _, work, lse = output
     ctx.meta = (ws, heads, float(scale), float(eps), bool(train))
     ctx.save_for_backward(x, ln_w, ln_b, wqkv, bqkv, table, index, wproj, bproj, work, lse)
@@ -306,7 +310,7 @@ def _attn_bwd(ctx, gout, _gwork, _glse):
                                                   scale)
     opt = lambda g, t: g if t is not None else None  # noqa: E731
     return (dx, opt(dlnw, ln_w), opt(dlnb, ln_b), None, dwqkv, opt(dbqkv, bqkv), dtable, None,
-            dwproj, opt(dbproj, bproj), None, None, None, None, None)
+            dwproj, opt(dbproj, bproj), None, None, None, None, None, None)
 
 
 window_attn.register_autograd(_attn_bwd, setup_context=_attn_setup)

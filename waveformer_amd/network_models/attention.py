@@ -47,8 +47,16 @@ class Attention(nn.Module):
         self.relative_position_bias_table = nn.Parameter(
             torch.zeros((2 * window_size - 1) ** 3, num_heads))
         self.register_buffer("relative_position_index", relative_position_index(window_size))
+        # the index equals the reference's formula (re-checked when a state_dict is loaded):
+        # the table-bias kernel then evaluates the formula in-kernel instead of reading it
+        self._index_formula = True
         nn.init.trunc_normal_(self.relative_position_bias_table, std=.02)
         self.softmax = nn.Softmax(dim=-1)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+        self._index_formula = ops.index_is_formula(self.relative_position_index,
+                                                   self.window_size)
 
     def _check_train(self):
         if self.training and (self.attn_drop.p > 0 or self.proj_drop.p > 0):
@@ -73,7 +81,7 @@ class Attention(nn.Module):
                                      self.relative_position_bias_table,
                                      self.relative_position_index, self.proj.weight,
                                      self.proj.bias, self.window_size, self.num_heads,
-                                     float(self.scale), prec, train)
+                                     float(self.scale), prec, train, self._index_formula)
         return out
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

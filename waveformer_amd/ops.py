@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import threading
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -103,7 +104,12 @@ def prec_id() -> int:
 class WeightArena:
     """The [2][numel] 16-bit planes of a list of fp32 CUDA weights in one buffer -- bf16
     {hi, lo} (f16=False) or {fp16, 0} (f16=True, WF_PREC_FP16) -- refreshed by one
-    wf_split_f32_to_bf16x2_multi / wf_cast_f32_to_f16x2_multi launch."""
+    wf_split_f32_to_bf16x2_multi / wf_cast_f32_to_f16x2_multi launch.
+
+    Stream safety: the forward that used the arena last records an event on its stream when
+    its scope closes; a refresh issued on another stream waits for that event first, so a
+    forward on stream B never rewrites planes that stream A's kernels still read (graph
+    capture skips the event: a captured graph replays on its own stream, in order)."""
 
     def __init__(self, params: Sequence[torch.Tensor], f16: bool = False):
         dev = params[0].device
@@ -124,10 +130,26 @@ class WeightArena:
         self.n, self.total = len(params), pre[-1]
         table = pre + [p.data_ptr() for p in params] + dsts
         self.table = torch.tensor(table, dtype=torch.int64).to(dev)
+        self.done: Optional[torch.cuda.Event] = None   # last forward's end, on done_stream
+        self.done_stream = None
 
     def refresh(self) -> None:
+        cur = torch.cuda.current_stream(self.buf.device)
+        if (self.done is not None and self.done_stream != cur.cuda_stream
+                and not torch.cuda.is_current_stream_capturing()):
+            cur.wait_event(self.done)
         _lib.call("wf_cast_f32_to_f16x2_multi" if self.f16 else "wf_split_f32_to_bf16x2_multi",
-                  self.table.data_ptr(), self.n, self.total, _stream())
+                  self.table.data_ptr(), self.n, self.total, cur.cuda_stream)
+
+    def release(self) -> None:
+        """The forward that refreshed the arena has issued its last kernel."""
+        if torch.cuda.is_current_stream_capturing():
+            return
+        cur = torch.cuda.current_stream(self.buf.device)
+        if self.done is None:
+            self.done = torch.cuda.Event()
+        self.done.record(cur)
+        self.done_stream = cur.cuda_stream
 
 
 class _Scope:
@@ -136,7 +158,11 @@ class _Scope:
         self.cache: Dict[tuple, torch.Tensor] = {}
 
 
-_scope: Optional[_Scope] = None
+_tls = threading.local()  # the open weight_scope of THIS thread (two threads: two scopes)
+
+
+def _cur_scope() -> Optional[_Scope]:
+    return getattr(_tls, "scope", None)
 
 
 def split_params(module: torch.nn.Module) -> List[torch.Tensor]:
@@ -159,15 +185,14 @@ class weight_scope:
     """`with ops.weight_scope(model): ...` -- one forward of `model`: its split weights are
     re-split in one launch on entry and looked up by every kernel wrapper inside; derived
     forms of other weights (packed conv weights, dense attention biases) are made once per
-    scope.  Nested scopes reuse the outer one."""
+    scope.  Nested scopes reuse the outer one.  Scopes are per thread."""
 
     def __init__(self, module: torch.nn.Module):
         self.module = module
         self.owner = False
 
     def __enter__(self):
-        global _scope
-        if _scope is not None:
+        if _cur_scope() is not None:
             return self
         arena = None
         params = split_params(self.module)
@@ -185,24 +210,27 @@ class weight_scope:
                 arena = WeightArena(params, f16)
                 arenas[f16] = arena
             arena.refresh()
-        _scope = _Scope(arena)
+        _tls.scope = _Scope(arena)
         self.owner = True
         return self
 
     def __exit__(self, *exc):
-        global _scope
         if self.owner:
-            _scope = None
+            sc = _cur_scope()
+            if sc is not None and sc.arena is not None:
+                sc.arena.release()
+            _tls.scope = None
 
 
 def per_forward(key: tuple, make):
     """make() once per weight_scope (once per call outside any scope)."""
-    if _scope is None:
+    sc = _cur_scope()
+    if sc is None:
         return make()
-    v = _scope.cache.get(key)
+    v = sc.cache.get(key)
     if v is None:
         v = make()
-        _scope.cache[key] = v
+        sc.cache[key] = v
     return v
 
 
@@ -213,8 +241,9 @@ def split_weight(p: torch.Tensor, shape: Optional[Tuple[int, ...]] = None,
     (wf_cast_f32_to_f16x2).  The weight arena's view inside a weight_scope, else made now."""
     shp = (2,) + tuple(p.shape if shape is None else shape)
     f16 = (_prec() if prec is None else prec) == FP16
-    if _scope is not None and _scope.arena is not None and _scope.arena.f16 == f16:
-        v = _scope.arena.views.get(p.data_ptr())
+    sc = _cur_scope()
+    if sc is not None and sc.arena is not None and sc.arena.f16 == f16:
+        v = sc.arena.views.get(p.data_ptr())
         if v is not None and v.numel() == 2 * p.numel():
             return v.view(shp)
 
@@ -735,31 +764,25 @@ def rel_pos_bias(table: torch.Tensor, index: torch.Tensor) -> torch.Tensor:
     return out
 
 
-_TABLE_OK: Dict[tuple, bool] = {}
-
-
 def index_is_formula(index: torch.Tensor, ws: int) -> bool:
     """relative_position_index == the reference's formula for window ws (attention.py:40-56)?
-    Cached per (buffer, version): the table-bias kernel evaluates the formula itself."""
-    key = (index.data_ptr(), index._version, ws, str(index.device))
-    ok = _TABLE_OK.get(key)
-    if ok is None:
-        r = torch.arange(ws, device=index.device)
-        s, h, w = torch.meshgrid(r, r, r, indexing="ij")
-        pos = torch.stack([s.reshape(-1), h.reshape(-1), w.reshape(-1)], dim=-1)
-        d = pos[:, None, :] - pos[None, :, :] + (ws - 1)
-        ref = d[..., 0] * (3 * ws - 1) + d[..., 1] * (2 * ws - 1) + d[..., 2]
-        ok = tuple(index.shape) == tuple(ref.shape) and bool(torch.equal(index, ref))
-        _TABLE_OK[key] = ok
-    return ok
+    A host-synchronising check: Attention runs it at init and on load_state_dict, never in a
+    forward."""
+    r = torch.arange(ws)
+    s, h, w = torch.meshgrid(r, r, r, indexing="ij")
+    pos = torch.stack([s.reshape(-1), h.reshape(-1), w.reshape(-1)], dim=-1)
+    d = pos[:, None, :] - pos[None, :, :] + (ws - 1)
+    ref = d[..., 0] * (3 * ws - 1) + d[..., 1] * (2 * ws - 1) + d[..., 2]
+    return tuple(index.shape) == tuple(ref.shape) and bool(torch.equal(index.detach().cpu(), ref))
 
 
 def attention_bias(table: torch.Tensor, index: torch.Tensor, ws: int, heads: int,
-                   head_dim: int) -> torch.Tensor:
+                   head_dim: int, formula: bool = False) -> torch.Tensor:
     """What the window-attention kernels read as the bias: the ((2ws-1)^3, heads) table itself
-    when the table-bias kernel applies (ws 8, head_dim 16, index == the formula), else the
-    dense (heads, N, N) expansion, made once per weight_scope."""
-    if ws == 8 and head_dim == 16 and index_is_formula(index, ws):
+    when the table-bias kernel applies (ws 8, head_dim 16, and the caller vouches that the
+    index is the reference's formula), else the dense (heads, N, N) expansion, made once per
+    weight_scope."""
+    if ws == 8 and head_dim == 16 and formula:
         return table.detach()
     return per_forward(("relbias", table.data_ptr(), index.data_ptr()),
                        lambda: rel_pos_bias(table.detach(), index))
