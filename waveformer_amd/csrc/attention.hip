@@ -442,16 +442,51 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
 // Table-bias attention for the default window (ws 8: N = 512 tokens, head_dim 16), one
 // workgroup per (window, head) -- or per 1/2 or 1/4 of its queries when there are too few
 // windows to fill the chip.  K and V are split into bf16 hi / lo ONCE per (window, head) and
-// staged in LDS (76 KB: two workgroups per CU), instead of once per 64-query workgroup.  Every
+// staged in LDS (68 KB: two workgroups per CU), instead of once per 64-query workgroup.  Every
 // product runs on v_mfma_f32_16x16x32_bf16:
-//   S^T = K Q^T : the K = 32 reduction packs [Kh | Kl] against [Qh | Qh] (Kh Qh + Kl Qh in one
-//                 MFMA), a second MFMA adds Kh Ql ([Kh | Kl] against [Ql | 0]);
+//   S^T = K Q'^T + B : the K = 32 reduction packs [Kh | Kl] against [Q'h | Q'h] (Kh Q'h + Kl Q'h
+//                 in one MFMA), a second MFMA adds Kh Q'l ([Kh | Kl] against [Q'l | 0]).  Q' is
+//                 Q pre-scaled by scale * log2 e, and the accumulator STARTS at the bias
+//                 (log2 e-scaled table entries), so the MFMA output is already the exp2-domain
+//                 logit: no scale / bias pass on the VALU;
 //   O^T = V^T P^T : 32 keys per MFMA, the B operand is the lane's two 4-key score quads of two
 //                 16-key sub-tiles as they come out of the S MFMAs (the K-slot order is matched
-//                 by reading V at the same keys), x3 for the split.
+//                 by reading V at the same keys), x3 for the split;
+//   l   = 1^T P^T : the softmax row sums on the same B operands (a ones A operand, hi + lo),
+//                 instead of an add per score on the VALU; every accumulator row holds the sum.
 // The bias index is the reference's formula (attention.py:40-56, Q2 depth stride 3 ws - 1)
 // with the key part reduced to per-tile constants: a 64-key tile is one z slice of the window.
+// The table is staged REVERSED, so a lane's 16 bias values of a tile are 4 ascending runs of 4
+// at one per-tile base + compile-time offsets 30 kt + i (ds_read2_b32 immediate offsets).
+// K rows are 64 B (hi 16 | lo 16) with the four 16-B chunks XOR-swizzled by (row / 4) & 3
+// through {0, 2, 3, 1}: every 16-lane group of a ds_read_b128 (gfx950 groups lanes
+// {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) then hits 16 distinct 4-bank sets -- the
+// round-2 80-B padded rows were 2-way conflicted (SQ_LDS_BANK_CONFLICT ~ SQ_INSTS_LDS).
 template <int P>
+__device__ __forceinline__ void load8_split_scaled(const void* base, int64_t off, float sc,
+                                                   bf16x8& hi, bf16x8& lo) {
+  if (store32(P)) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(base) + off);
+    const f32x4 a = p[0] * sc, b = p[1] * sc;
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint16_t h = op_cvt<P>(v[j]);
+      hi[j] = (short)h;
+      lo[j] = op_lo<P>(v[j], h);
+    }
+  } else {
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const uint16_t*>(base) + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hi[j] = (short)f2bf(bf2f((uint16_t)r[j]) * sc);
+  }
+}
+
+__device__ __forceinline__ int kswz(int row) {  // 16-B chunk XOR of a K row (see above)
+  return (0x1E0 >> (2 * ((row >> 2) & 3))) & 3;   // {0, 2, 3, 1}[(row >> 2) & 3]
+}
+
+template <int P, int DIAG = 0>
 __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict__ qkv,
                                                           const float* __restrict__ table,
                                                           void* __restrict__ out, int heads,
@@ -459,11 +494,15 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
   constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   constexpr int N = 512, HD = 16;
   constexpr int TBLN = 547;      // reachable rows of the (15^3, heads) table under Q2
-  constexpr int KS = 40;         // K row: hi[16] | lo[16] | pad (80 B: conflict-free b128)
-  constexpr int VQ = (N / 4) * HD * 4;
+  constexpr int KS = 32;         // K row: hi[16] | lo[16], chunks swizzled (kswz)
+  // V: [hi, lo][key/4][hd][4 keys], each key-quad block padded to 136 B so the staging
+  // stores (lanes 64 / 128 B apart) spread over the banks; the loop's 16-lane reads stay
+  // contiguous inside one block
+  constexpr int VB = HD * 4 + 4;
+  constexpr int VQ = (N / 4) * VB;
   __shared__ __attribute__((aligned(16))) uint16_t Ks[N * KS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vq[2 * VQ];  // [hi, lo][key/4][hd][4 keys]
-  __shared__ float tb[TBLN];
+  __shared__ __attribute__((aligned(16))) uint16_t Vq[2 * VQ];
+  __shared__ __attribute__((aligned(16))) float tbr[TBLN + 1];  // reversed, x log2 e
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int qs, h;
   int64_t bw;
@@ -472,13 +511,14 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
   const int64_t row0 = bw * N;
   const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
 
-  for (int i = tid; i < TBLN; i += 512) tb[i] = table[(int64_t)i * heads + h] * 1.4426950408889634f;
+  for (int i = tid; i < TBLN; i += 512)
+    tbr[TBLN - 1 - i] = table[(int64_t)i * heads + h] * 1.4426950408889634f;
   for (int it = tid; it < N * 2; it += 512) {  // K: (key, 8-value chunk)
-    const int key = it >> 1, ch = it & 1;
+    const int key = it >> 1, ch = it & 1, sw = kswz(key);
     bf16x8 hi = z8, lo = z8;
     load8_split<P>(qkv, (row0 + key) * ld + C + h * HD + ch * 8, hi, lo);
-    *reinterpret_cast<bf16x8*>(&Ks[key * KS + ch * 8]) = hi;
-    *reinterpret_cast<bf16x8*>(&Ks[key * KS + 16 + ch * 8]) = SPLIT ? lo : z8;
+    *reinterpret_cast<bf16x8*>(&Ks[key * KS + 8 * (ch ^ sw)]) = hi;
+    *reinterpret_cast<bf16x8*>(&Ks[key * KS + 8 * ((2 + ch) ^ sw)]) = SPLIT ? lo : z8;
   }
   for (int it = tid; it < (N / 4) * 2; it += 512) {  // V: (key quad, 8-value chunk)
     const int k4 = it >> 1, ch = it & 1;
@@ -491,7 +531,7 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int o = ((k4 * HD) + ch * 8 + j) * 4;
+      const int o = k4 * VB + (ch * 8 + j) * 4;
       *reinterpret_cast<bf16x4*>(&Vq[o]) = bf16x4{vh[0][j], vh[1][j], vh[2][j], vh[3][j]};
       if (SPLIT) *reinterpret_cast<bf16x4*>(&Vq[VQ + o]) = bf16x4{vl[0][j], vl[1][j], vl[2][j], vl[3][j]};
     }
@@ -499,66 +539,68 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
   __syncthreads();
 
   const int l15 = lane & 15, g4 = lane >> 4;
+  const int kch = 8 * (g4 ^ kswz(l15));  // this lane's K chunk (rows t*64 + kt*16 + l15)
+  const short one = (short)op_cvt<P>(1.0f);
+  const bf16x8 ones = bf16x8{one, one, one, one, one, one, one, one};
   const int nsub = N / 16 / qsplit;  // 16-query sub-tiles of this workgroup
   for (int st = wid; st < nsub; st += 8) {
     const int q = qs * (N / qsplit) + st * 16 + l15;
-    // B operands of S: slots 8 g4 .. +7 <- Q[q][8 (g4 & 1) ..]: [Qh | Qh] and [Ql | 0]
+    // B operands of S: slots 8 g4 .. +7 <- Q'[q][8 (g4 & 1) ..]: [Q'h | Q'h] and [Q'l | 0]
     bf16x8 b1 = z8, b2 = z8;
     {
       bf16x8 hi = z8, lo = z8;
-      load8_split<P>(qkv, (row0 + q) * ld + h * HD + 8 * (g4 & 1), hi, lo);
+      load8_split_scaled<P>(qkv, (row0 + q) * ld + h * HD + 8 * (g4 & 1), scale_log2, hi, lo);
       b1 = hi;
       b2 = (SPLIT && g4 < 2) ? lo : z8;
     }
     const int qz = q >> 6, qy = (q >> 3) & 7, qx = q & 7;
-    const int ib = (qz + 7) * 23 + (qy + 7) * 15 + (qx + 7) - ((g4 >> 1) * 15 + 4 * (g4 & 1));
+    // reversed-table base of tile 0: (TBLN - 1) - index(q, key (0, 2 (g4 >> 1), 4 (g4 & 1)))
+    const int rb = (TBLN - 1) - ((qz + 7) * 23 + (qy + 7) * 15 + (qx + 7)) +
+                   ((g4 >> 1) * 15 + 4 * (g4 & 1));
     f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
-    float mrun = -INFINITY, lrun = 0.f;
+    f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f};
+    float mrun = -INFINITY;
 #pragma unroll 2
     for (int t = 0; t < 8; ++t) {  // 64-key tiles (one z slice of the window each)
+      const float* bt = tbr + rb + 23 * t;
       f32x4 s[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ks[(t * 64 + kt * 16 + l15) * KS + 8 * g4]);
-        s[kt] = mma32<P>(a, b1, f32x4{0.f, 0.f, 0.f, 0.f});
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ks[(t * 64 + kt * 16 + l15) * KS + kch]);
+        f32x4 bias = f32x4{bt[30 * kt], bt[30 * kt + 1], bt[30 * kt + 2], bt[30 * kt + 3]};
+        if (DIAG) bias = *reinterpret_cast<const f32x4*>(tbr + 32 * kt + (((rb + 23 * t) & 127) & ~3));
+        s[kt] = mma32<P>(a, b1, bias);
         if (SPLIT) s[kt] = mma32<P>(a, b2, s[kt]);
       }
-      float tmax = -INFINITY;
+      float tmax = mrun;  // a chain, so the compiler pairs it into v_max3_f32
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const int i0 = ib - t * 23 - kt * 30;
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          s[kt][i] = s[kt][i] * scale_log2 + tb[i0 - i];
-          tmax = fmaxf(tmax, s[kt][i]);
-        }
-      }
+        for (int i = 0; i < 4; ++i) tmax = fmaxf(tmax, s[kt][i]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(mrun, tmax);
+      const float mnew = tmax;
       const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
       mrun = mnew;
-      float psum = 0.f;
       bf16x4 ph[4], pl[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float p = __builtin_amdgcn_exp2f(s[kt][i] - mnew);
-          psum += p;
           const uint16_t hb = op_cvt<P>(p);
           ph[kt][i] = (short)hb;
           pl[kt][i] = op_lo<P>(p, hb);
         }
       }
-      lrun = lrun * alpha + psum;
       o *= alpha;
+      l4 *= alpha;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const bf16x8 pb = bf16x8{ph[2 * j][0], ph[2 * j][1], ph[2 * j][2], ph[2 * j][3],
                                  ph[2 * j + 1][0], ph[2 * j + 1][1], ph[2 * j + 1][2], ph[2 * j + 1][3]};
-        const int o1 = (((16 * t + 8 * j + g4) * HD) + l15) * 4;
-        const int o2 = (((16 * t + 8 * j + 4 + g4) * HD) + l15) * 4;
+        const int o1 = (16 * t + 8 * j + g4) * VB + l15 * 4;
+        const int o2 = (16 * t + 8 * j + 4 + g4) * VB + l15 * 4;
         const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(&Vq[o1]);
         const bf16x4 v2 = *reinterpret_cast<const bf16x4*>(&Vq[o2]);
         const bf16x8 vh = bf16x8{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
@@ -571,13 +613,13 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
           const bf16x8 vl = bf16x8{w1[0], w1[1], w1[2], w1[3], w2[0], w2[1], w2[2], w2[3]};
           o = mma32<P>(vl, pb, o);
           o = mma32<P>(vh, plb, o);
+          l4 = mma32<P>(ones, plb, l4);
         }
         o = mma32<P>(vh, pb, o);
+        l4 = mma32<P>(ones, pb, l4);
       }
     }
-    lrun += __shfl_xor(lrun, 16, 64);
-    lrun += __shfl_xor(lrun, 32, 64);
-    const float inv = 1.f / lrun;
+    const float inv = 1.f / l4[0];
     const int64_t off = (row0 + q) * C + h * HD + 4 * g4;
     if (store32(P)) {
       *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off) = o * inv;
@@ -616,7 +658,8 @@ int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, 
       const int64_t wh = Bw * heads;
       const int qsplit = wh >= 512 ? 1 : (wh >= 256 ? 2 : 4);
       const dim3 g1((unsigned)(wh * qsplit));
-      auto k = split ? attn_tbl_kernel<PREC_SPLIT>
+      static const bool diag = getenv("WF_ATTN_DIAG") != nullptr;
+      auto k = split ? (diag ? attn_tbl_kernel<PREC_SPLIT, 1> : attn_tbl_kernel<PREC_SPLIT>)
                      : (f16 ? attn_tbl_kernel<PREC_FP16> : attn_tbl_kernel<PREC_BF16>);
       hipLaunchKernelGGL(k, g1, dim3(512), 0, s, qkv, bias, out, heads, qsplit, sl2);
       return check_launch("attention core (table bias, window per workgroup)");
