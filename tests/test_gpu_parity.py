@@ -11,7 +11,8 @@ Tolerances (stated per check):
       - fast precision "bf16": rel-L2 <= 1e-2 for a single op, <= 2e-2 through a Block,
         <= 3e-2 through the encoder (bf16 rounds to 2^-9 = 2e-3 relative per operand);
       - config 5's "fp16" (fp16 operands on the f16 MFMA pipes, fp32 accumulation and fp32
-        LayerNorm / softmax / residual): rel-L2 <= 2e-3 for a single op, <= 3e-3 through a
+        LayerNorm / softmax / residual; window attention and the skip-feature convolutions keep
+        the bf16x3 split, ops.FP16_SPLIT_OPS): rel-L2 <= 2e-3 for a single op, <= 3e-3 through a
         Block, <= 5e-3 through the encoder and the full model (fp16 rounds to 2^-12 = 2.4e-4
         relative per operand, 8x finer than bf16).
   * end-to-end metric (BASELINE.json north_star): Dice of TC / WT / ET of the full model's
@@ -260,7 +261,7 @@ def test_window_attention_q1_layout_on_raster():
 # ------------------------------------------------------------------------------ module level
 # Dice bound of the fp16 path (see test_full_model_128_dice_vs_reference for why reduced-
 # precision operands move Dice at all with these weights)
-FP16_DICE = 5e-3  # measured 2.4e-3 (192^3 HF) and 2.9e-3 (128^3)
+FP16_DICE = 1e-3  # the north star's bound; fp16 policy (ops.FP16_SPLIT_OPS): 192^3 HF 6.7e-4
 
 # rel-L2 bounds per precision (measured: bf16x3 2.5e-6..2.6e-5, bf16 1.5e-3..1e-2)
 TOL = {"bf16x3": {"tensor": 5e-5, "block": 5e-5, "encoder": 1e-4, "full": 1e-4},

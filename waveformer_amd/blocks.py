@@ -102,6 +102,8 @@ class UnetResBlock(nn.Module):
     """conv3-norm-lrelu-conv3-norm (+ 1x1 conv + norm residual when channels change) -> lrelu
     (monai dynunet_block.py:25-111)."""
 
+    _split_conv1 = False  # fp16 policy: conv1 keeps bf16x3 (ops.FP16_SPLIT_OPS "skip_conv")
+
     def __init__(self, spatial_dims: int, in_channels: int, out_channels: int,
                  kernel_size=3, stride=1, norm_name: Union[Tuple, str] = "instance",
                  act_name=("leakyrelu", {"inplace": True, "negative_slope": 0.01}), dropout=None):
@@ -129,8 +131,9 @@ class UnetResBlock(nn.Module):
         if self._fast(inp):
             slope = self.lrelu.negative_slope
             x = ops.to_cl(inp)
-            h, s1 = ops.conv3d_k3(x, self.conv1.conv.weight, self.conv1.conv.bias,
-                                  norm_eps=self.norm1.eps)
+            with ops.op_precision("skip_conv" if self._split_conv1 else "conv"):
+                h, s1 = ops.conv3d_k3(x, self.conv1.conv.weight, self.conv1.conv.bias,
+                                      norm_eps=self.norm1.eps)
             ops.norm_act(h, s1, slope=slope, out=h)
             out, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
                                     norm_eps=self.norm2.eps)
@@ -166,6 +169,8 @@ class UnetResBlock(nn.Module):
 class UnetBasicBlock(nn.Module):
     """conv3-norm-lrelu-conv3-norm-lrelu (monai dynunet_block.py:114-185)."""
 
+    _split_conv1 = False  # fp16 policy, as UnetResBlock
+
     def __init__(self, spatial_dims: int, in_channels: int, out_channels: int, kernel_size=3,
                  stride=1, norm_name: Union[Tuple, str] = "instance", act_name=None, dropout=None):
         super().__init__()
@@ -180,8 +185,9 @@ class UnetBasicBlock(nn.Module):
                 and _k3_ok(self.conv2.conv, self.conv2.conv.in_channels)
                 and _in_ok(self.norm1) and _in_ok(self.norm2)):
             slope = self.lrelu.negative_slope
-            h, s1 = ops.conv3d_k3(inp, self.conv1.conv.weight, self.conv1.conv.bias,
-                                  norm_eps=self.norm1.eps)
+            with ops.op_precision("skip_conv" if self._split_conv1 else "conv"):
+                h, s1 = ops.conv3d_k3(inp, self.conv1.conv.weight, self.conv1.conv.bias,
+                                      norm_eps=self.norm1.eps)
             ops.norm_act(h, s1, slope=slope, out=h)
             out, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
                                     norm_eps=self.norm2.eps)

@@ -483,10 +483,10 @@ __device__ __forceinline__ void load8_split_scaled(const void* base, int64_t off
 }
 
 __device__ __forceinline__ int kswz(int row) {  // 16-B chunk XOR of a K row (see above)
-  return (0x1E0 >> (2 * ((row >> 2) & 3))) & 3;   // {0, 2, 3, 1}[(row >> 2) & 3]
+  return (0x78 >> (2 * ((row >> 2) & 3))) & 3;  // {0, 2, 3, 1}[(row >> 2) & 3]
 }
 
-template <int P, int DIAG = 0>
+template <int P>
 __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict__ qkv,
                                                           const float* __restrict__ table,
                                                           void* __restrict__ out, int heads,
@@ -567,8 +567,7 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ks[(t * 64 + kt * 16 + l15) * KS + kch]);
-        f32x4 bias = f32x4{bt[30 * kt], bt[30 * kt + 1], bt[30 * kt + 2], bt[30 * kt + 3]};
-        if (DIAG) bias = *reinterpret_cast<const f32x4*>(tbr + 32 * kt + (((rb + 23 * t) & 127) & ~3));
+        const f32x4 bias = f32x4{bt[30 * kt], bt[30 * kt + 1], bt[30 * kt + 2], bt[30 * kt + 3]};
         s[kt] = mma32<P>(a, b1, bias);
         if (SPLIT) s[kt] = mma32<P>(a, b2, s[kt]);
       }
@@ -658,8 +657,7 @@ int launch_attn_core(const void* qkv, const float* bias, void* out, float* lse, 
       const int64_t wh = Bw * heads;
       const int qsplit = wh >= 512 ? 1 : (wh >= 256 ? 2 : 4);
       const dim3 g1((unsigned)(wh * qsplit));
-      static const bool diag = getenv("WF_ATTN_DIAG") != nullptr;
-      auto k = split ? (diag ? attn_tbl_kernel<PREC_SPLIT, 1> : attn_tbl_kernel<PREC_SPLIT>)
+      auto k = split ? attn_tbl_kernel<PREC_SPLIT>
                      : (f16 ? attn_tbl_kernel<PREC_FP16> : attn_tbl_kernel<PREC_BF16>);
       hipLaunchKernelGGL(k, g1, dim3(512), 0, s, qkv, bias, out, heads, qsplit, sl2);
       return check_launch("attention core (table bias, window per workgroup)");

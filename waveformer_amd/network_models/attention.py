@@ -76,7 +76,7 @@ class Attention(nn.Module):
         self._check_train()
         lw, lb, eps = ln if ln is not None else (None, None, 0.0)
         train = wfa.needs_grad(x_cl, *self.parameters(), lw, lb)
-        prec = wfa.SPLIT if train else ops.prec_id()
+        prec = wfa.SPLIT if train else ops.op_prec("attn")
         out, _, _ = _OPS.window_attn(x_cl, lw, lb, float(eps), self.qkv.weight, self.qkv.bias,
                                      self.relative_position_bias_table,
                                      self.relative_position_index, self.proj.weight,

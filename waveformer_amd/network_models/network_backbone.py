@@ -122,6 +122,10 @@ class Waveformer(nn.Module):
         self.encoder2 = blk(in_channels=fs[0], out_channels=fs[0])
         self.encoder3 = blk(in_channels=fs[1], out_channels=fs[1])
         self.encoder4 = blk(in_channels=fs[2], out_channels=fs[2])
+        # config 5's fp16 policy (ops.FP16_SPLIT_OPS): the first convolution of each block
+        # reading the transformer's skip features keeps the fp32-faithful split
+        for e in (self.encoder2, self.encoder3, self.encoder4):
+            e.layer._split_conv1 = True
         self.encoder10 = ChannelCalibration(in_channels=fs[3], reduction_ratio=4,
                                             norm_layer=nn.InstanceNorm3d)
         idwt = partial(UnetrIDWTBlock, spatial_dims=spatial_dims, in_channels=fs[3],
