@@ -9,6 +9,83 @@
 namespace wf {
 
 // ---------------------------------------------------------------------------------------
+// PatchEmbed, one output position per lane, weights as wave-uniform (scalar-cache) operands:
+// the Conv3d(k = 2, s = 2) of the encoder stem (Cin 4 or 1 -> Cout 48; patchembedding.py:
+// 188-214) is a (32 or 8) x 48 product per position.  A lane loads its 2x2x2 x Cin inputs
+// straight from the NCDHW volume (float2 per (ci, dz, dy) row pair: the wave's 64 consecutive
+// x positions read 512 contiguous bytes per load), keeps them in VGPRs, and runs the 48 output
+// channels as 48 independent FMA chains whose weights w[c][k] are uniform across the wave --
+// the compiler fetches them with s_load into SGPR operands -- in exact fp32 (the reference's
+// arithmetic; no MFMA rounding).  HBM-streaming: the input once, the channel-last output once.
+// (The row-staged kernels below ran their FMAs on packed pairs; with packed-FP32 instructions
+// off (Makefile) their VALU work doubled: 182 -> 377 us per B = 8 launch.)
+// ---------------------------------------------------------------------------------------
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void patch_embed_lane_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ out, int D, int H, int W, int64_t total) {
+  constexpr int K = CIN * 8;
+  constexpr int RS = COUT + 4;  // LDS row stride (floats): 8-lane store groups conflict-free
+  __shared__ __attribute__((aligned(16))) float tile[4][64 * RS];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t p0 = (int64_t)blockIdx.x * 256 + wv * 64;     // first position of this wave
+  const int64_t p = min(p0 + lane, total - 1);                // (b, z, y, x) raster position
+  const int xo = (int)(p % W);
+  int64_t t = p / W;
+  const int yo = (int)(t % H);
+  t /= H;
+  const int zo = (int)(t % D);
+  const int64_t b = t / D;
+  const int W2 = 2 * W, H2 = 2 * H, D2 = 2 * D;
+  float v[K];
+#pragma unroll
+  for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const float2 u = *reinterpret_cast<const float2*>(
+            x + (((b * CIN + ci) * D2 + 2 * zo + dz) * H2 + 2 * yo + dy) * W2 + 2 * xo);
+        v[ci * 8 + dz * 4 + dy * 2] = u.x;
+        v[ci * 8 + dz * 4 + dy * 2 + 1] = u.y;
+      }
+  float* row = &tile[wv][lane * RS];
+  // 4 channels per iteration, K split in halves of at most 16 weights per channel: 64 weight
+  // SGPRs in flight (the whole 48 x 32 set would spill the scalar file)
+  constexpr int KH = K > 16 ? 16 : K;
+#pragma unroll 1
+  for (int c4 = 0; c4 < COUT / 4; ++c4) {
+    float a[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a[e] = bias ? bias[4 * c4 + e] : 0.f;
+#pragma unroll 1
+    for (int k0 = 0; k0 < K; k0 += KH) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float* wc = w + (4 * c4 + e) * K + k0;
+#pragma unroll
+        for (int k = 0; k < KH; ++k) a[e] = fmaf(v[k0 + k], wc[k], a[e]);
+      }
+    }
+    *reinterpret_cast<f32x4*>(row + 4 * c4) = f32x4{a[0], a[1], a[2], a[3]};
+  }
+  // the wave's 64 positions x COUT channels are one contiguous run of the channel-last output:
+  // write it back with every store instruction covering 1 KB (the per-lane rows would leave
+  // each instruction 64 scattered 16-B pieces)
+  const int nval = (int)min<int64_t>(64, total - p0) * COUT / 4;  // f32x4 of this wave
+  float* o = out + p0 * COUT;
+#pragma unroll
+  for (int j = 0; j < COUT / 4; ++j) {
+    const int e = j * 64 + lane;  // f32x4 index in the run
+    if (e < nval) {
+      const int pos = e / (COUT / 4), c = (e - pos * (COUT / 4)) * 4;
+      *reinterpret_cast<f32x4*>(o + 4 * (int64_t)e) =
+          *reinterpret_cast<const f32x4*>(&tile[wv][pos * RS + c]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // PatchEmbed, streaming variant (Cin = 4, Cout % 4 == 0, W % 2 == 0: the encoder's 4 -> 48
 // stem): a persistent workgroup walks groups of R output rows; the next group's 2x2 input
 // rows are loaded into registers (8 float4 per thread at R = 4) while the current group is
@@ -519,6 +596,18 @@ extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* b
   const size_t row_lds = (size_t)Cin * 8 * W * sizeof(float);
   WF_REQUIRE(row_lds <= 64 * 1024, "PatchEmbed row tile exceeds 64 KB of LDS");
   static const bool one_shot = getenv("WF_PE_ONESHOT") != nullptr;  // A/B: the kernel below
+  static const bool rowstream = getenv("WF_PE_ROWSTREAM") != nullptr;  // A/B: the row stream
+  if (!one_shot && !rowstream && Cout == 48 && (Cin == 4 || Cin == 1)) {
+    const int64_t total = B * D * H * W;
+    const unsigned blocks = (unsigned)cdiv(total, 256);
+    if (Cin == 4)
+      hipLaunchKernelGGL((patch_embed_lane_kernel<4, 48>), dim3(blocks), dim3(256), 0,
+                         (hipStream_t)stream, x, w, bias, out, (int)D, (int)H, (int)W, total);
+    else
+      hipLaunchKernelGGL((patch_embed_lane_kernel<1, 48>), dim3(blocks), dim3(256), 0,
+                         (hipStream_t)stream, x, w, bias, out, (int)D, (int)H, (int)W, total);
+    return check_launch("wf_patch_embed_fwd");
+  }
   if (!one_shot && Cin == 4 && Cout % 4 == 0 && Cout <= 256 && H % 4 == 0 &&
       4 * (int64_t)Cin * 8 * W / 4 <= 8 * 256) {
     constexpr int R = 4;
