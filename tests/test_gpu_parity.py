@@ -197,13 +197,15 @@ def test_ccf_ffn_stage1_fused_vs_oracle(shape, block):
         assert C.rel_l2(out, ref) <= tol, prec
 
 
-@pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (3, 7, 4, 9)])
+@pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (3, 7, 4, 9), (1, 20, 8, 8),
+                                   (1, 16, 16, 16)])
 @pytest.mark.parametrize("block", [False, True])
 def test_ccf_ffn_stage2_vs_oracle(shape, block):
     """C = 96, hidden = 384 (encoder stage 2): the pwconv + LN1 + GELU GEMM with the columns
-    split over the waves (gemm_lnw.hip; rows not a multiple of its 64-row tile included), the
-    z-marching depthwise conv with LN2 moments, the fc with LN2 + GELU in its loader and the
-    Q4 residual -- same bars as stage 1."""
+    split over the waves (gemm_lnw.hip; rows not a multiple of its 64-row tile included), then
+    the fused back half (ffn_dwfc.hip's ffn_dwfc2_kernel: depthwise conv, LN2 + GELU, fc and
+    the Q4 residual with h2 on chip; ragged 4 x 4 tiles, z segments shorter than the volume
+    at (1, 20, 8, 8)) -- same bars as stage 1."""
     import waveformer_amd.network_models as NM
     from oracle.weight_rule import rule_state_dict
     from waveformer_amd import ops
@@ -230,6 +232,16 @@ def test_ccf_ffn_stage2_vs_oracle(shape, block):
             stats = ops.msfuse([], xc, 1e-6)[1] if block else None
             out = ops.ccf_ffn(xc, stats, norm2 if block else None, mlp, cuda(bs))
         assert C.rel_l2(out, ref) <= tol, prec
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11)])
+@pytest.mark.parametrize("block", [False, True])
+def test_ccf_ffn_stage2_staged_path_vs_oracle(shape, block, monkeypatch):
+    """The unfused stage-2 back half (WF_FFN_NO_DWFC=1: z-marching depthwise conv with LN2
+    moments, then the fc with LN2 + GELU in its loader) -- the path training keeps, since its
+    backward needs h2."""
+    monkeypatch.setenv("WF_FFN_NO_DWFC", "1")
+    test_ccf_ffn_stage2_vs_oracle(shape, block)
 
 
 @pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (1, 16, 16, 16), (1, 3, 12, 9)])

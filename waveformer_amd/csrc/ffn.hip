@@ -552,12 +552,13 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
     }
   }
   if (rc) return rc;
-  // dwconv + LN2 + GELU (+ fc + residual): the stage-1 shape runs the fused back half
-  // (ffn_dwfc.hip, h2 stays on chip); other shapes either fuse dwconv + LN over the full 4C row
+  // dwconv + LN2 + GELU (+ fc + residual): the stage-1 and stage-2 shapes run the fused back
+  // half (ffn_dwfc.hip, h2 stays on chip); other shapes either fuse dwconv + LN over the full 4C row
   // in LDS, or run the z-marching depthwise conv with LN2 + GELU moved into the fc loader
   static const bool fused_dw = getenv("WF_FFN_FUSED_DW") != nullptr;
-  static const bool no_dwfc = getenv("WF_FFN_NO_DWFC") != nullptr;
-  if (!keep && !no_dwfc && C == 48 && hidden == 192) {
+  const bool no_dwfc = getenv("WF_FFN_NO_DWFC") != nullptr;  // per call: tests switch it
+  const bool dwfc1 = C == 48 && hidden == 192, dwfc2 = C == 96 && hidden == 384;
+  if (!keep && !no_dwfc && (dwfc1 || dwfc2)) {
     if (stage == 1 || stage == 3) return rc;  // stage 3 (fc) is part of the fused kernel
     DwFcArgs d{};
     d.h1 = h1;
@@ -578,7 +579,7 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
     d.D = (int)D;
     d.H = (int)H;
     d.W = (int)W;
-    return launch_ffn_dwfc(d, precision, s);
+    return dwfc1 ? launch_ffn_dwfc(d, precision, s) : launch_ffn_dwfc2(d, precision, s);
   }
   const bool split_ln = (keep || !fused_dw) && hidden % 32 == 0;
   WF_REQUIRE(!keep || split_ln, "training needs hidden % 32 == 0 (h2 kept pre-LayerNorm)");

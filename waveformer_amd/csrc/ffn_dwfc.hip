@@ -672,6 +672,399 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Stage-2 shape (C = 96, hidden = 384): the same back half, re-tiled for a 4C row twice as
+// wide.  Double-buffered planes and h2 tiles no longer fit next to the fc weights, so this one
+// keeps ONE plane buffer (the next plane waits in registers) and 4 x 4 tiles:
+//   LDS = haloed 6 x 6 x 384 plane (55 KB) + 16 x 384 h2 tile (25 KB) + the fc weight's hi
+//         half (96 x 384 bf16, 75 KB) + LN2 / bias vectors = 159.6 KB, one workgroup per CU.
+//   depthwise (all 12 waves): thread = (channel c, column pair xp) -- 384 x 2 = 768 threads;
+//         one channel's 27 taps in VGPRs, four scalar LDS reads per input row (64 consecutive
+//         channels per wave: conflict-free), rolling accumulators over the 3 output planes.
+// Two roles with separate loops (same barrier sequence), so neither holds the other's
+// registers and neither's loads sit in front of the other's in the in-order load counter:
+//   F (waves 0..5): the fc, one 16-channel output tile each over the 16-position tile; A =
+//         weight hi from LDS and (split) weight lo held in VGPRs for the whole march; + bias +
+//         Q4 residual; the residual rows are prefetched one plane ahead;
+//   G (waves 6..11): the h1 plane staging (fetched two planes ahead, committed one ahead);
+//         waves 8..11 (one per SIMD) run LN2 + GELU + split, 16 lanes x 24 channels per
+//         position (lane g owns the 16-byte chunks 4g + 64 j), in place as bf16 {hi, lo}.
+// Per iteration p (3 barriers), with zo = p - 1 the output plane scatter(p) completed:
+//   C | G commit(p+1); all write the fp32 h2 tile (zo); F issue the next plane's residual
+//   loads | A | G fetch(p+2); waves 8..11 LN2(zo), the rest scatter(p+1) rows 0..s-1 | B |
+//   F fc(zo) + store; everyone finishes scatter(p+1).
+// (A variant that split LN2 into statistics on 4 waves + normalise / GELU / split by every
+// thread from its own registers, behind a fourth barrier, measured 380 vs 361 us.)
+// ---------------------------------------------------------------------------------------
+#ifdef WF_DWFC2_PROBE
+// diagnostic builds only: per-wave cycles of workgroup 0 by phase (C->A work, A wait, A->B
+// work, B wait, B->C work, C wait), read back by wf_debug_dwfc2_probe
+__device__ long long g_dwfc2_probe[12 * 8];
+extern "C" int wf_debug_dwfc2_probe(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dwfc2_probe), sizeof(g_dwfc2_probe));
+}
+#define PROBE_DECL                                                              \
+  const bool probe_on = blockIdx.x == 0;                                         \
+  long long pr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pr_last = __builtin_amdgcn_s_memtime();
+#define PROBE(i)                                                                \
+  if (probe_on) {                                                               \
+    const long long t_ = __builtin_amdgcn_s_memtime();                          \
+    pr_acc[i] += t_ - pr_last;                                                  \
+    pr_last = t_;                                                               \
+  }
+#define PROBE_DUMP                                                              \
+  if (probe_on && (tid & 63) == 0)                                              \
+    for (int i_ = 0; i_ < 8; ++i_) g_dwfc2_probe[wid * 8 + i_] = pr_acc[i_];
+#else
+#define PROBE_DECL
+#define PROBE(i)
+#define PROBE_DUMP
+#endif
+
+struct DwFc2 {
+  static constexpr int C = 96, HID = 384, TY = 4, TX = 4;
+  static constexpr int NTH = 768, PY = TY + 2, PX = TX + 2, PP = PY * PX, NPOS = TY * TX;
+  static constexpr int HS = HID + 4, WKP = HID + 8;
+  static constexpr int PLANE_F = PP * HID, H2_F = NPOS * HS;
+  static constexpr int NG = 384;                                   // G threads (staging)
+  static constexpr int NV = HID / 4, NLD = (PP * NV + NG - 1) / NG;
+  static constexpr int CT = C / 16, KS = HID / 32;
+  static constexpr int LNL = 16, LNC = HID / LNL, LN_W0 = 8;      // LN2 rows: waves 8..11
+  static constexpr size_t LDS_BYTES =
+      (size_t)(PLANE_F + H2_F) * 4 + (size_t)C * WKP * 2 + (size_t)(2 * HID + 3 * C) * 4;
+  static_assert(NPOS * LNL == NTH - 64 * LN_W0, "LN2 waves cover the tile");
+  static_assert(CT * 64 == NTH - NG, "one F wave per fc column tile");
+  static_assert(LDS_BYTES <= 160 * 1024, "one workgroup per CU");
+  static_assert(HID * 27 <= PLANE_F, "depthwise weights staged in the plane buffer");
+};
+
+template <int P, typename T>
+__global__ __launch_bounds__(768, 1) void ffn_dwfc2_kernel(DwFcArgs a) {
+  typedef DwFc2 K;
+  constexpr int C = K::C, HID = K::HID, TY = K::TY, TX = K::TX;
+  constexpr bool SPLIT = P == PREC_SPLIT;
+  typedef H1Load<T> L;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* plane = lds;                                            // [PP][HID]
+  float* h2t = lds + K::PLANE_F;                                 // [NPOS][HS]
+  uint16_t* wf = reinterpret_cast<uint16_t*>(h2t + K::H2_F);     // [C][WKP] fc weight hi
+  float* lnw = reinterpret_cast<float*>(wf + C * K::WKP);        // [HID] halved
+  float* lnb = lnw + HID;
+  float* fcb = lnb + HID;                                        // [C]
+  float* n2w = fcb + C;
+  float* n2b = n2w + C;
+
+  const int tid = threadIdx.x;
+  // wave-uniform (scalar) wave index: role branches are real branches
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int D = a.D, H = a.H, W = a.W;
+  const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY, nzs = (D + a.ZS - 1) / a.ZS;
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int xt = t % ntx;
+  t /= ntx;
+  const int yt = t % nty;
+  t /= nty;
+  const int zt = t % nzs;
+  const int b = t / nzs;
+  const int x0 = xt * TX, y0 = yt * TY, z0 = zt * a.ZS, z1 = min(z0 + a.ZS, D);
+  const int64_t plane_sz = (int64_t)H * W;
+
+  for (int i = tid; i < C * (HID / 8); i += K::NTH) {
+    const int n = i / (HID / 8), k8 = i % (HID / 8);
+    *reinterpret_cast<bf16x8*>(wf + n * K::WKP + 8 * k8) =
+        *reinterpret_cast<const bf16x8*>(a.fc + (size_t)n * HID + 8 * k8);
+  }
+  for (int i = tid; i < HID; i += K::NTH) {  // halved: GELU is evaluated from x / 2
+    lnw[i] = 0.5f * a.ln2_w[i];
+    lnb[i] = 0.5f * a.ln2_b[i];
+  }
+  for (int i = tid; i < C; i += K::NTH) {
+    fcb[i] = a.fc_b ? a.fc_b[i] : 0.f;
+    n2w[i] = a.stats ? a.n2_w[i] : 1.f;
+    n2b[i] = a.stats ? a.n2_b[i] : 0.f;
+  }
+  for (int i = tid; i < HID * 27; i += K::NTH) plane[i] = a.dw_w[i];
+  __syncthreads();  // S0
+
+  // ---- depthwise role (everyone): channel c, output columns 2 xp and 2 xp + 1
+  const int c = tid % HID, xp = tid / HID;
+  float w[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) w[k] = plane[c * 27 + k];
+  const float bias = a.dw_b[c];
+  float aA[2][TY], aB[2][TY], aC[2][TY];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int o = 0; o < TY; ++o) aA[q][o] = aB[q][o] = aC[q][o] = 0.f;
+  const bool dscat = !(a.dbg & 1);  // timing experiments only (WF_FFN_DBG)
+  // input rows [r_lo, r_hi) of the current plane into output planes +1 (aC), 0 (aB), -1 (aA)
+  auto rows = [&](int r_lo, int r_hi) {
+    if (!dscat) return;
+    const float* Pin = plane + 2 * xp * HID + c;
+#pragma unroll
+    for (int r = 0; r < K::PY; ++r) {
+      if (r < r_lo || r >= r_hi) continue;
+      const float u0 = Pin[(r * K::PX + 0) * HID];
+      const float u1 = Pin[(r * K::PX + 1) * HID];
+      const float u2 = Pin[(r * K::PX + 2) * HID];
+      const float u3 = Pin[(r * K::PX + 3) * HID];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int o = r - ky;
+        if (o < 0 || o >= TY) continue;
+        const float* w0 = w + ky * 3;
+        aC[0][o] = fmaf(w0[2], u2, fmaf(w0[1], u1, fmaf(w0[0], u0, aC[0][o])));
+        aC[1][o] = fmaf(w0[2], u3, fmaf(w0[1], u2, fmaf(w0[0], u1, aC[1][o])));
+        aB[0][o] = fmaf(w0[11], u2, fmaf(w0[10], u1, fmaf(w0[9], u0, aB[0][o])));
+        aB[1][o] = fmaf(w0[11], u3, fmaf(w0[10], u2, fmaf(w0[9], u1, aB[1][o])));
+        aA[0][o] = fmaf(w0[20], u2, fmaf(w0[19], u1, fmaf(w0[18], u0, aA[0][o])));
+        aA[1][o] = fmaf(w0[20], u3, fmaf(w0[19], u2, fmaf(w0[18], u1, aA[1][o])));
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one input row in flight at a time (VGPRs)
+    }
+  };
+  // the completed output plane (aA + bias) into the fp32 h2 tile, then the accumulators roll
+  auto h2_out = [&](bool valid) {
+    if (valid) {
+#pragma unroll
+      for (int o = 0; o < TY; ++o)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          float h = aA[q][o] + bias;
+          if (sizeof(T) == 2) h = bf2f(f2bf(h));
+          h2t[(o * TX + 2 * xp + q) * K::HS + c] = h;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int o = 0; o < TY; ++o) {
+        aA[q][o] = aB[q][o];
+        aB[q][o] = aC[q][o];
+        aC[q][o] = 0.f;
+      }
+  };
+  // LN2 + GELU + split of one tile position per 16 lanes (24 channels each, lane g owns the
+  // 16-byte chunks 4g + 64 j), rewritten in place as bf16 {hi[HID], lo[HID]}: the lanes of a
+  // row are one 16-lane group of a wave, so all its reads precede its writes
+  auto ln2_row = [&]() {
+    const int ltid = tid - 64 * K::LN_W0;
+    const int pos = ltid / K::LNL, g = ltid % K::LNL;
+    float* row = h2t + pos * K::HS;
+    f32x4 v[K::LNC / 4];
+#pragma unroll
+    for (int j = 0; j < K::LNC / 4; ++j) v[j] = *reinterpret_cast<const f32x4*>(row + 4 * g + 64 * j);
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < K::LNC / 4; ++j) sm += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    const float mean = group_sum<K::LNL>(sm) * (1.f / HID);
+    float qs = 0.f;
+#pragma unroll
+    for (int j = 0; j < K::LNC / 4; ++j) {
+      const f32x4 d = v[j] - mean;
+      qs += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+    }
+    const float rstd = rsqrtf(group_sum<K::LNL>(qs) * (1.f / HID) + a.eps2);
+    const float nmr = -mean * rstd;
+    uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
+#pragma unroll
+    for (int j = 0; j < K::LNC / 4; ++j) {
+      const int cc = 4 * g + 64 * j;
+      const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + cc);
+      const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + cc);
+      const f32x4 y = gelu_half4((v[j] * rstd + nmr) * lw4 + lb4);
+      bf16x4 hi4, lo4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint16_t hb = op_cvt<P>(y[e]);
+        hi4[e] = (short)hb;
+        lo4[e] = op_lo<P>(y[e], hb);
+      }
+      *reinterpret_cast<bf16x4*>(rowh + cc) = hi4;
+      if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + cc) = lo4;
+    }
+  };
+  const int sF = a.ws_split & 7, sG = (a.ws_split >> 3) & 7;  // scatter rows before B
+  PROBE_DECL
+
+  if (wid < K::CT) {
+    // ================================ F waves: fc + epilogue ==============================
+    const int lln = tid & 63, l15 = lln & 15, g4 = lln >> 4;
+    const int ct = wid;
+    const int col = ct * 16 + 4 * g4;
+    const int yo = y0 + l15 / TX, xo = x0 + l15 % TX;
+    const bool rv = yo < H && xo < W;
+    const int64_t gpos0 =
+        (int64_t)b * D * plane_sz + (int64_t)min(yo, H - 1) * W + min(xo, W - 1);
+    const float* sbase = a.stats ? a.stats : a.x;
+    const float bs = a.bscale ? a.bscale[b] : 1.f;
+    const uint16_t* wr = a.fc + (size_t)(C + ct * 16 + l15) * HID + 8 * g4;
+    // residual rows of output plane z (unconditional, clamped to the volume: the values of a
+    // plane outside the segment are never used)
+    f32x4 xr, xrn;
+    f32x2 es, esn;
+    auto epi_load = [&](int z, f32x4& xv, f32x2& ev) {
+      const int64_t gpos = gpos0 + (int64_t)min(max(z, 0), D - 1) * plane_sz;
+      xv = *reinterpret_cast<const f32x4*>(a.x + gpos * C + col);
+      ev = *reinterpret_cast<const f32x2*>(sbase + 2 * gpos);
+    };
+    // the fc weight's lo half of this wave's 16 output channels stays in VGPRs for the whole
+    // z march (48 VGPRs; per plane it would be 1.3x the h1 plane's bytes through the load path)
+    bf16x8 fwl[K::KS];
+#pragma unroll
+    for (int ks = 0; ks < K::KS; ++ks)
+      fwl[ks] = SPLIT ? *reinterpret_cast<const bf16x8*>(wr + ks * 32) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    epi_load(z0, xrn, esn);
+    __syncthreads();  // S1
+    __syncthreads();  // S2: plane z0-1 visible
+    rows(0, K::PY);
+    for (int p = z0 - 1; p <= z1; ++p) {
+      const int zo = p - 1;
+      const bool valid = zo >= z0, more = p + 1 <= z1;
+      __syncthreads();  // C: scatter(p) done everywhere, fc(zo-1) done
+      PROBE(5)
+      h2_out(valid);
+      // issued unconditionally (a load pending across a branch join makes the compiler wait
+      // for it right there)
+      xr = xrn;
+      es = esn;
+      epi_load(zo + 1, xrn, esn);
+      PROBE(0)
+      __syncthreads();  // A: fp32 h2 tile (zo) and plane p+1 visible
+      PROBE(1)
+      if (more) rows(0, sF);
+      PROBE(2)
+      __syncthreads();  // B: bf16 {hi, lo} tile visible
+      PROBE(3)
+      if (valid && !(a.dbg & 4)) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)l15 * (2 * K::HS);
+        const uint16_t* Wh = wf + (size_t)(ct * 16 + l15) * K::WKP;
+#pragma unroll
+        for (int ks = 0; ks < K::KS; ++ks) {
+          const int k = ks * 32 + 8 * g4;
+          const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bh + k);
+          const bf16x8 wh = *reinterpret_cast<const bf16x8*>(Wh + k);
+          if (SPLIT) {
+            const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
+            acc = mma32<P>(wh, bl, acc);
+            acc = mma32<P>(fwl[ks], bh, acc);
+          }
+          acc = mma32<P>(wh, bh, acc);
+        }
+        f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+        if (a.stats) {
+          const f32x4 nw = *reinterpret_cast<const f32x4*>(n2w + col);
+          const f32x4 nbv = *reinterpret_cast<const f32x4*>(n2b + col);
+          const f32x4 n2 = (xr - es.x) * es.y * nw + nbv;
+          v = xr + (n2 + v) * bs;
+        } else {
+          v = xr + v * bs;
+        }
+        if (rv) *reinterpret_cast<f32x4*>(a.out + (gpos0 + (int64_t)zo * plane_sz) * C + col) = v;
+      }
+      if (more) rows(sF, K::PY);
+      PROBE(4)
+    }
+    PROBE_DUMP
+    return;
+  }
+
+  // ================================== G waves ============================================
+  const int gt = tid - 64 * K::CT;
+  const T* src = reinterpret_cast<const T*>(a.h1) + (int64_t)b * D * plane_sz * HID;
+  const int64_t plane_elems = plane_sz * HID;
+  int off[K::NLD];
+  unsigned okmask = 0;
+#pragma unroll
+  for (int j = 0; j < K::NLD; ++j) {
+    const int i = min(j * K::NG + gt, K::PP * K::NV - 1);
+    const int pos = i / K::NV, v = i - pos * K::NV;
+    const int yy = y0 - 1 + pos / K::PX, xx = x0 - 1 + pos % K::PX;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    const int yc = min(max(yy, 0), H - 1), xc = min(max(xx, 0), W - 1);
+    off[j] = (yc * W + xc) * HID + 4 * v;
+    okmask |= (ok ? 1u : 0u) << j;
+  }
+  typename L::raw stg[K::NLD];
+  auto fetch = [&](int p) {
+    const T* base = src + (int64_t)min(max(p, 0), D - 1) * plane_elems;
+#pragma unroll
+    for (int j = 0; j < K::NLD; ++j) stg[j] = L::load(base, off[j]);
+  };
+  auto commit = [&](int p) {
+    const bool pz = p >= 0 && p < D;
+#pragma unroll
+    for (int j = 0; j < K::NLD; ++j) {
+      const int i = j * K::NG + gt;
+      const bool ok = pz && ((okmask >> j) & 1u);
+      const f32x4 u = L::up(stg[j]);
+      if (i < K::PP * K::NV)
+        *reinterpret_cast<f32x4*>(plane + (size_t)i * 4) = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  const bool stat_role = wid >= K::LN_W0;  // LN2 rows
+  fetch(z0 - 1);
+  __syncthreads();  // S1: depthwise weights read out of the plane buffer
+  commit(z0 - 1);
+  fetch(z0);
+  __syncthreads();  // S2
+  rows(0, K::PY);
+  for (int p = z0 - 1; p <= z1; ++p) {
+    const int zo = p - 1;
+    const bool valid = zo >= z0, more = p + 1 <= z1;
+    __syncthreads();  // C
+    PROBE(5)
+#pragma unroll
+    for (int j = 0; j < K::NLD; ++j) asm volatile("" ::"v"(stg[j]));
+    if (more && !(a.dbg & 8)) commit(p + 1);
+    h2_out(valid);
+    PROBE(0)
+    __syncthreads();  // A
+    PROBE(1)
+    // the plane after next: issued here so its address work and load issue overlap the LN2 /
+    // scatter VALU work rather than the commit (latency: one full iteration)
+    if (p + 2 <= z1 && !(a.dbg & 8)) fetch(p + 2);
+    if (stat_role) {
+      if (valid && !(a.dbg & 2)) ln2_row();
+    } else if (more) {
+      rows(0, sG);
+    }
+    PROBE(2)
+    __syncthreads();  // B
+    PROBE(3)
+    if (more) rows(stat_role ? 0 : sG, K::PY);
+    PROBE(4)
+  }
+  PROBE_DUMP
+}
+
+int launch_ffn_dwfc2(const DwFcArgs& a, int prec, hipStream_t s) {
+  typedef DwFc2 K;
+  DwFcArgs g = a;
+  // z segment: whole columns where that still gives two workgroups per CU (B = 8 at 32^3:
+  // 512 tiles of 4 x 4 x 32), shorter segments for small batches
+  const int64_t base = (int64_t)g.B * cdiv(g.H, K::TY) * cdiv(g.W, K::TX);
+  int ZS = g.D;
+  while (ZS > 8 && base * cdiv(g.D, ZS) < 512) ZS = (ZS + 1) / 2;
+  g.ZS = ZS;
+  g.dbg = getenv("WF_FFN_DBG") ? atoi(getenv("WF_FFN_DBG")) : 0;  // timing experiments only
+  // depthwise input rows scattered before barrier B: F waves (bits 0..2), waves 6, 7 (3..5);
+  // B = 8 stage 2: (F, 6/7) = (3, 3) 352 us, (6, 3) 337, (2, 2) 361, (4, 4) 337, (6, 6) 345
+  static const int split = getenv("WF_FFN2_SPLIT") ? atoi(getenv("WF_FFN2_SPLIT")) : 4 + 8 * 4;
+  g.ws_split = split;
+  const int64_t blocks = base * cdiv(g.D, ZS);
+  void (*kern)(DwFcArgs) = prec == PREC_SPLIT  ? ffn_dwfc2_kernel<PREC_SPLIT, float>
+                           : prec == PREC_FP16 ? ffn_dwfc2_kernel<PREC_FP16, float>
+                                               : ffn_dwfc2_kernel<PREC_BF16, uint16_t>;
+  set_max_lds(reinterpret_cast<const void*>(kern), (int)K::LDS_BYTES);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(K::NTH), K::LDS_BYTES, s, g);
+  return check_launch("ffn_dwfc2");
+}
+
 template <int TY, int TX>
 static int go_dwfc(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks) {
   constexpr int C = 48, HID = 192;

@@ -149,6 +149,8 @@ struct DwFcArgs {
   int ws_split;          // wave-specialised ffn_dwfc: D rows of a plane in phase 1 (1..5)
 };
 int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s);
+// the same for C = 96, hidden = 384 (4 x 4 tiles, one plane buffer, fc weight hi in LDS)
+int launch_ffn_dwfc2(const DwFcArgs& a, int prec, hipStream_t s);
 // ---- the whole CCF_FFN + norm2 + Q4 residual in one kernel for C = 48, hidden = 192: the
 // haloed h1 plane is computed in LDS from the x rows (pw MFMA + LN1 + GELU), never stored
 int launch_ffn_fused(const DwFcArgs& a, int prec, hipStream_t s);
