@@ -358,6 +358,32 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
   }
 }
 
+#ifdef WF_DWFC2_PROBE
+// diagnostic builds only (ffn_dwfc_ws_kernel and ffn_dwfc2_kernel): per-wave cycles of
+// workgroup 0 by phase between the kernel's barriers (work, then wait), read back by
+// wf_debug_dwfc2_probe
+__device__ long long g_dwfc2_probe[12 * 8];
+extern "C" int wf_debug_dwfc2_probe(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dwfc2_probe), sizeof(g_dwfc2_probe));
+}
+#define PROBE_DECL                                                              \
+  const bool probe_on = blockIdx.x == 0;                                         \
+  long long pr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pr_last = __builtin_amdgcn_s_memtime();
+#define PROBE(i)                                                                \
+  if (probe_on) {                                                               \
+    const long long t_ = __builtin_amdgcn_s_memtime();                          \
+    pr_acc[i] += t_ - pr_last;                                                  \
+    pr_last = t_;                                                               \
+  }
+#define PROBE_DUMP                                                              \
+  if (probe_on && (tid & 63) == 0)                                              \
+    for (int i_ = 0; i_ < 8; ++i_) g_dwfc2_probe[wid * 8 + i_] = pr_acc[i_];
+#else
+#define PROBE_DECL
+#define PROBE(i)
+#define PROBE_DUMP
+#endif
+
 // ---------------------------------------------------------------------------------------
 // Wave-specialised variant (same math, same tile): 6 "D" waves run the depthwise scatter while
 // 6 "E" waves run everything else one output plane behind -- LN2 + GELU + split of plane z-2,
@@ -387,6 +413,10 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
   // ~2.8k cycles of work against ~5.3k for the E waves, measured with s_memtime probes),
   // positions 16..31 by the E waves 0..3
   constexpr int LNL = 16, LNC = HID / LNL;
+  // D's input rows split over the two phases: rows 0..1 (3 of the 12 row-tap FMA groups)
+  // alongside E's LN2 + GELU, rows 2..5 alongside E's commit + fetch + fc (B = 8 stage 1,
+  // split 0..5 measured 916, 894, 879-888, 903, 934, 952 us in round 2)
+  constexpr int WS_SPLIT = 2;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* planes = lds;                                  // [2][PP][HID]
   float* h2b = lds + 2 * K::PLANE_F;                     // [2][NPOS][HS]
@@ -476,6 +506,7 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
     }
   };
 
+  PROBE_DECL
   if (isD) {
     // ================================ D waves: depthwise scatter ==========================
     const int cp = tid % NPAIR, xg = tid / NPAIR;  // columns xg and xg + 4
@@ -491,27 +522,42 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
       for (int o = 0; o < TY; ++o) aA[c][o] = aB[c][o] = aC[c][o] = f32x2{0.f, 0.f};
     __syncthreads();  // (prologue) weights read out of the plane buffer
     __syncthreads();  // (prologue) planes z0-1 committed
+    // input rows [r_lo, r_hi) (compile-time after inlining) of plane cur; each row's six LDS
+    // reads are issued one row ahead of its FMAs, and unconditionally (a load pending across a
+    // branch join is waited for at the join)
     auto rows = [&](const float* cur, int r_lo, int r_hi) {
+      f32x2 nx[2][3];
+      auto ld = [&](int r) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+            nx[c][k] = *reinterpret_cast<const f32x2*>(cur + (xg + 4 * c) * HID + 2 * cp +
+                                                       (r * K::PX + k) * HID);
+      };
+      ld(r_lo);
 #pragma unroll
       for (int r = 0; r < K::PY; ++r) {
         if (r < r_lo || r >= r_hi) continue;
+        f32x2 v[2][3];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) v[c][k] = nx[c][k];
+        if (r + 1 < r_hi) ld(r + 1);
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          const float* Pin = cur + (xg + 4 * c) * HID + 2 * cp;
-          const f32x2 v0 = *reinterpret_cast<const f32x2*>(Pin + (r * K::PX + 0) * HID);
-          const f32x2 v1 = *reinterpret_cast<const f32x2*>(Pin + (r * K::PX + 1) * HID);
-          const f32x2 v2 = *reinterpret_cast<const f32x2*>(Pin + (r * K::PX + 2) * HID);
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky) {
             const int o = r - ky;
             if (o < 0 || o >= TY) continue;
             const f32x2* w0 = w2 + ky * 3;
-            aC[c][o] = w0[2] * v2 + (w0[1] * v1 + (w0[0] * v0 + aC[c][o]));
-            aB[c][o] = w0[11] * v2 + (w0[10] * v1 + (w0[9] * v0 + aB[c][o]));
-            aA[c][o] = w0[20] * v2 + (w0[19] * v1 + (w0[18] * v0 + aA[c][o]));
+            aC[c][o] = w0[2] * v[c][2] + (w0[1] * v[c][1] + (w0[0] * v[c][0] + aC[c][o]));
+            aB[c][o] = w0[11] * v[c][2] + (w0[10] * v[c][1] + (w0[9] * v[c][0] + aB[c][o]));
+            aA[c][o] = w0[20] * v[c][2] + (w0[19] * v[c][1] + (w0[18] * v[c][0] + aA[c][o]));
           }
         }
-        __builtin_amdgcn_sched_barrier(0);  // one input row in flight at a time (VGPRs)
+        __builtin_amdgcn_sched_barrier(0);  // rows stay in order (VGPRs)
       }
     };
     for (int p = z0 - 1; p <= z1 + 1; ++p) {
@@ -524,10 +570,12 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
         asm volatile("" : "+v"(ltid));
         ln2_row(h2b + ((zl - z0) & 1) * H2F, ltid / LNL, ltid % LNL);
       }
-      if (live && dscat) rows(cur, 0, a.ws_split);
+      if (live && dscat) rows(cur, 0, WS_SPLIT);
+      PROBE(0)
       __syncthreads();  // 1 -> 2
+      PROBE(1)
       if (live) {
-        if (dscat) rows(cur, a.ws_split, K::PY);
+        if (dscat) rows(cur, WS_SPLIT, K::PY);
         const int zo = p - 1;
         if (zo >= z0) {
           float* h2t = h2b + ((zo - z0) & 1) * H2F;
@@ -552,8 +600,11 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
             aC[c][o] = f32x2{0.f, 0.f};
           }
       }
+      PROBE(2)
       __syncthreads();  // 2 -> next 1
+      PROBE(3)
     }
+    PROBE_DUMP
     return;
   }
 
@@ -632,7 +683,9 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
       asm volatile("" : "+v"(ltid));
       ln2_row(h2t, 16 + ltid / LNL, ltid % LNL);
     }
+    PROBE(0)
     __syncthreads();  // 1 -> 2: LN rows of tile (p-2) visible
+    PROBE(1)
     // ---- phase 2: commit plane p+1 into the free buffer (D is done with plane p-1 since the
     // last barrier of iteration p-1), fetch p+2, fc GEMM of tile (p-2) + residual + store
 #pragma unroll
@@ -668,8 +721,11 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
         *reinterpret_cast<f32x4*>(a.out + gpos * C + col) = v;
       }
     }
+    PROBE(2)
     __syncthreads();  // 2 -> next 1
+    PROBE(3)
   }
+  PROBE_DUMP
 }
 
 // ---------------------------------------------------------------------------------------
@@ -696,30 +752,6 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
 // (A variant that split LN2 into statistics on 4 waves + normalise / GELU / split by every
 // thread from its own registers, behind a fourth barrier, measured 380 vs 361 us.)
 // ---------------------------------------------------------------------------------------
-#ifdef WF_DWFC2_PROBE
-// diagnostic builds only: per-wave cycles of workgroup 0 by phase (C->A work, A wait, A->B
-// work, B wait, B->C work, C wait), read back by wf_debug_dwfc2_probe
-__device__ long long g_dwfc2_probe[12 * 8];
-extern "C" int wf_debug_dwfc2_probe(long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dwfc2_probe), sizeof(g_dwfc2_probe));
-}
-#define PROBE_DECL                                                              \
-  const bool probe_on = blockIdx.x == 0;                                         \
-  long long pr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pr_last = __builtin_amdgcn_s_memtime();
-#define PROBE(i)                                                                \
-  if (probe_on) {                                                               \
-    const long long t_ = __builtin_amdgcn_s_memtime();                          \
-    pr_acc[i] += t_ - pr_last;                                                  \
-    pr_last = t_;                                                               \
-  }
-#define PROBE_DUMP                                                              \
-  if (probe_on && (tid & 63) == 0)                                              \
-    for (int i_ = 0; i_ < 8; ++i_) g_dwfc2_probe[wid * 8 + i_] = pr_acc[i_];
-#else
-#define PROBE_DECL
-#define PROBE(i)
-#define PROBE_DUMP
-#endif
 
 struct DwFc2 {
   static constexpr int C = 96, HID = 384, TY = 4, TX = 4;
@@ -800,17 +832,23 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc2_kernel(DwFcArgs a) {
 #pragma unroll
     for (int o = 0; o < TY; ++o) aA[q][o] = aB[q][o] = aC[q][o] = 0.f;
   const bool dscat = !(a.dbg & 1);  // timing experiments only (WF_FFN_DBG)
-  // input rows [r_lo, r_hi) of the current plane into output planes +1 (aC), 0 (aB), -1 (aA)
+  // input rows [r_lo, r_hi) (compile-time after inlining) of the current plane into output
+  // planes +1 (aC), 0 (aB), -1 (aA); each row's four LDS reads are issued one row ahead of its
+  // FMAs, unconditionally (a load pending across a branch join is waited for at the join)
   auto rows = [&](int r_lo, int r_hi) {
     if (!dscat) return;
     const float* Pin = plane + 2 * xp * HID + c;
+    float nx[4];
+    auto ld = [&](int r) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) nx[k] = Pin[(r * K::PX + k) * HID];
+    };
+    ld(r_lo);
 #pragma unroll
     for (int r = 0; r < K::PY; ++r) {
       if (r < r_lo || r >= r_hi) continue;
-      const float u0 = Pin[(r * K::PX + 0) * HID];
-      const float u1 = Pin[(r * K::PX + 1) * HID];
-      const float u2 = Pin[(r * K::PX + 2) * HID];
-      const float u3 = Pin[(r * K::PX + 3) * HID];
+      const float u0 = nx[0], u1 = nx[1], u2 = nx[2], u3 = nx[3];
+      if (r + 1 < r_hi) ld(r + 1);
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky) {
         const int o = r - ky;
@@ -823,7 +861,7 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc2_kernel(DwFcArgs a) {
         aA[0][o] = fmaf(w0[20], u2, fmaf(w0[19], u1, fmaf(w0[18], u0, aA[0][o])));
         aA[1][o] = fmaf(w0[20], u3, fmaf(w0[19], u2, fmaf(w0[18], u1, aA[1][o])));
       }
-      __builtin_amdgcn_sched_barrier(0);  // one input row in flight at a time (VGPRs)
+      __builtin_amdgcn_sched_barrier(0);  // rows stay in order (VGPRs)
     }
   };
   // the completed output plane (aA + bias) into the fp32 h2 tile, then the accumulators roll
@@ -887,7 +925,10 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc2_kernel(DwFcArgs a) {
       if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + cc) = lo4;
     }
   };
-  const int sF = a.ws_split & 7, sG = (a.ws_split >> 3) & 7;  // scatter rows before B
+  // depthwise input rows scattered before barrier B by the F waves (sF) and waves 6, 7 (sG)
+  // (B = 8 stage 2, runtime-swept: (sF, sG) = (3, 3) 352 us, (6, 3) 337, (2, 2) 361, (4, 4)
+  // 337, (6, 6) 345)
+  constexpr int sF = 4, sG = 4;
   PROBE_DECL
 
   if (wid < K::CT) {
@@ -1052,10 +1093,6 @@ int launch_ffn_dwfc2(const DwFcArgs& a, int prec, hipStream_t s) {
   while (ZS > 8 && base * cdiv(g.D, ZS) < 512) ZS = (ZS + 1) / 2;
   g.ZS = ZS;
   g.dbg = getenv("WF_FFN_DBG") ? atoi(getenv("WF_FFN_DBG")) : 0;  // timing experiments only
-  // depthwise input rows scattered before barrier B: F waves (bits 0..2), waves 6, 7 (3..5);
-  // B = 8 stage 2: (F, 6/7) = (3, 3) 352 us, (6, 3) 337, (2, 2) 361, (4, 4) 337, (6, 6) 345
-  static const int split = getenv("WF_FFN2_SPLIT") ? atoi(getenv("WF_FFN2_SPLIT")) : 4 + 8 * 4;
-  g.ws_split = split;
   const int64_t blocks = base * cdiv(g.D, ZS);
   void (*kern)(DwFcArgs) = prec == PREC_SPLIT  ? ffn_dwfc2_kernel<PREC_SPLIT, float>
                            : prec == PREC_FP16 ? ffn_dwfc2_kernel<PREC_FP16, float>
@@ -1095,11 +1132,6 @@ static int go_dwfc_ws(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks
   g.ZS = ZS;
   const int64_t blocks = base * cdiv(g.D, ZS);
   const size_t lds = (size_t)(2 * K::PLANE_F + 2 * K::H2_F + 2 * HID + 3 * C) * 4;
-  // D's input rows split over the two phases: rows 0..1 (3 of the 12 row-tap FMA groups)
-  // alongside E's LN2 + GELU, rows 2..5 alongside E's commit + fetch + fc (B = 8 stage 1,
-  // split 0..5: 916, 894, 879-888, 903, 934, 952 us; the classic kernel 1072 us)
-  static const int split = getenv("WF_FFN_WS_SPLIT") ? atoi(getenv("WF_FFN_WS_SPLIT")) : 2;
-  g.ws_split = split;
   static const int dbg = getenv("WF_FFN_DBG") ? atoi(getenv("WF_FFN_DBG")) : 0;
   g.dbg = dbg;  // timing experiments only: bit mask of phases skipped (results invalid)
   void (*kern)(DwFcArgs) = prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>
