@@ -163,12 +163,14 @@ def test_attention_vs_oracle(ws, heads, dim, B_):
         assert C.rel_l2(out, ref) <= tol, prec
 
 
-@pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (1, 16, 16, 16), (1, 3, 12, 9)])
+@pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (1, 16, 16, 16), (1, 3, 12, 9),
+                                   (1, 20, 8, 8), (3, 7, 4, 9)])
 @pytest.mark.parametrize("block", [False, True])
 def test_ccf_ffn_stage1_fused_vs_oracle(shape, block):
     """C = 48, hidden = 192: the fused dwconv + LN2 + GELU + fc + residual kernel
-    (ffn_dwfc.hip), ragged tiles included; Block form (norm2 + Q4 double residual, per-sample
-    DropPath factors) and bare CCF_FFN.forward."""
+    (ffn_dwfc.hip), ragged tiles included, z segments shorter than the volume at (1, 20, 8, 8);
+    Block form (norm2 + Q4 double residual, per-sample DropPath factors) and bare
+    CCF_FFN.forward."""
     import waveformer_amd.network_models as NM
     from oracle.weight_rule import rule_state_dict
     from waveformer_amd import ops
@@ -183,7 +185,7 @@ def test_ccf_ffn_stage1_fused_vs_oracle(shape, block):
         norm2.bias.copy_(seeded_randn((48,), 32) * 0.1)
     norm2 = norm2.to(DEV)
     x = seeded_randn(shape + (48,), 33)
-    bs = torch.tensor([0.5, 2.0][:B])
+    bs = torch.tensor([0.5, 2.0, 1.0][:B])
     if block:
         n2 = F.layer_norm(x, [48], norm2.weight.detach().cpu(), norm2.bias.detach().cpu(), 1e-6)
         ref = x + R.ccf_ffn(sd, "", n2) * bs.view(-1, 1, 1, 1, 1)

@@ -729,6 +729,425 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_ws_kernel(DwFcArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// SIMD-balanced variant (round 3, the default): the same tile, planes and h2 tiles, but the
+// 12 waves get roles per SIMD so every SIMD carries the same VALU load -- the kernel is
+// VALU-issue-bound (s_memtime probes: each SIMD's VALU saturated, ~4 cycles per instruction),
+// and in ffn_dwfc_ws SIMDs 0/1 held two scatter waves + an LN2 wave against one on SIMDs 2/3:
+//   on each SIMD, 2 "D" waves: LN2 + GELU + split of 4 of the 32 tile positions each (16
+//        lanes x 12 channels per position), then the depthwise scatter of one tile column
+//        (lane l owns channels l, l + 64 and l + 128: consecutive lanes read consecutive LDS
+//        words; 27 weights per channel in VGPRs, LDS reads one row ahead, rolling
+//        output-plane accumulators);
+//   and 1 "E" wave: the h1 plane staging (fetch two planes ahead, commit one ahead) and the fc
+//        of one 16-channel output column tile over both 16-position row tiles (weights hi in
+//        VGPRs, lo in LDS; the E wave of the fourth SIMD has no fc tile) + bias + Q4 residual
+//        + store.
+// LN2 stays on the D waves: on a lone wave (the E wave) its dependent chains (reductions,
+// transcendentals) ran latency-bound, ~2x slower than interleaved over two waves per SIMD.
+// The E wave runs at raised priority: it is the youngest wave on its SIMD, and without it its
+// few VALU instructions waited behind the two D waves' streams (probe: fc + staging took
+// 3.3-3.5k cycles per plane against 1.9-2.4k for the scatter).
+// Roles are taken from the wave's SIMD (HW_ID), first come first served, so the balance does
+// not depend on how the dispatcher places waves; if a SIMD did not get exactly three waves the
+// roles fall back to wave-id order (still correct, just unbalanced).
+// Per input plane p, two barriers:
+//   phase 1: D  LN2 of h2 tile (p-2); scatter rows [0, SB_SPLIT) of plane p
+//            E  residual / norm2-statistics rows of output plane p-2
+//   phase 2: D  scatter rows [SB_SPLIT, 6) of plane p -> output plane p-1 -> h2 tile (p-1)
+//            E  commit plane p+1, fetch plane p+2, fc of tile (p-2) + epilogue + store
+// The plane loop is unrolled by three so the rolling accumulators are renamed, not moved, and
+// each output plane's first contribution assigns instead of accumulating.
+//
+// Measured at B = 8 (tools/gpu_ab3.sh, one box, three rounds): 1047-1055 us against
+// 1056-1071 for ffn_dwfc_ws.  s_memtime probes put every SIMD's VALU ~86 % busy: the kernel is
+// bound by FP32 VALU work (27 depthwise FMAs + ~25 for LN2 / GELU / split per element).  A
+// build with packed-FP32 scatter and LN2 (the D waves read only LDS, so the packed-op hazard
+// of DESIGN.md 6.1 could not apply) measured 1058-1066 us: v_pk_fma_f32 costs the issue time
+// of two v_fma_f32 here, so it is not used.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int hw_simd_id() {
+  // HW_ID (hwreg 4) bits [5:4]: the SIMD the wave runs on
+  return (int)((__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4)) & 3);
+}
+
+template <int P, typename T>
+__global__ __launch_bounds__(768, 1) void ffn_dwfc_sb_kernel(DwFcArgs a) {
+  constexpr int C = 48, HID = 192, TY = 4, TX = 8;
+  constexpr bool SPLIT = P == PREC_SPLIT;
+  typedef DwFcCfg<C, HID, TY, TX> K;
+  typedef H1Load<T> L;
+  constexpr int NE = 256;                              // E threads (4 waves)
+  constexpr int NLDE = (K::PP * K::NV + NE - 1) / NE;  // staged vectors per E thread (12)
+  constexpr int H2F = K::NPOS * K::HS;
+  constexpr int LNL = 16, LNC = HID / LNL;             // LN2: 16 lanes x 12 channels / position
+#ifndef WF_SB_SPLIT
+#define WF_SB_SPLIT 0
+#endif
+  constexpr int SB_SPLIT = WF_SB_SPLIT;                // D rows scattered in phase 1
+  static_assert(TX == 8 && K::NPOS == 32 && HID == 3 * 64, "8 D waves = 8 tile columns");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* planes = lds;                                  // [2][PP][HID]
+  float* h2b = lds + 2 * K::PLANE_F;                     // [2][NPOS][HS]
+  float* lnw = h2b + 2 * H2F;                            // [HID] (halved: GELU from x / 2)
+  float* lnb = lnw + HID;
+  float* fcb = lnb + HID;                                // [C]
+  float* n2w = fcb + C;
+  float* n2b = n2w + C;
+  // fc weight lo plane [C][HID] bf16 (the E waves keep only the hi plane in VGPRs)
+  uint16_t* fwlo = reinterpret_cast<uint16_t*>(n2b + C);
+  __shared__ int simd_cnt[4];
+
+  const int tid = threadIdx.x;
+  const int wid = tid >> 6, lane = tid & 63;
+  const int D = a.D, H = a.H, W = a.W;
+  const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY, nzs = (D + a.ZS - 1) / a.ZS;
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int xt = t % ntx;
+  t /= ntx;
+  const int yt = t % nty;
+  t /= nty;
+  const int zt = t % nzs;
+  const int b = t / nzs;
+  const int x0 = xt * TX, y0 = yt * TY, z0 = zt * a.ZS, z1 = min(z0 + a.ZS, D);
+  const int64_t plane_sz = (int64_t)H * W;
+
+  if (tid < 4) simd_cnt[tid] = 0;
+  for (int i = tid; i < HID; i += K::NTH) {
+    lnw[i] = 0.5f * a.ln2_w[i];
+    lnb[i] = 0.5f * a.ln2_b[i];
+  }
+  for (int i = tid; i < C; i += K::NTH) {
+    fcb[i] = a.fc_b ? a.fc_b[i] : 0.f;
+    n2w[i] = a.stats ? a.n2_w[i] : 1.f;
+    n2b[i] = a.stats ? a.n2_b[i] : 0.f;
+  }
+  if (SPLIT)
+    for (int i = tid; i < C * HID / 8; i += K::NTH)
+      reinterpret_cast<bf16x8*>(fwlo)[i] = reinterpret_cast<const bf16x8*>(a.fc + C * HID)[i];
+  // depthwise weights and bias, coalesced into the (not yet used) plane buffer
+  for (int i = tid; i < HID * 27; i += K::NTH) planes[i] = a.dw_w[i];
+  for (int i = tid; i < HID; i += K::NTH) planes[HID * 27 + i] = a.dw_b[i];
+  __syncthreads();
+  // ---- roles: per SIMD, arrival slots 0, 1 -> D waves 2 s, 2 s + 1; slot 2 -> E wave s
+  const int simd = hw_simd_id();
+  int slot = 0;
+  if (lane == 0) slot = atomicAdd(&simd_cnt[simd], 1);
+  slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0, 64));
+  __syncthreads();
+  const bool even = simd_cnt[0] == 3 && simd_cnt[1] == 3 && simd_cnt[2] == 3 && simd_cnt[3] == 3;
+  int role = even ? (slot < 2 ? 2 * simd + slot : 8 + simd) : wid;  // 0..7 D, 8..11 E
+  role = __builtin_amdgcn_readfirstlane(role);
+
+  // LN2 + GELU + the bf16 hi / lo split of one h2 tile row, rewritten in place (16 lanes)
+  auto ln2_row = [&](float* h2t, int pos, int g) {
+    float* row = h2t + pos * K::HS;
+    float v[LNC];
+#pragma unroll
+    for (int j = 0; j < LNC / 4; ++j) {
+      const f32x4 u = *reinterpret_cast<const f32x4*>(row + g * LNC + 4 * j);
+      v[4 * j] = u.x;
+      v[4 * j + 1] = u.y;
+      v[4 * j + 2] = u.z;
+      v[4 * j + 3] = u.w;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < LNC; ++j) sm += v[j];
+    const float mean = group_sum<LNL>(sm) * (1.f / HID);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < LNC; ++j) {
+      const float d = v[j] - mean;
+      q += d * d;
+    }
+    const float rstd = rsqrtf(group_sum<LNL>(q) * (1.f / HID) + a.eps2);
+    const float nmr = -mean * rstd;
+    uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
+#pragma unroll
+    for (int j = 0; j < LNC / 4; ++j) {
+      const int c = g * LNC + 4 * j;
+      const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + c);
+      const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + c);
+      const f32x4 y = gelu_half4((f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]} *
+                                  rstd + nmr) * lw4 + lb4);
+      bf16x4 hi4, lo4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint16_t hb = op_cvt<P>(y[k]);
+        hi4[k] = (short)hb;
+        lo4[k] = op_lo<P>(y[k], hb);
+      }
+      *reinterpret_cast<bf16x4*>(rowh + c) = hi4;
+      if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + c) = lo4;
+    }
+  };
+
+  PROBE_DECL
+#ifdef WF_DWFC2_PROBE
+  pr_acc[6] = role;
+  pr_acc[7] = simd * 16 + slot + (even ? 256 : 0);
+#endif
+  if (role < 8) {
+    // ================================ D waves: depthwise scatter ==========================
+    const int xc = role;  // tile column
+    f32x2 wp[27];         // channels l, l + 64 (a pair: two v_fma_f32 per operation)
+    float wsg[27];        // channel l + 128
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      wp[k] = f32x2{planes[lane * 27 + k], planes[(lane + 64) * 27 + k]};
+      wsg[k] = planes[(lane + 128) * 27 + k];
+    }
+    const f32x2 biasp = f32x2{planes[HID * 27 + lane], planes[HID * 27 + lane + 64]};
+    const float biass = planes[HID * 27 + lane + 128];
+    f32x2 accp[3][TY];  // output-plane accumulators, slot (o - z0 + 2) mod 3
+    float accs[3][TY];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int o = 0; o < TY; ++o) {
+        accp[s][o] = f32x2{0.f, 0.f};
+        accs[s][o] = 0.f;
+      }
+    __syncthreads();  // (prologue) weights read out of the plane buffer
+    __syncthreads();  // (prologue) plane z0-1 committed
+    // input rows [r_lo, r_hi) of plane `cur` into A = acc[SA] (kz 2), B = acc[SB] (kz 1) and
+    // C = acc[SC] (kz 0, first touch assigns); each row's LDS reads issued one row ahead
+    auto rows = [&](const float* cur, auto SAc, auto SBc, auto SCc, int r_lo, int r_hi) {
+      constexpr int SA = decltype(SAc)::value, SB = decltype(SBc)::value,
+                    SC = decltype(SCc)::value;
+      f32x2 nxp[3];
+      float nxs[3];
+      auto ld = [&](int r) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float* q = cur + (r * K::PX + xc + k) * HID + lane;
+          nxp[k] = f32x2{q[0], q[64]};
+          nxs[k] = q[128];
+        }
+      };
+      if (r_lo < r_hi) ld(r_lo);
+#pragma unroll
+      for (int r = 0; r < K::PY; ++r) {
+        if (r < r_lo || r >= r_hi) continue;
+        f32x2 vp[3];
+        float vs[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          vp[k] = nxp[k];
+          vs[k] = nxs[k];
+        }
+        if (r + 1 < r_hi) ld(r + 1);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int o = r - ky;
+          if (o < 0 || o >= TY) continue;
+          const f32x2* w0 = wp + ky * 3;
+          const float* s0 = wsg + ky * 3;
+          if (ky == 0) {
+            accp[SC][o] = w0[2] * vp[2] + (w0[1] * vp[1] + w0[0] * vp[0]);
+            accs[SC][o] = s0[2] * vs[2] + (s0[1] * vs[1] + s0[0] * vs[0]);
+          } else {
+            accp[SC][o] = w0[2] * vp[2] + (w0[1] * vp[1] + (w0[0] * vp[0] + accp[SC][o]));
+            accs[SC][o] = s0[2] * vs[2] + (s0[1] * vs[1] + (s0[0] * vs[0] + accs[SC][o]));
+          }
+          accp[SB][o] = w0[11] * vp[2] + (w0[10] * vp[1] + (w0[9] * vp[0] + accp[SB][o]));
+          accs[SB][o] = s0[11] * vs[2] + (s0[10] * vs[1] + (s0[9] * vs[0] + accs[SB][o]));
+          accp[SA][o] = w0[20] * vp[2] + (w0[19] * vp[1] + (w0[18] * vp[0] + accp[SA][o]));
+          accs[SA][o] = s0[20] * vs[2] + (s0[19] * vs[1] + (s0[18] * vs[0] + accs[SA][o]));
+        }
+        __builtin_amdgcn_sched_barrier(0);  // rows stay in order (VGPRs)
+      }
+    };
+    // one input plane p; R = (p - z0 + 1) mod 3 at compile time
+    auto step = [&](int p, auto Rc) {
+      constexpr int R = decltype(Rc)::value;
+      typedef std::integral_constant<int, R> SA;
+      typedef std::integral_constant<int, (R + 1) % 3> SB;
+      typedef std::integral_constant<int, (R + 2) % 3> SC;
+      const bool live = p <= z1;
+      const float* cur = planes + ((p - z0 + 1) & 1) * K::PLANE_F;
+      const bool dscat = !(a.dbg & 1);  // timing experiments only (WF_FFN_DBG)
+      const int zl = p - 2;
+      if (zl >= z0 && zl < z1 && !(a.dbg & 2)) {
+        int ltid = lane;
+        asm volatile("" : "+v"(ltid));
+        ln2_row(h2b + ((zl - z0) & 1) * H2F, 4 * xc + ltid / LNL, ltid % LNL);
+      }
+      if (live && dscat) rows(cur, SA(), SB(), SC(), 0, SB_SPLIT);
+      PROBE(0)
+      __syncthreads();  // 1 -> 2
+      PROBE(1)
+      if (live) {
+        if (dscat) rows(cur, SA(), SB(), SC(), SB_SPLIT, K::PY);
+        const int zo = p - 1;
+        if (zo >= z0) {
+          float* h2t = h2b + ((zo - z0) & 1) * H2F;
+#pragma unroll
+          for (int o = 0; o < TY; ++o) {
+            float h[3] = {accp[R][o].x + biasp.x, accp[R][o].y + biasp.y, accs[R][o] + biass};
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              if (sizeof(T) == 2) h[j] = bf2f(f2bf(h[j]));
+              h2t[(o * TX + xc) * K::HS + lane + 64 * j] = h[j];
+            }
+          }
+        }
+      }
+      PROBE(2)
+      __syncthreads();  // 2 -> next 1
+      PROBE(3)
+    };
+    // p - z0 + 1 = 0, 1, 2, ... : R cycles 0, 1, 2
+    for (int p = z0 - 1; p <= z1 + 1; p += 3) {
+      step(p, std::integral_constant<int, 0>());
+      if (p + 1 <= z1 + 1) step(p + 1, std::integral_constant<int, 1>());
+      if (p + 2 <= z1 + 1) step(p + 2, std::integral_constant<int, 2>());
+    }
+    PROBE_DUMP
+    return;
+  }
+
+  // ================================== E waves ============================================
+  __builtin_amdgcn_s_setprio(3);
+  const int e = role - 8, et = e * 64 + lane;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const bool has_fc = e < C / 16;  // E waves 0..2: one output column tile each
+  const int ct = has_fc ? e : 0;
+  const T* src = reinterpret_cast<const T*>(a.h1) + (int64_t)b * D * H * W * HID;
+  const int64_t plane_elems = (int64_t)H * W * HID;
+  const float bs = a.bscale ? a.bscale[b] : 1.f;
+
+  // fc weights hi in registers: A operand rows ct*16 + l15, k = ks*32 + 8 g4; lo from LDS
+  bf16x8 fwh[HID / 32];
+  const uint16_t* fwl = fwlo + (ct * 16 + l15) * HID + 8 * g4;
+  {
+    const uint16_t* wr = a.fc + (size_t)(ct * 16 + l15) * HID + 8 * g4;
+#pragma unroll
+    for (int ks = 0; ks < HID / 32; ++ks) fwh[ks] = *reinterpret_cast<const bf16x8*>(wr + ks * 32);
+  }
+  // h1 staging: byte offsets inside one plane, loaded through a per-plane buffer descriptor
+  // (32-bit voffsets).  Halo positions outside the volume get an offset past the descriptor's
+  // range and planes outside [0, D) a zero-range descriptor: the loads return the zero
+  // padding themselves and the commit is a plain copy.
+  uint32_t off[NLDE];
+#pragma unroll
+  for (int j = 0; j < NLDE; ++j) {
+    const int i = min(j * NE + et, K::PP * K::NV - 1);
+    const int pos = i / K::NV, v = i - pos * K::NV;
+    const int yy = y0 - 1 + pos / K::PX, xx = x0 - 1 + pos % K::PX;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    off[j] = ok ? (uint32_t)(((yy * W + xx) * HID + 4 * v) * (int)sizeof(T)) : 0x80000000u;
+  }
+  typename L::raw stg[NLDE];
+  auto fetch = [&](int p) {
+    const bool pz = p >= 0 && p < D;
+    const T* base = src + (int64_t)min(max(p, 0), D - 1) * plane_elems;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(base), 0, pz ? (int)(plane_elems * (int64_t)sizeof(T)) : 0, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NLDE; ++j) {
+      if constexpr (sizeof(T) == 4)
+        stg[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[j], 0, 0));
+      else
+        stg[j] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(rs, off[j], 0, 0));
+    }
+  };
+  auto commit = [&](float* dst) {
+    float* d0 = dst + et * 4;
+#pragma unroll
+    for (int j = 0; j < NLDE; ++j)
+      if ((j + 1) * NE <= K::PP * K::NV || j * NE + et < K::PP * K::NV)
+        *reinterpret_cast<f32x4*>(d0 + j * NE * 4) = L::up(stg[j]);
+  };
+  const int col = ct * 16 + 4 * g4;
+  const float* sbase = a.stats ? a.stats : a.x;
+  // output position of this lane's fc row in row tile rt
+  auto gpos_of = [&](int zo, int rt, bool clamp) {
+    const int lp = rt * 16 + l15;
+    int yo = y0 + lp / TX, xo = x0 + lp % TX;
+    if (clamp) {
+      yo = min(yo, H - 1);
+      xo = min(xo, W - 1);
+    }
+    return (int64_t)b * D * plane_sz + (int64_t)zo * plane_sz + (int64_t)yo * W + xo;
+  };
+  auto row_ok = [&](int rt) {
+    const int lp = rt * 16 + l15;
+    return y0 + lp / TX < H && x0 + lp % TX < W;
+  };
+  f32x4 xr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  f32x2 es[2] = {f32x2{0.f, 1.f}, f32x2{0.f, 1.f}};
+  auto load_resid = [&](int zo, int rt) {
+    const int64_t g = gpos_of(zo, rt, true);
+    xr[rt] = *reinterpret_cast<const f32x4*>(a.x + g * C + col);
+    es[rt] = *reinterpret_cast<const f32x2*>(sbase + 2 * g);
+  };
+  // fc of row tile rt of h2 tile h2t + bias + Q4 residual + store of output plane zo
+  auto fc_store = [&](const float* h2t, int zo, int rt) {
+    const int lp = rt * 16 + l15;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)lp * (2 * K::HS);
+#pragma unroll
+    for (int ks = 0; ks < HID / 32; ++ks) {
+      const int k = ks * 32 + 8 * g4;
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bh + k);
+      if (SPLIT) {
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
+        acc = mma32<P>(fwh[ks], bl, acc);
+        acc = mma32<P>(*reinterpret_cast<const bf16x8*>(fwl + ks * 32), bh, acc);
+      }
+      acc = mma32<P>(fwh[ks], bh, acc);
+    }
+    f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+    const f32x4 xv = xr[rt];
+    if (a.stats) {
+      const f32x4 lw = *reinterpret_cast<const f32x4*>(n2w + col);
+      const f32x4 lb = *reinterpret_cast<const f32x4*>(n2b + col);
+      const float em = es[rt].x, er = es[rt].y;
+      const f32x4 n2 = (xv - em) * er * lw + lb;
+      v = xv + (n2 + v) * bs;
+    } else {
+      v = xv + v * bs;
+    }
+    if (row_ok(rt)) *reinterpret_cast<f32x4*>(a.out + gpos_of(zo, rt, false) * C + col) = v;
+  };
+
+  fetch(z0 - 1);
+  __syncthreads();  // (prologue) weights read out of the plane buffer
+  commit(planes);
+  fetch(z0);
+  __syncthreads();  // (prologue) plane z0-1 visible
+  for (int p = z0 - 1; p <= z1 + 1; ++p) {
+    const int zo = p - 2;  // output plane this iteration finishes
+    const bool epi = has_fc && zo >= z0 && zo < z1;
+    float* h2t = h2b + ((zo - z0) & 1) * H2F;
+    // ---- phase 1: residual / statistics rows of plane p-2
+    if (epi) {
+      load_resid(zo, 0);
+      load_resid(zo, 1);
+    }
+    PROBE(0)
+    __syncthreads();  // 1 -> 2: LN rows of tile (p-2) visible
+    PROBE(1)
+    // ---- phase 2: commit plane p+1 into the free buffer, fetch p+2, fc of tile (p-2)
+#pragma unroll
+    for (int j = 0; j < NLDE; ++j) asm volatile("" ::"v"(stg[j]));
+    if (p + 1 <= z1 && !(a.dbg & 8)) commit(planes + ((p - z0) & 1) * K::PLANE_F);
+    if (p + 2 <= z1 && !(a.dbg & 8)) fetch(p + 2);
+    if (epi && !(a.dbg & 4)) {
+      fc_store(h2t, zo, 0);
+      fc_store(h2t, zo, 1);
+    }
+    PROBE(2)
+    __syncthreads();  // 2 -> next 1
+    PROBE(3)
+  }
+  PROBE_DUMP
+}
+
+// ---------------------------------------------------------------------------------------
 // Stage-2 shape (C = 96, hidden = 384): the same back half, re-tiled for a 4C row twice as
 // wide.  Double-buffered planes and h2 tiles no longer fit next to the fc weights, so this one
 // keeps ONE plane buffer (the next plane waits in registers) and 4 x 4 tiles:
@@ -1131,12 +1550,20 @@ static int go_dwfc_ws(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks
   while (ZS > 8 && base * cdiv(g.D, ZS) < min_blocks) ZS = (ZS + 1) / 2;
   g.ZS = ZS;
   const int64_t blocks = base * cdiv(g.D, ZS);
-  const size_t lds = (size_t)(2 * K::PLANE_F + 2 * K::H2_F + 2 * HID + 3 * C) * 4;
+  // + the fc weight lo plane for the SIMD-balanced kernel (bf16x3 only)
+  const size_t lds = (size_t)(2 * K::PLANE_F + 2 * K::H2_F + 2 * HID + 3 * C) * 4 +
+                     (prec == PREC_SPLIT ? (size_t)C * HID * 2 : 0);
   static const int dbg = getenv("WF_FFN_DBG") ? atoi(getenv("WF_FFN_DBG")) : 0;
   g.dbg = dbg;  // timing experiments only: bit mask of phases skipped (results invalid)
-  void (*kern)(DwFcArgs) = prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>
-                           : prec == PREC_FP16 ? ffn_dwfc_ws_kernel<PREC_FP16, float>
-                                               : ffn_dwfc_ws_kernel<PREC_BF16, uint16_t>;
+  // WF_FFN_DWFC_WS=1: the round-2 wave-specialised kernel (A/B); default the SIMD-balanced one
+  static const bool ws = getenv("WF_FFN_DWFC_WS") != nullptr;
+  void (*kern)(DwFcArgs) =
+      ws ? (prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>
+            : prec == PREC_FP16 ? ffn_dwfc_ws_kernel<PREC_FP16, float>
+                                : ffn_dwfc_ws_kernel<PREC_BF16, uint16_t>)
+         : (prec == PREC_SPLIT  ? ffn_dwfc_sb_kernel<PREC_SPLIT, float>
+            : prec == PREC_FP16 ? ffn_dwfc_sb_kernel<PREC_FP16, float>
+                                : ffn_dwfc_sb_kernel<PREC_BF16, uint16_t>);
   set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(K::NTH), lds, s, g);
   return check_launch("ffn_dwfc_ws");
