@@ -46,7 +46,8 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 # bench op name -> kernel-name substring in the PMC summary (profiles/*pmc*.json)
 PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_fused_kernel" if os.environ.get("WF_FFN_FUSED")
               else "ffn_dwfc_kernel" if os.environ.get("WF_FFN_DWFC_CLASSIC")
-              else "ffn_dwfc_ws_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
+              else "ffn_dwfc_ws_kernel" if os.environ.get("WF_FFN_DWFC_WS")
+              else "ffn_dwfc_sb_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
               "window_attention": "attn_tbl_kernel",
               "msfuse": "msfuse", "proj_out": "proj_out"}
 
@@ -218,6 +219,54 @@ def pmc_traffic(kernel_substr, batch):
                 return v.get("hbm_bytes_per_launch_largest")
         return None
     return None
+
+
+def pmc_valu(kernel_substr, batch):
+    """(VALU issue fraction, source file) of a kernel from the newest profiles/*valu*.json
+    written by tools/pmc_valu.py at this per-GPU batch; (None, None) when none matches."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*valu*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("per_gpu_batch") != batch:
+            continue
+        for k, v in d["kernels"].items():
+            if kernel_substr in k:
+                return v["valu_issue_frac"], os.path.relpath(f, REPO)
+        return None, None
+    return None, None
+
+
+def idwt_roofline(batch, dev):
+    """The decoder's level-0 Haar IDWT (UnetrIDWTBlock's waverec3 replacement,
+    idwt_upsample.py:160, §8a row a11) at the encoder's stage-0 band shape: 8 bands of
+    (B, 48, 64^3) -> (B, 48, 128^3), written into the first half of a 96-channel concat buffer
+    as the decoder does.  Algorithmic bytes: read 8 bands + write the output, 8 B per output
+    element.  HIP events on the launch stream around REPS back-to-back launches."""
+    from waveformer_amd import ops
+    g = torch.Generator(device=dev).manual_seed(7)
+    shp = (batch, 48, 64, 64, 64)
+    ll = torch.randn(shp, device=dev, generator=g)
+    det = [{k: torch.randn(shp, device=dev, generator=g) for k in ops.DETAIL_KEYS}]
+    out = torch.empty(batch, 96, 128, 128, 128, device=dev)
+    ops.idwt3d_haar(ll, det, out=out)
+    reps = 10
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        ops.idwt3d_haar(ll, det, out=out)
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) / reps * 1e3
+    alg = 8 * batch * 48 * 128 ** 3  # 8 B per output element (4 B of bands read + 4 B written)
+    ach = alg / (us * 1e-6) / 1e9
+    del ll, det, out
+    return {"bound": "hbm", "kernel": "idwt3d_haar", "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": pmc_traffic("idwt3d_haar", batch), "algorithmic_bytes_per_launch": alg,
+            "avg_launch_us": round(us, 2), "launches_timed": reps,
+            "shape": f"8 x ({batch}, 48, 64^3) -> ({batch}, 48, 128^3) into a 96-channel buffer"}
 
 
 def build_encoder(img, device):
@@ -648,15 +697,29 @@ def main():
                         "launches_timed": r["launches"],
                         "mfma_issue_frac": round(issue * ach / MFMA_BF16_PEAK_TFLOPS, 4)}
             ach = r["rate"] / 1e9
-            return {"bound": "hbm", "kernel": name, "achieved": round(ach, 1),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                    "traffic": pmc_traffic(PMC_KERNEL.get(name, name), args.batch),
-                    "algorithmic_bytes_per_launch": r["work_per_launch"],
-                    "avg_launch_us": round(r["avg_ms"] * 1e3, 2), "launches_timed": r["launches"]}
+            d = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1),
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                 "traffic": pmc_traffic(PMC_KERNEL.get(name, name), args.batch),
+                 "algorithmic_bytes_per_launch": r["work_per_launch"],
+                 "avg_launch_us": round(r["avg_ms"] * 1e3, 2), "launches_timed": r["launches"]}
+            if name == "ccf_ffn_dwconv":
+                # the kernel is FP32-VALU-bound: its VALU issue fraction from
+                # the committed counter pass of the same bench command
+                vf, src = pmc_valu(PMC_KERNEL[name], args.batch)
+                if vf is not None:
+                    d["valu_issue_frac"], d["valu_source"] = vf, src
+            return d
 
         if roofs.get(roof_op):
             out["roofline"] = roofline(roof_op, roofs[roof_op])
         out["rooflines"] = {n: roofline(n, r) for n, r in roofs.items() if r and n != roof_op}
+        if args.op_timers and not full:
+            out["rooflines"]["idwt3d_haar"] = idwt_roofline(args.batch, dev)
+        if "window_attention" in out["rooflines"]:
+            vf, src = pmc_valu("attn_tbl_kernel", args.batch)
+            if vf is not None:
+                out["rooflines"]["window_attention"]["core_valu_issue_frac"] = vf
+                out["rooflines"]["window_attention"]["valu_source"] = src
         if args.parity:
             try:
                 out["parity"] = parity_dice(dev, "full192hf" if hf else "full128")

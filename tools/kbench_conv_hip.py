@@ -14,6 +14,7 @@ _lib.load()
 SHAPES = [  # (B, Cin, Cout, S) -- sliding-window batches of 2
     (2, 4, 48, 128), (2, 48, 48, 128), (2, 96, 48, 128), (2, 96, 48, 64), (2, 48, 48, 64),
     (2, 384, 192, 8), (2, 384, 96, 8), (2, 192, 96, 16), (2, 96, 96, 32),
+    (2, 96, 48, 192), (2, 48, 48, 192),  # config 5's full-resolution decoder convs
 ]
 ITERS = int(os.environ.get("ITERS", "10"))
 only = int(sys.argv[1]) if len(sys.argv) > 1 else None
