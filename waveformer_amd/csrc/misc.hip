@@ -445,7 +445,12 @@ template <int G, int V>
 __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
   extern __shared__ __attribute__((aligned(16))) float R[];  // sum_s sw[s] * C
   const int C = a.C, C4 = C >> 2;
-  int r = blockIdx.x;
+  // XCD-contiguous row order: the hardware deals consecutive workgroups round-robin over the
+  // 8 XCDs, which put neighbouring output rows -- which read the same 4 source rows per
+  // source -- on different XCDs, each fetching them into its own L2 (PMC: 1.25x the
+  // algorithmic bytes at stage 1).  Each XCD takes a contiguous run of rows instead.
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  int r = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
   const int y = r % a.H;
   r /= a.H;
   const int z = r % a.D;
@@ -575,6 +580,15 @@ __global__ __launch_bounds__(256) void proj_out_kernel(const float* __restrict__
   }
   __syncthreads();
   float* ob = out + (int64_t)b * C * S + s0;
+  if (TP == 64) {
+    // lane = position, wave = channel stride: no per-element index division (the generic loop
+    // below divides by np for every element; the VALU pass showed the kernel 77 % issue-busy)
+    const int p = threadIdx.x & 63;
+    if (p < np)
+      for (int c = threadIdx.x >> 6; c < C; c += blockDim.x >> 6)
+        ob[(int64_t)c * S + p] = T[c * (TP + 1) + p];
+    return;
+  }
   for (int i = threadIdx.x; i < C * np; i += blockDim.x) {
     const int c = i / np, p = i - c * np;
     ob[(int64_t)c * S + p] = T[c * (TP + 1) + p];
