@@ -246,9 +246,11 @@ def idwt_roofline(batch, dev):
     element.  HIP events on the launch stream around REPS back-to-back launches."""
     from waveformer_amd import ops
     g = torch.Generator(device=dev).manual_seed(7)
-    shp = (batch, 48, 64, 64, 64)
-    ll = torch.randn(shp, device=dev, generator=g)
-    det = [{k: torch.randn(shp, device=dev, generator=g) for k in ops.DETAIL_KEYS}]
+    # the decoder's inputs: detail bands as the channel-last views of the DWT's (8, B, d, h,
+    # w, C) output (ops.dwt3d_haar), the LL as an NCDHW tensor
+    bands = torch.randn(8, batch, 64, 64, 64, 48, device=dev, generator=g)
+    ll = bands[0].permute(0, 4, 1, 2, 3).contiguous()
+    det = [{k: bands[i + 1].permute(0, 4, 1, 2, 3) for i, k in enumerate(ops.DETAIL_KEYS)}]
     out = torch.empty(batch, 96, 128, 128, 128, device=dev)
     ops.idwt3d_haar(ll, det, out=out)
     reps = 10
@@ -261,12 +263,13 @@ def idwt_roofline(batch, dev):
     us = s.elapsed_time(e) / reps * 1e3
     alg = 8 * batch * 48 * 128 ** 3  # 8 B per output element (4 B of bands read + 4 B written)
     ach = alg / (us * 1e-6) / 1e9
-    del ll, det, out
+    del bands, ll, det, out
     return {"bound": "hbm", "kernel": "idwt3d_haar", "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic("idwt3d_haar", batch), "algorithmic_bytes_per_launch": alg,
             "avg_launch_us": round(us, 2), "launches_timed": reps,
-            "shape": f"8 x ({batch}, 48, 64^3) -> ({batch}, 48, 128^3) into a 96-channel buffer"}
+            "shape": f"channel-last bands 8 x ({batch}, 64^3, 48) -> ({batch}, 48, 128^3) NCDHW "
+                     f"into a 96-channel buffer"}
 
 
 def build_encoder(img, device):
