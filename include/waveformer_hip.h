@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 11
+#define WF_ABI_VERSION 12
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
@@ -113,6 +113,16 @@ int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float* ln_b, floa
 int wf_idwt3d_haar(const float* ll, int64_t ll_bstride, const float* const* det,
                    const int64_t* det_s, int levels, float* out, int64_t out_bstride,
                    int64_t B, int64_t C, int64_t d, int64_t h, int64_t w, void* stream);
+/* The same into a channel-last output (ABI 12): element (b, c, z, y, x) of out lives at
+ * out[b*out_bstride + ((z*H + y)*W + x)*ldo + c] -- channels [0, C) of a channels_last_3d
+ * buffer of ldo >= C channels, so the decoder's concat buffer (idwt_upsample.py:163) stays in
+ * the channel-last layout its convolutions read; the LL element (b, c, z, y, x) is read at
+ * ll[b*ll_bstride + c*ll_cstride + ((z*h + y)*w + x)*ll_pstride] (NCDHW: d*h*w, 1;
+ * channel-last: 1, its position stride).                                                  */
+int wf_idwt3d_haar_cl(const float* ll, int64_t ll_bstride, int64_t ll_cstride,
+                      int64_t ll_pstride, const float* const* det, const int64_t* det_s,
+                      int levels, float* out, int64_t out_bstride, int64_t ldo, int64_t B,
+                      int64_t C, int64_t d, int64_t h, int64_t w, void* stream);
 
 /* ---- C5: general wavelets (db1..db4), NCDHW, any sizes ------------------------------- */
 /* One analysis level of ptwt.wavedec3(x, wavelet, mode='zero') (wave_helper.py:350 with a

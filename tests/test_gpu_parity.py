@@ -86,6 +86,15 @@ def test_idwt_multilevel_vs_oracle_and_roundtrip(levels, C_, base):
     ops.idwt3d_haar(ll, dets_cl, out=buf)
     assert C.rel_l2(buf[:, :C_], ref) <= 1e-5
     assert torch.all(buf[:, C_:] == 7.0)
+    # channel-last concat buffer (the decoder's, ABI 12 wf_idwt3d_haar_cl), with the LL read
+    # channel-last too: the same values bit for bit, the skip channels untouched
+    if C_ % 4 == 0:
+        bcl = torch.full((B, C_ + 4) + full, 7.0, device=DEV).contiguous(
+            memory_format=torch.channels_last_3d)
+        llcl = ll.contiguous(memory_format=torch.channels_last_3d)
+        ops.idwt3d_haar(llcl, dets_cl, out=bcl)
+        assert torch.equal(bcl[:, :C_], buf[:, :C_])
+        assert torch.all(bcl[:, C_:] == 7.0)
 
 
 def test_encoder_hf_feed_idwt_roundtrip():

@@ -34,6 +34,8 @@ SIGNATURES = {
     "wf_patch_embed_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwt3d_haar_fwd": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_idwt3d_haar_cl": (_I, [_P, _I64, _I64, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64,
+                               _I64, _I64, _I64, _P]),
     "wf_dwt3d_fwd": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _I, _P]),
     "wf_idwt3d_level": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _P, _I, _P, _I64, _I64,
                              _P]),
@@ -106,7 +108,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 _lock = threading.Lock()
 _lib = None
 _err = None

@@ -107,11 +107,12 @@ __global__ __launch_bounds__(256) void dwt3d_haar_fwd_kernel(
 constexpr int kMaxLevels = 4;
 struct IdwtArgs {
   const float* ll;
-  int64_t ll_bstride;
+  int64_t ll_bstride, ll_cs, ll_ps;  // LL element (b, c, p) at b*ll_bstride + c*ll_cs + p*ll_ps
   const float* det[kMaxLevels * 7];
   int64_t ds[kMaxLevels * 4];  // per level: batch, channel, z, (y*W_l+x) strides
   float* out;
   int64_t out_bstride;
+  int64_t ldo;   // channel-last output (CL kernel): floats between positions, channels contiguous
   int levels, B, C, d, h, w, CB;
 };
 
@@ -123,6 +124,10 @@ __device__ __forceinline__ float idwt_coef(const IdwtArgs& a, int l, int k, int 
   return a.det[l * 7 + k][off];
 }
 
+// CL: write a channel-last output (the decoder's concat buffer kept channels_last_3d) -- the
+// LDS image is then [2][2][2*w1][CB+1] (channels innermost, padded) and phase 2 writes each
+// position's CB channels contiguously
+template <bool CL>
 __global__ __launch_bounds__(256) void idwt3d_haar_kernel(IdwtArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_out[];  // [CB][2][2][2*w1]
   const int L = a.levels;
@@ -141,8 +146,8 @@ __global__ __launch_bounds__(256) void idwt3d_haar_kernel(IdwtArgs a) {
     const int c = c0 + cl;
     // coarsest LL (NCDHW, contiguous spatial)
     const int zc = z1 >> (L - 1), yc = y1 >> (L - 1), xc = x1 >> (L - 1);
-    float ll = a.ll[b * a.ll_bstride + (int64_t)c * a.d * a.h * a.w +
-                    ((int64_t)zc * a.h + yc) * a.w + xc];
+    float ll = a.ll[b * a.ll_bstride + (int64_t)c * a.ll_cs +
+                    (((int64_t)zc * a.h + yc) * a.w + xc) * a.ll_ps];
     // levels 0..L-2 produce the LL of the next level at the ancestor of (z1,y1,x1)
     for (int l = 0; l < L - 1; ++l) {
       const int sh = L - 1 - l;             // ancestor at level l is (z1,y1,x1) >> sh
@@ -178,12 +183,26 @@ __global__ __launch_bounds__(256) void idwt3d_haar_kernel(IdwtArgs a) {
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
       const int sz = n >> 2, sy = (n >> 1) & 1, sx = n & 1;
-      lds_out[((cl * 2 + sz) * 2 + sy) * Wo + 2 * x1 + sx] = v[n] * kHaar3;
+      if (CL)
+        lds_out[((sz * 2 + sy) * Wo + 2 * x1 + sx) * (a.CB + 1) + cl] = v[n] * kHaar3;
+      else
+        lds_out[((cl * 2 + sz) * 2 + sy) * Wo + 2 * x1 + sx] = v[n] * kHaar3;
     }
   }
   __syncthreads();
-  const int64_t plane = (int64_t)Do * Ho * Wo;
   float* obase = a.out + b * a.out_bstride;
+  if (CL) {
+    // item = (row r = (sz, sy), position xo, channel cl), channels fastest
+    const int n = 4 * Wo * CB;
+    for (int item = threadIdx.x; item < n; item += blockDim.x) {
+      const int cl = item % CB, q = item / CB;
+      const int xo = q % Wo, r = q / Wo;
+      const int zo = 2 * z1 + (r >> 1), yo = 2 * y1 + (r & 1);
+      obase[(((int64_t)zo * Ho + yo) * Wo + xo) * a.ldo + c0 + cl] = lds_out[q * (a.CB + 1) + cl];
+    }
+    return;
+  }
+  const int64_t plane = (int64_t)Do * Ho * Wo;
   const int nrows = CB * 4;
   for (int item = threadIdx.x; item < nrows * Wo; item += blockDim.x) {
     const int xo = item % Wo, r = item / Wo;
@@ -231,10 +250,10 @@ extern "C" int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float*
   return dispatch_gv(C / 4, go);
 }
 
-extern "C" int wf_idwt3d_haar(const float* ll, int64_t ll_bstride, const float* const* det,
-                              const int64_t* det_s, int levels, float* out, int64_t out_bstride,
-                              int64_t B, int64_t C, int64_t d, int64_t h, int64_t w,
-                              void* stream) {
+static int idwt_launch(const float* ll, int64_t ll_bstride, int64_t ll_cs, int64_t ll_ps,
+                       const float* const* det, const int64_t* det_s, int levels, float* out,
+                       int64_t out_bstride, int64_t ldo, int64_t B, int64_t C, int64_t d,
+                       int64_t h, int64_t w, void* stream) {
   WF_REQUIRE(levels >= 1 && levels <= kMaxLevels, "levels must be in [1, 4]");
   WF_REQUIRE(B >= 1 && C >= 1 && d >= 1 && h >= 1 && w >= 1, "empty tensor");
   WF_REQUIRE_PTR(ll);
@@ -244,6 +263,8 @@ extern "C" int wf_idwt3d_haar(const float* ll, int64_t ll_bstride, const float* 
   IdwtArgs a{};
   a.ll = ll;
   a.ll_bstride = ll_bstride;
+  a.ll_cs = ll_cs;
+  a.ll_ps = ll_ps;
   for (int i = 0; i < levels * 7; ++i) {
     WF_REQUIRE_PTR(det[i]);
     a.det[i] = det[i];
@@ -257,15 +278,39 @@ extern "C" int wf_idwt3d_haar(const float* ll, int64_t ll_bstride, const float* 
   a.d = (int)d;
   a.h = (int)h;
   a.w = (int)w;
+  a.ldo = ldo;
+  const bool cl = ldo > 0;
   const int64_t w1 = w << (levels - 1), h1 = h << (levels - 1), d1 = d << (levels - 1);
   WF_REQUIRE(w1 <= 4096, "row too long");
-  // LDS budget 48 KB: CB * 8 * w1 floats
-  int64_t cb = (48 * 1024 / 4) / (8 * w1);
+  // LDS budget 48 KB: CB * 8 * w1 floats (+ 8 * w1 of padding in the channel-last image)
+  int64_t cb = (48 * 1024 / 4) / (8 * w1) - (cl ? 1 : 0);
   if (cb < 1) cb = 1;
   if (cb > C) cb = C;
   a.CB = (int)cb;
-  const size_t lds = (size_t)cb * 8 * w1 * sizeof(float);
+  const size_t lds = (size_t)(cb + (cl ? 1 : 0)) * 8 * w1 * sizeof(float);
   dim3 grid((unsigned)(B * d1 * h1), (unsigned)cdiv(C, cb));
-  hipLaunchKernelGGL(idwt3d_haar_kernel, grid, dim3(256), lds, (hipStream_t)stream, a);
+  if (cl)
+    hipLaunchKernelGGL(idwt3d_haar_kernel<true>, grid, dim3(256), lds, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(idwt3d_haar_kernel<false>, grid, dim3(256), lds, (hipStream_t)stream, a);
   return check_launch("wf_idwt3d_haar");
+}
+
+extern "C" int wf_idwt3d_haar(const float* ll, int64_t ll_bstride, const float* const* det,
+                              const int64_t* det_s, int levels, float* out, int64_t out_bstride,
+                              int64_t B, int64_t C, int64_t d, int64_t h, int64_t w,
+                              void* stream) {
+  return idwt_launch(ll, ll_bstride, d * h * w, 1, det, det_s, levels, out, out_bstride, 0, B,
+                     C, d, h, w, stream);
+}
+
+extern "C" int wf_idwt3d_haar_cl(const float* ll, int64_t ll_bstride, int64_t ll_cstride,
+                                 int64_t ll_pstride, const float* const* det,
+                                 const int64_t* det_s, int levels, float* out,
+                                 int64_t out_bstride, int64_t ldo, int64_t B, int64_t C,
+                                 int64_t d, int64_t h, int64_t w, void* stream) {
+  WF_REQUIRE(ldo >= C, "channel-last output: ldo must be >= C");
+  WF_REQUIRE(ll_cstride >= 1 && ll_pstride >= 1, "LL strides must be positive");
+  return idwt_launch(ll, ll_bstride, ll_cstride, ll_pstride, det, det_s, levels, out,
+                     out_bstride, ldo, B, C, d, h, w, stream);
 }

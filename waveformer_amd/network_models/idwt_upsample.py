@@ -110,7 +110,10 @@ class UnetrIDWTBlock(nn.Module):
                 t.requires_grad for d in hf_coeffs for t in d.values())):
             out = wfa.idwt3d_haar(inp, hf_coeffs)
             return self.conv_block(torch.cat((out, skip), dim=1))
-        buf = torch.empty((B, C + skip.shape[1]) + size, dtype=inp.dtype, device=inp.device)
+        # channel-last: the layout the conv_block's kernels read, so neither the IDWT output nor
+        # the concatenation is converted again (round 2 built it NCDHW: two full-resolution
+        # layout copies per decoder level)
+        buf = ops.empty_cl(B, C + skip.shape[1], *size, inp.device)
         ops.idwt3d_haar(inp, hf_coeffs, out=buf)   # channels [0, C)
         buf[:, C:].copy_(skip)                      # torch.cat((out, skip), 1)
         return self.conv_block(buf)

@@ -356,7 +356,8 @@ def idwt3d_haar(ll: torch.Tensor, details: Sequence[Dict[str, torch.Tensor]],
     if ll.dtype != torch.float32:
         raise TypeError("idwt3d_haar: float32 only")
     B, C, d, h, w = ll.shape
-    if ll.stride()[1:] != (d * h * w, h * w, w, 1):
+    ll_ld = cl_ld(ll)  # a channel-last LL is read in place by the channel-last entry
+    if ll_ld is None and ll.stride()[1:] != (d * h * w, h * w, w, 1):
         ll = ll.contiguous()
     L = len(details)
     if not 1 <= L <= 4:
@@ -388,17 +389,26 @@ def idwt3d_haar(ll: torch.Tensor, details: Sequence[Dict[str, torch.Tensor]],
         ptrs.extend(t.data_ptr() for t in ts)
         strides.extend(pats[0])
     Do, Ho, Wo = d * 2 ** L, h * 2 ** L, w * 2 ** L
+    ldo = None
     if out is None:
         out = torch.empty((B, C, Do, Ho, Wo), dtype=torch.float32, device=ll.device)
     else:
         if out.shape[0] != B or out.shape[1] < C or tuple(out.shape[2:]) != (Do, Ho, Wo):
             raise ValueError(f"idwt3d_haar: out {tuple(out.shape)} does not fit ({B},{C},{Do},{Ho},{Wo})")
-        if out.stride()[1:] != (Do * Ho * Wo, Ho * Wo, Wo, 1):
-            raise ValueError("idwt3d_haar: out must be contiguous inside each batch")
+        ldo = cl_ld(out)  # channel-last output (channels contiguous, positions ldo apart)
+        if ldo is None and out.stride()[1:] != (Do * Ho * Wo, Ho * Wo, Wo, 1):
+            raise ValueError("idwt3d_haar: out must be channel-last or contiguous inside each batch")
     arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
     sarr = (ctypes.c_int64 * len(strides))(*strides)
-    _lib.call("wf_idwt3d_haar", ll.data_ptr(), ll.stride(0), arr, sarr, L, out.data_ptr(),
-              out.stride(0), B, C, d, h, w, _stream())
+    if ll_ld is not None and ldo is None:
+        ll, ll_ld = ll.contiguous(), None  # the NCDHW-output entry reads an NCDHW LL
+    if ldo is not None:
+        ll_cs, ll_ps = (1, ll_ld) if ll_ld is not None else (d * h * w, 1)
+        _lib.call("wf_idwt3d_haar_cl", ll.data_ptr(), ll.stride(0), ll_cs, ll_ps, arr, sarr, L,
+                  out.data_ptr(), out.stride(0), ldo, B, C, d, h, w, _stream())
+    else:
+        _lib.call("wf_idwt3d_haar", ll.data_ptr(), ll.stride(0), arr, sarr, L, out.data_ptr(),
+                  out.stride(0), B, C, d, h, w, _stream())
     del keep
     return out
 
