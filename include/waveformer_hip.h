@@ -124,6 +124,29 @@ int wf_idwt3d_haar_cl(const float* ll, int64_t ll_bstride, int64_t ll_cstride,
                       int levels, float* out, int64_t out_bstride, int64_t ldo, int64_t B,
                       int64_t C, int64_t d, int64_t h, int64_t w, void* stream);
 
+/* ---- channel-last data movement of the decoder (ABI 12) ---------------------------- */
+/* dst[p*ldd + c] = src[p*lds + c] for P positions x C channels (C, lds, ldd multiples of 4,
+ * 16-byte aligned): a channel slice of one channels_last_3d tensor into another -- the
+ * torch.cat((out, skip), 1) of UnetrUpBlock / UnetrIDWTBlock (monai unetr_block.py:84,
+ * idwt_upsample.py:163) and network_backbone.py's torch.cat([up4, up3, dec2], 1).          */
+int wf_copy_cl(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t P, int64_t C,
+               void* stream);
+/* ConvTranspose3d(k = s = 2) output placement (monai unetr_block.py:73-80): g holds
+ * (B*d*h*w, 8*C) GEMM rows, column s*C + c with s = dz*4 + dy*2 + dx; each goes to channel c of
+ * position (b, 2z+dz, 2y+dy, 2x+dx) of the channel-last dst (positions ldd floats apart), plus
+ * bias[c] (bias may be NULL).                                                              */
+int wf_subvoxel_scatter_cl(const float* g, const float* bias, float* dst, int64_t ldd,
+                           int64_t B, int64_t C, int64_t d, int64_t h, int64_t w, void* stream);
+/* ConvTranspose3d(Cin, Cout, k = 2, s = 2) of the dense channel-last x (B, d, h, w, Cin) as one
+ * MFMA GEMM (positions x Cin) . (Cin x 8 Cout) whose epilogue stores each 4-channel group, +
+ * bias[c], straight to its sub-voxel of the channel-last out (positions ldo floats apart): the
+ * transposed conv of UnetrUpBlock (monai unetr_block.py:73-80) without the (8 Cout)-wide
+ * intermediate.  w_bf16x2: [2][8 Cout][Cin] 16-bit planes of weight.permute(2, 3, 4, 1, 0)
+ * (row s * Cout + c).  Cin % 8 == 0, Cout % 4 == 0, ldo % 4 == 0.                           */
+int wf_convtranspose2_cl(const float* x, const uint16_t* w_bf16x2, const float* bias, float* out,
+                         int64_t ldo, int64_t B, int64_t Cin, int64_t Cout, int64_t d, int64_t h,
+                         int64_t w, int precision, void* stream);
+
 /* ---- C5: general wavelets (db1..db4), NCDHW, any sizes ------------------------------- */
 /* One analysis level of ptwt.wavedec3(x, wavelet, mode='zero') (wave_helper.py:350 with a
  * wavelet other than 'db1'; BASELINE config 5 "db2 3-level DWT").  dec_lo / dec_hi are HOST

@@ -294,3 +294,81 @@ def test_norm_act_autograd_vs_torch(mode, B, C_, S):
     assert C.rel_l2(ac.grad, ad.grad) <= 1e-5
     if mode:
         assert C.rel_l2(rc.grad, rd.grad) <= 1e-5
+
+
+def test_channel_last_copy_cat_and_subvoxel_scatter():
+    """layout.hip: wf_copy_cl (channel slices of channels_last_3d tensors), ops.cat_cl (mixed
+    layouts) and wf_subvoxel_scatter_cl (ConvTranspose3d k = s = 2 placement + bias) against
+    the torch ops they replace, bit for bit."""
+    from waveformer_amd import ops
+    cl = torch.channels_last_3d
+    a = seeded_randn((2, 8, 5, 6, 7), 41).cuda().contiguous(memory_format=cl)
+    b = seeded_randn((2, 12, 5, 6, 7), 42).cuda().contiguous(memory_format=cl)
+    c = seeded_randn((2, 4, 5, 6, 7), 43).cuda()  # NCDHW: the torch-copy fallback
+    got = ops.cat_cl([a, b, c])
+    assert got.is_contiguous(memory_format=cl)
+    assert torch.equal(got, torch.cat([a, b, c], 1))
+    buf = torch.full((2, 20, 5, 6, 7), 3.0, device="cuda").contiguous(memory_format=cl)
+    ops.copy_cl(b, buf[:, 4:16])
+    assert torch.equal(buf[:, 4:16], b) and torch.all(buf[:, :4] == 3) and torch.all(buf[:, 16:] == 3)
+    # transposed conv k = s = 2 as rows @ W, scattered into the first Cout channels
+    B, Cin, Cout, d, h, w = 2, 16, 12, 3, 4, 5
+    x = seeded_randn((B, Cin, d, h, w), 44).cuda()
+    tc = torch.nn.ConvTranspose3d(Cin, Cout, 2, 2).cuda()
+    with torch.no_grad():
+        tc.bias.copy_(seeded_randn((Cout,), 45).cuda())
+        want = tc(x)
+    rows = x.permute(0, 2, 3, 4, 1).reshape(-1, Cin)
+    g = rows @ tc.weight.detach().permute(0, 2, 3, 4, 1).reshape(Cin, 8 * Cout)
+    dst = torch.full((B, Cout + 4, 2 * d, 2 * h, 2 * w), 5.0, device="cuda").contiguous(memory_format=cl)
+    ops.subvoxel_scatter_cl(g, tc.bias.detach(), dst)
+    assert C.rel_l2(dst[:, :Cout], want) <= 1e-5
+    assert torch.all(dst[:, Cout:] == 5.0)
+
+
+@pytest.mark.parametrize("B,Cin,Cout,d,h,w", [(2, 16, 12, 3, 4, 5), (1, 144, 48, 6, 6, 6),
+                                              (2, 8, 4, 1, 1, 3), (1, 96, 48, 5, 7, 9)])
+def test_convtranspose2_gemm_subvoxel_epilogue(B, Cin, Cout, d, h, w):
+    """wf_convtranspose2_cl: ConvTranspose3d(k = s = 2) as one streaming MFMA GEMM whose
+    epilogue stores the sub-voxels + bias into a channel slice of a wider channel-last buffer,
+    against torch's fp32 transposed conv (bf16x3 operands: fp32-faithful, rel-L2 <= 1e-5);
+    ragged row counts (M % 16 != 0) and one- and multi-chunk column splits included."""
+    from waveformer_amd import ops
+    cl = torch.channels_last_3d
+    x = seeded_randn((B, Cin, d, h, w), 51).cuda()
+    tc = torch.nn.ConvTranspose3d(Cin, Cout, 2, 2).cuda()
+    with torch.no_grad():
+        tc.weight.copy_(seeded_randn(tuple(tc.weight.shape), 52).cuda() * 0.1)
+        tc.bias.copy_(seeded_randn((Cout,), 53).cuda())
+        want = tc(x)
+    dst = torch.full((B, Cout + 8, 2 * d, 2 * h, 2 * w), 5.0, device="cuda").contiguous(memory_format=cl)
+    ops.convtranspose2_cl(x, tc.weight.detach(), tc.bias.detach(), dst)
+    assert C.rel_l2(dst[:, :Cout], want) <= 1e-5
+    assert torch.all(dst[:, Cout:] == 5.0)
+    dst2 = ops.empty_cl(B, Cout, 2 * d, 2 * h, 2 * w, x.device)  # dense, no bias, cl input
+    ops.convtranspose2_cl(x.contiguous(memory_format=cl), tc.weight.detach(), None, dst2)
+    assert C.rel_l2(dst2 + tc.bias.detach().view(1, -1, 1, 1, 1), want) <= 1e-5
+
+
+def test_unetr_up_block_skip_in_place():
+    """UnetrUpBlock's fast path with the skip produced into its concat buffer (ops.cl_parent,
+    as the backbone's encoder1 does) and with a free-standing skip: the same result as the
+    reference composition torch.cat((ConvTranspose3d(x), skip), 1) -> conv block."""
+    from waveformer_amd import ops
+    from waveformer_amd.blocks import UnetrUpBlock
+    torch.manual_seed(0)
+    blk = UnetrUpBlock(3, 24, 8, 3, 2, "instance", res_block=True).cuda().eval()
+    x = seeded_randn((1, 24, 4, 4, 4), 61).cuda()
+    skip = seeded_randn((1, 8, 8, 8, 8), 62).cuda()
+    buf = ops.empty_cl(1, 16, 8, 8, 8, x.device)
+    buf[:, 8:].copy_(skip)
+    view = buf[:, 8:]
+    assert ops.cl_parent(view, 8) is buf or ops.cl_parent(view, 8).data_ptr() == buf.data_ptr()
+    with torch.no_grad():
+        got_inplace = blk(x, view)
+        got_free = blk(x, skip)
+        tc = blk.transp_conv.conv
+        ref_in = torch.cat((tc(x), skip), 1)
+        want = blk.conv_block(ref_in)
+    assert C.rel_l2(got_free, want) <= 1e-5
+    assert C.rel_l2(got_inplace, want) <= 1e-5

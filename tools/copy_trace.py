@@ -26,7 +26,7 @@ names = ("aten::copy_", "aten::contiguous", "aten::cat", "aten::clone", "aten::a
 rows = []
 for e in prof.events():
     if e.name in names and e.device_type.name == "CPU":
-        t = sum(k.device_time for k in e.kernels) if hasattr(e, "kernels") else 0
+        t = getattr(e, "device_time_total", 0) or getattr(e, "cuda_time_total", 0)
         st = [s for s in (e.stack or []) if "waveformer_amd" in s][:3]
         rows.append((t, e.name, str(e.input_shapes)[:90], " <- ".join(st)[:260]))
 rows.sort(key=lambda r: -r[0])

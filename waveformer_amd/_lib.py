@@ -36,6 +36,9 @@ SIGNATURES = {
     "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar_cl": (_I, [_P, _I64, _I64, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64,
                                _I64, _I64, _I64, _P]),
+    "wf_copy_cl": (_I, [_P, _I64, _P, _I64, _I64, _I64, _P]),
+    "wf_subvoxel_scatter_cl": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_convtranspose2_cl": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
     "wf_dwt3d_fwd": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _I, _P]),
     "wf_idwt3d_level": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P, _P, _I, _P, _I64, _I64,
                              _P]),

@@ -13,7 +13,7 @@ activation LeakyReLU(0.01), as Waveformer builds them.
 """
 from __future__ import annotations
 
-from typing import Sequence, Tuple, Union
+from typing import Optional, Sequence, Tuple, Union
 
 import torch
 import torch.nn as nn
@@ -98,6 +98,10 @@ def get_conv_layer(spatial_dims: int, in_channels: int, out_channels: int,
     return Convolution(in_channels, out_channels, kernel_size, stride, pad, bias, is_transposed, op)
 
 
+def _into(y: torch.Tensor, out: Optional[torch.Tensor]) -> torch.Tensor:
+    return y if out is None else out.copy_(y)
+
+
 class UnetResBlock(nn.Module):
     """conv3-norm-lrelu-conv3-norm (+ 1x1 conv + norm residual when channels change) -> lrelu
     (monai dynunet_block.py:25-111)."""
@@ -127,7 +131,9 @@ class UnetResBlock(nn.Module):
                 and (c3 is None or (type(c3) is nn.Conv3d and c3.kernel_size == (1, 1, 1)
                                     and c3.stride == (1, 1, 1) and _in_ok(self.norm3))))
 
-    def forward(self, inp):
+    def forward(self, inp, out=None):
+        """out: optional channel-last destination (e.g. a channel slice of a decoder's concat
+        buffer) the result is written into and returned as."""
         if self._fast(inp):
             slope = self.lrelu.negative_slope
             x = ops.to_cl(inp)
@@ -135,14 +141,18 @@ class UnetResBlock(nn.Module):
                 h, s1 = ops.conv3d_k3(x, self.conv1.conv.weight, self.conv1.conv.bias,
                                       norm_eps=self.norm1.eps)
             ops.norm_act(h, s1, slope=slope, out=h)
-            out, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
-                                    norm_eps=self.norm2.eps)
+            y, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
+                                  norm_eps=self.norm2.eps)
+            dst = y if out is None else out
             if self.downsample:
                 c3 = self.conv3.conv
                 res = ops.conv1x1_cl(x, c3.weight, c3.bias)
-                return ops.norm_act(out, s2, res, ops.instnorm_stats(res, self.norm3.eps),
-                                    slope=slope, out=out)
-            return ops.norm_act(out, s2, x, slope=slope, out=out)
+                return ops.norm_act(y, s2, res, ops.instnorm_stats(res, self.norm3.eps),
+                                    slope=slope, out=dst)
+            return ops.norm_act(y, s2, x, slope=slope, out=dst)
+        return _into(self._forward_slow(inp), out)
+
+    def _forward_slow(self, inp):
         if self._train_ok(inp):
             # training on the GPU: convolutions through wfa.conv_train, each InstanceNorm +
             # residual + LeakyReLU as one fused HIP op with a HIP backward (wfa.NormActFn)
@@ -180,7 +190,7 @@ class UnetBasicBlock(nn.Module):
         self.norm1 = _norm(norm_name, out_channels)
         self.norm2 = _norm(norm_name, out_channels)
 
-    def forward(self, inp):
+    def forward(self, inp, out=None):
         if (_fast_ok(inp, self) and _k3_ok(self.conv1.conv, inp.shape[1])
                 and _k3_ok(self.conv2.conv, self.conv2.conv.in_channels)
                 and _in_ok(self.norm1) and _in_ok(self.norm2)):
@@ -189,9 +199,12 @@ class UnetBasicBlock(nn.Module):
                 h, s1 = ops.conv3d_k3(inp, self.conv1.conv.weight, self.conv1.conv.bias,
                                       norm_eps=self.norm1.eps)
             ops.norm_act(h, s1, slope=slope, out=h)
-            out, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
-                                    norm_eps=self.norm2.eps)
-            return ops.norm_act(out, s2, slope=slope, out=out)
+            y, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
+                                  norm_eps=self.norm2.eps)
+            return ops.norm_act(y, s2, slope=slope, out=y if out is None else out)
+        return _into(self._forward_slow(inp), out)
+
+    def _forward_slow(self, inp):
         if (inp.is_cuda and inp.dtype == torch.float32 and inp.dim() == 5
                 and self.conv1.conv.out_channels % 4 == 0 and _in_ok(self.norm1)
                 and _in_ok(self.norm2) and self.lrelu.negative_slope > 0):
@@ -222,8 +235,8 @@ class UnetrBasicBlock(nn.Module):
         cls = UnetResBlock if res_block else UnetBasicBlock
         self.layer = cls(spatial_dims, in_channels, out_channels, kernel_size, stride, norm_name)
 
-    def forward(self, inp):
-        return self.layer(inp)
+    def forward(self, inp, out=None):
+        return self.layer(inp, out=out)
 
 
 class UnetrUpBlock(nn.Module):
@@ -257,16 +270,35 @@ class UnetrUpBlock(nn.Module):
         Cout = tc.out_channels
         if tuple(skip.shape) != (B, skip.shape[1], 2 * d, 2 * h, 2 * w):
             raise ValueError(f"skip {tuple(skip.shape)} does not match the up-sampled input")
-        buf = ops.empty_cl(B, Cout + skip.shape[1], 2 * d, 2 * h, 2 * w, inp.device)
+        # a skip already produced into channels [Cout, ...) of a buffer (the backbone's
+        # encoder1 writes there) needs no copy
+        parent = ops.cl_parent(skip, Cout)
+        in_place = parent is not None and parent.shape[1] == Cout + skip.shape[1]
+        buf = parent if in_place else ops.empty_cl(B, Cout + skip.shape[1], 2 * d, 2 * h, 2 * w,
+                                                   inp.device)
+        if Cin % 8 == 0 and Cout % 4 == 0:
+            # one MFMA GEMM whose epilogue stores the sub-voxels + bias (wf_convtranspose2_cl)
+            ops.convtranspose2_cl(inp, tc.weight, tc.bias, buf)
+            if not in_place:
+                ops.copy_cl(skip, buf[:, Cout:])
+            return buf
         rows = ops.to_cl(inp).permute(0, 2, 3, 4, 1).reshape(-1, Cin)
         wr = tc.weight.permute(0, 2, 3, 4, 1).reshape(Cin, 8 * Cout)
         g = rows @ wr
+        if Cout % 4 == 0:
+            # sub-voxel scatter + bias in one HIP pass (layout.hip), skip copied channel-last
+            bias = tc.bias.detach().contiguous() if tc.bias is not None else None
+            ops.subvoxel_scatter_cl(g, bias, buf)
+            if not in_place:
+                ops.copy_cl(skip, buf[:, Cout:])
+            return buf
         if tc.bias is not None:
             g = g + tc.bias.repeat(8)
         dst = buf.permute(0, 2, 3, 4, 1)[..., :Cout]
         dst = dst.unflatten(3, (w, 2)).unflatten(2, (h, 2)).unflatten(1, (d, 2))
         dst.permute(0, 1, 3, 5, 2, 4, 6, 7).copy_(g.view(B, d, h, w, 2, 2, 2, Cout))
-        buf[:, Cout:].copy_(skip)
+        if not in_place:
+            buf[:, Cout:].copy_(skip)
         return buf
 
 

@@ -73,7 +73,8 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
   }
   for (int i = tid; i < NCOL; i += blockDim.x) {
     const int n = c0 + i;
-    ebias[i] = (g.bias && n < N) ? g.bias[n] : 0.f;
+    const int nb = EPI == EPI_SUBVOXEL ? n % (N >> 3) : n;  // sub-voxel columns share a bias
+    ebias[i] = (g.bias && n < N) ? g.bias[nb] : 0.f;
     const bool e = EPI == EPI_LN_GELU && n < N;
     elw[i] = e ? 0.5f * g.e_ln_w[n] : 0.f;  // half: the epilogue feeds gelu_half2
     elb[i] = e ? 0.5f * g.e_ln_b[n] : 0.f;
@@ -87,6 +88,19 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
   // current tile's last k step, so they are in flight through its epilogue
   int tile = blockIdx.x * nwaves + wid;
   int arow_c = min(tile * 16 + l15, M - 1);
+  // EPI_SUBVOXEL: position offset (dz, dy, dx) and channel of each of this lane's 4-column
+  // groups -- tile-invariant, so the column -> sub-voxel division runs once per kernel
+  int sv_off[NT], sv_col[NT];
+  if constexpr (EPI == EPI_SUBVOXEL) {
+    const int Cs = N >> 3, W2 = 2 * g.mW, H2 = 2 * g.mH;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = c0 + t * 16 + 4 * g4;
+      const int s = col / Cs;
+      sv_col[t] = col - s * Cs;
+      sv_off[t] = ((s >> 2) * H2 + ((s >> 1) & 1)) * W2 + (s & 1);
+    }
+  }
   RowMapper<MAP> rm(g, arow_c);
   // LN + GELU (CCF_FFN pwconv, K <= 64): BOTH k steps of the next tile are loaded at the top of
   // the current one, ahead of its epilogue stores.  vmcnt counts stores too and retires in
@@ -243,6 +257,16 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] += *reinterpret_cast<const f32x4*>(ebias + t * 16 + 4 * g4);
     float rm_ = 0.f, rs_ = 1.f, bs = 1.f;
+    int64_t sv_p0 = 0;  // EPI_SUBVOXEL: output position of sub-voxel (0, 0, 0) of this row
+    if (EPI == EPI_SUBVOXEL) {
+      int r = rowc;
+      const int x = r % g.mW;
+      r /= g.mW;
+      const int y = r % g.mH;
+      r /= g.mH;
+      const int z = r % g.mD, b = r / g.mD;
+      sv_p0 = (((int64_t)b * 2 * g.mD + 2 * z) * (2 * g.mH) + 2 * y) * (2 * g.mW) + 2 * x;
+    }
     if (EPI == EPI_LN_GELU) {  // full row in this wave (NCOL == N): the 4 lanes of a position
       // moments on packed pairs straight off the accumulator registers (v_pk_add / v_pk_fma
       // on .xy / .zw: no repacking moves, half the instructions of per-element scalar code)
@@ -318,6 +342,10 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), orsrc,
                                                  (int)((row * g.ldo + col) * 4), 0, 0);
         }
+      } else if (EPI == EPI_SUBVOXEL) {
+        if (rv)
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(g.out) +
+                                    (sv_p0 + sv_off[t]) * g.ldo + sv_col[t]) = v;
       } else if (rv && cv) {
         if (obf) {
           bf16x4 o;
@@ -397,16 +425,21 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
   if (g.epi == EPI_LN_GELU && (g.K > 64 || out_bytes >= ((int64_t)1 << 31) || (g.a_ln != LN_GIVEN && g.a_ln != LN_NONE) || g.a_gelu ||
                                (g.out_bf16 != 0) != (g.prec == PREC_BF16 || g.a_bf16 != 0)))
     return 0;
+  if (g.epi == EPI_SUBVOXEL && (g.out_bf16 || (g.N / 8) % 4 != 0 || g.a_map != MAP_IDENTITY))
+    return 0;
   const bool split = g.prec == PREC_SPLIT;
   const int K32 = (g.K + 31) & ~31;
   const size_t per_col = (size_t)(split ? 2 : 1) * (K32 + 8) * 2;
   const int tiles = g.N / 16;
   static const int cand[] = {12, 9, 8, 6, 4, 3, 2, 1};
+  // the transposed conv's N = 8 Cout is wide: one workgroup per CU holding half the columns
+  // reads A twice instead of six times at 64 KB
+  const size_t wbudget = g.epi == EPI_SUBVOXEL ? 136 * 1024 : 64 * 1024;
   int nt = 0;
   for (int c : cand) {
     if (tiles % c != 0) continue;
     if (g.epi == EPI_LN_GELU && c != tiles) continue;  // LayerNorm needs the full row
-    if ((size_t)c * 16 * per_col <= 64 * 1024) {
+    if ((size_t)c * 16 * per_col <= wbudget) {
       nt = c;
       break;
     }
@@ -428,6 +461,7 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
   else if (g.a_map == MAP_MERGE) dispatch_nt<MAP_MERGE, EPI_STORE>(nt, g, grid, lds, s);
   else if (g.epi == EPI_LN_GELU) dispatch_nt<MAP_IDENTITY, EPI_LN_GELU>(nt, g, grid, lds, s);
   else if (g.epi == EPI_RESID) dispatch_nt<MAP_IDENTITY, EPI_RESID>(nt, g, grid, lds, s);
+  else if (g.epi == EPI_SUBVOXEL) dispatch_nt<MAP_IDENTITY, EPI_SUBVOXEL>(nt, g, grid, lds, s);
   else dispatch_nt<MAP_IDENTITY, EPI_STORE>(nt, g, grid, lds, s);
   return 1;
 }

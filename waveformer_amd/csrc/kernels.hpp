@@ -54,7 +54,10 @@ enum RowMap { MAP_IDENTITY = 0, MAP_WINDOW = 1, MAP_MERGE = 2 };
 // LN_PARTIAL: a_stats holds a_np (mean, M2) pairs per row, each over K / a_np consecutive
 // columns (written by the producing kernel); the loader combines them (Chan et al.).
 enum LnMode { LN_NONE = 0, LN_GIVEN = 1, LN_COMPUTE = 2, LN_PARTIAL = 3 };
-enum EpiMode { EPI_STORE = 0, EPI_LN_GELU = 1, EPI_RESID = 2 };
+// EPI_SUBVOXEL: ConvTranspose3d(k = s = 2) -- row m = position (b, z, y, x) of a (B, d, h, w)
+// raster (mB..mW), column s * (N / 8) + c stored + bias at channel c of output position
+// (b, 2z + dz, 2y + dy, 2x + dx), s = dz * 4 + dy * 2 + dx, rows ldo floats apart
+enum EpiMode { EPI_STORE = 0, EPI_LN_GELU = 1, EPI_RESID = 2, EPI_SUBVOXEL = 3 };
 
 struct GemmArgs {
   int prec;              // Prec

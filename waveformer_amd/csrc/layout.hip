@@ -1,0 +1,114 @@
+// layout.hip -- data movement of the decoder's channel-last buffers (config 3 / 5 inference).
+//
+// The decoder keeps its activations channel-last (channels_last_3d: the channels of one
+// position contiguous, positions `ld` floats apart).  Two moves the PyTorch layer left to
+// generic copy kernels (strided, 4-byte elements; profiled in one 192^3 config-5 forward,
+// tools/copy_trace.py):
+//   * torch.cat((out, skip), 1) / torch.cat([up4, up3, dec2], 1): channel slices of one
+//     channel-last tensor into another -- wf_copy_cl, one float4 per lane (1.16 ms for the
+//     2 x 48 x 192^3 skip copy of decoder1);
+//   * ConvTranspose3d(k = s = 2) as a GEMM (positions x Cin) . (Cin x 8 Cout) whose columns
+//     are the 8 sub-voxels (monai unetr_block.py:73-80 via blocks.UnetrUpBlock): the GEMM rows
+//     scattered into the 2 x 2 x 2 children of each position, + bias -- wf_subvoxel_scatter_cl
+//     (1.35 ms as a permuted copy_, plus a separate bias add).
+// Both are HBM-bound: 8 bytes of traffic per float moved.
+#include "kernels.hpp"
+
+namespace wf {
+
+// n / d for 0 <= n < 2^31 by a multiply-high and a shift (Granlund-Montgomery round-up
+// method, multiplier and shift made on the host): a 64-bit division per element made these
+// copies VALU-bound (the sub-voxel scatter ran at 1.1 TB/s)
+struct FastDiv {
+  uint32_t d, m, s;
+  explicit FastDiv(uint32_t dv = 1) : d(dv), m(1), s(0) {
+    while ((1ull << s) < dv) ++s;
+    m = (uint32_t)((((1ull << 32) * ((1ull << s) - dv)) / dv) + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return (__umulhi(n, m) + n) >> s;
+  }
+};
+
+__global__ __launch_bounds__(256) void copy_cl_kernel(const float* __restrict__ src, int64_t lds,
+                                                      float* __restrict__ dst, int64_t ldd,
+                                                      FastDiv c4d, uint32_t total) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    const uint32_t p = c4d.div(i);
+    const uint32_t c = (i - p * c4d.d) * 4;
+    *reinterpret_cast<f32x4*>(dst + (int64_t)p * ldd + c) =
+        *reinterpret_cast<const f32x4*>(src + (int64_t)p * lds + c);
+  }
+}
+
+// g: (B*d*h*w, 8*C) rows, column s*C + c with s = dz*4 + dy*2 + dx (g.view(B,d,h,w,2,2,2,C));
+// dst: channel-last (B, C, 2d, 2h, 2w) positions ldd floats apart
+__global__ __launch_bounds__(256) void subvoxel_scatter_cl_kernel(
+    const float* __restrict__ g, const float* __restrict__ bias, float* __restrict__ dst,
+    int64_t ldd, FastDiv c4d, FastDiv wd, FastDiv hd, FastDiv dd, uint32_t total) {
+  const uint32_t C = 4 * c4d.d, w = wd.d, h = hd.d, d = dd.d;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += gridDim.x * blockDim.x) {
+    // i = ((row * 8 + s) * C4 + c4): consecutive lanes read consecutive 16 B of a g row
+    const uint32_t rs = c4d.div(i);
+    const uint32_t c = (i - rs * c4d.d) * 4;
+    const uint32_t sv = rs & 7, r0 = rs >> 3;
+    const uint32_t r1 = wd.div(r0), x = r0 - r1 * w;
+    const uint32_t r2 = hd.div(r1), y = r1 - r2 * h;
+    const uint32_t b = dd.div(r2), z = r2 - b * d;
+    const uint32_t dz = sv >> 2, dy = (sv >> 1) & 1, dx = sv & 1;
+    f32x4 v = *reinterpret_cast<const f32x4*>(g + (int64_t)rs * C + c);
+    if (bias) v += *reinterpret_cast<const f32x4*>(bias + c);
+    const int64_t pos = (((int64_t)b * (2 * d) + 2 * z + dz) * (2 * h) + 2 * y + dy) * (2 * w) +
+                        2 * x + dx;
+    *reinterpret_cast<f32x4*>(dst + pos * ldd + c) = v;
+  }
+}
+
+static unsigned grid_for(int64_t total) {
+  int64_t blocks = cdiv(total, 256);
+  if (blocks > 65536) blocks = 65536;  // grid-stride beyond: ~256 workgroups per CU
+  return (unsigned)(blocks < 1 ? 1 : blocks);
+}
+
+}  // namespace wf
+
+using namespace wf;
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int wf_copy_cl(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t P,
+                          int64_t C, void* stream) {
+  WF_REQUIRE(P >= 0 && C >= 4 && C % 4 == 0, "C must be a positive multiple of 4");
+  WF_REQUIRE(lds >= C && ldd >= C && lds % 4 == 0 && ldd % 4 == 0,
+             "position strides must be >= C and multiples of 4");
+  WF_REQUIRE_PTR(src);
+  WF_REQUIRE_PTR(dst);
+  WF_REQUIRE(aligned16(src) && aligned16(dst), "src / dst must be 16-byte aligned");
+  if (P == 0) return WF_OK;
+  const int64_t total = P * (C / 4);
+  WF_REQUIRE(total < ((int64_t)1 << 31), "wf_copy_cl: more than 2^31 float4 items");
+  hipLaunchKernelGGL(copy_cl_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                     src, lds, dst, ldd, FastDiv((uint32_t)(C / 4)), (uint32_t)total);
+  return check_launch("wf_copy_cl");
+}
+
+extern "C" int wf_subvoxel_scatter_cl(const float* g, const float* bias, float* dst, int64_t ldd,
+                                      int64_t B, int64_t C, int64_t d, int64_t h, int64_t w,
+                                      void* stream) {
+  WF_REQUIRE(B >= 1 && d >= 1 && h >= 1 && w >= 1, "empty tensor");
+  WF_REQUIRE(C >= 4 && C % 4 == 0 && ldd >= C && ldd % 4 == 0,
+             "C must be a positive multiple of 4, ldd >= C a multiple of 4");
+  WF_REQUIRE_PTR(g);
+  WF_REQUIRE_PTR(dst);
+  WF_REQUIRE(aligned16(g) && aligned16(dst) && (!bias || aligned16(bias)),
+             "g / dst / bias must be 16-byte aligned");
+  const int64_t total = B * d * h * w * 8 * (C / 4);
+  WF_REQUIRE(total < ((int64_t)1 << 31), "wf_subvoxel_scatter_cl: more than 2^31 float4 items");
+  hipLaunchKernelGGL(subvoxel_scatter_cl_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, g, bias, dst, ldd, FastDiv((uint32_t)(C / 4)),
+                     FastDiv((uint32_t)w), FastDiv((uint32_t)h), FastDiv((uint32_t)d),
+                     (uint32_t)total);
+  return check_launch("wf_subvoxel_scatter_cl");
+}

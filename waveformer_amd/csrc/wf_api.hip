@@ -212,6 +212,44 @@ using namespace wf;
 // out[m, n] = bias[n] + sum_k act(x[m, k]) * W[n, k] over fp32 rows (act = GELU(erf) or
 // identity): the decoder's 1x1x1 convolutions of ProjectionUpsample on the MFMA GEMM family
 // (gemm_rows / gemm_kc / gemm_ares, bf16x3 or bf16 operands, fp32 accumulation).
+extern "C" int wf_convtranspose2_cl(const float* x, const uint16_t* w_bf16x2, const float* bias,
+                                    float* out, int64_t ldo, int64_t B, int64_t Cin, int64_t Cout,
+                                    int64_t d, int64_t h, int64_t w, int precision, void* stream) {
+  WF_REQUIRE(B >= 1 && d >= 1 && h >= 1 && w >= 1, "empty tensor");
+  WF_REQUIRE(Cin >= 8 && Cin % 8 == 0 && Cout >= 4 && Cout % 4 == 0,
+             "need Cin a multiple of 8 and Cout a multiple of 4");
+  WF_REQUIRE(ldo >= Cout && ldo % 4 == 0, "ldo must be >= Cout and a multiple of 4");
+  WF_REQUIRE(valid_prec(precision), "unknown precision");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(w_bf16x2);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0,
+             "x / out must be 16-byte aligned");
+  WF_REQUIRE(B * d * h * w < ((int64_t)1 << 31) && 8 * Cout <= 4096, "shape too large");
+  GemmArgs g{};
+  g.prec = precision;
+  g.a_src = x;
+  g.a_C = (int)Cin;
+  g.a_nseg = 1;
+  g.a_map = MAP_IDENTITY;
+  g.a_ln = LN_NONE;
+  g.mB = (int)B;
+  g.mD = (int)d;
+  g.mH = (int)h;
+  g.mW = (int)w;
+  g.w = w_bf16x2;
+  g.M = B * d * h * w;
+  g.N = (int)(8 * Cout);
+  g.K = (int)Cin;
+  g.epi = EPI_SUBVOXEL;
+  g.bias = bias;
+  g.out = out;
+  g.ldo = ldo;
+  if (!try_launch_gemm_rows(g, (hipStream_t)stream, false))
+    return fail(WF_E_SHAPE, "wf_convtranspose2_cl: shape not covered by the streaming GEMM");
+  return check_launch("wf_convtranspose2_cl");
+}
+
 extern "C" int wf_linear_fwd(const float* x, const uint16_t* w_bf16x2, const float* bias,
                              float* out, int64_t M, int64_t K, int64_t N, int gelu_in,
                              int precision, void* stream) {

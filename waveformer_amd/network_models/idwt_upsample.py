@@ -115,5 +115,5 @@ class UnetrIDWTBlock(nn.Module):
         # layout copies per decoder level)
         buf = ops.empty_cl(B, C + skip.shape[1], *size, inp.device)
         ops.idwt3d_haar(inp, hf_coeffs, out=buf)   # channels [0, C)
-        buf[:, C:].copy_(skip)                      # torch.cat((out, skip), 1)
+        ops.copy_cl(skip, buf[:, C:])               # torch.cat((out, skip), 1)
         return self.conv_block(buf)

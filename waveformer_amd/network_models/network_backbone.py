@@ -158,7 +158,16 @@ class Waveformer(nn.Module):
 
     def _forward(self, x_in: torch.Tensor) -> torch.Tensor:
         outs, outs_hf = self.waveformer_encoder(x_in)
-        enc0 = self.encoder1(x_in)
+        fs0 = self.decoder1.transp_conv.conv.out_channels
+        if x_in.is_cuda and not torch.is_grad_enabled():
+            # inference: encoder1 writes straight into channels [fs0, 2 fs0) of decoder1's
+            # channel-last concat buffer (blocks.UnetrUpBlock finds it there, no skip copy)
+            B, _, D, H, W = x_in.shape
+            buf1 = ops.empty_cl(B, fs0 + self.encoder1.layer.conv1.conv.out_channels, D, H, W,
+                                x_in.device)
+            enc0 = self.encoder1(x_in, out=buf1[:, fs0:])
+        else:
+            enc0 = self.encoder1(x_in)
         enc1 = self.encoder2(outs[0])
         enc2 = self.encoder3(outs[1])
         enc3 = self.encoder4(outs[2])
@@ -168,7 +177,11 @@ class Waveformer(nn.Module):
         dec2 = self.decoder2(dec5, enc1, outs_hf[-3])
         up4 = self.learnable_up4(dec4)
         up3 = self.learnable_up3(dec3)
-        dec1 = self.decoder1(torch.cat([up4, up3, dec2], dim=1), enc0)
+        if torch.is_grad_enabled() and any(t.requires_grad for t in (up4, up3, dec2)):
+            cat = torch.cat([up4, up3, dec2], dim=1)
+        else:  # inference: one channel-last buffer, the layout decoder1's kernels read
+            cat = ops.cat_cl([up4, up3, dec2])
+        dec1 = self.decoder1(cat, enc0)
         # the HIP decoder path is channel-last; hand the caller the reference's NCDHW layout
         return self.out(dec1).contiguous()
 

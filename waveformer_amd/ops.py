@@ -612,6 +612,97 @@ def to_cl(x: torch.Tensor) -> torch.Tensor:
     return x if cl_ld(x) is not None else x.contiguous(memory_format=torch.channels_last_3d)
 
 
+def _cl_ok(t: torch.Tensor) -> bool:
+    return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 5 and t.shape[1] % 4 == 0
+            and cl_ld(t) is not None)
+
+
+def copy_cl(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """dst.copy_(src) for two NCDHW-shaped channel-last tensors of one shape (channel slices of
+    wider buffers allowed) on wf_copy_cl; other layouts take torch's copy."""
+    if tuple(src.shape) != tuple(dst.shape):
+        raise ValueError(f"copy_cl: shapes {tuple(src.shape)} and {tuple(dst.shape)} differ")
+    if not (_cl_ok(src) and _cl_ok(dst)) or src.device != dst.device:
+        return dst.copy_(src)
+    B, C, D, H, W = src.shape
+    _lib.call("wf_copy_cl", src.data_ptr(), cl_ld(src), dst.data_ptr(), cl_ld(dst),
+              B * D * H * W, C, _stream())
+    return dst
+
+
+def cat_cl(tensors: Sequence[torch.Tensor]) -> torch.Tensor:
+    """torch.cat(tensors, 1) into a channels_last_3d result (the decoder's layout); inputs in
+    any layout (channel-last ones are moved by wf_copy_cl, the rest by torch)."""
+    t0 = tensors[0]
+    B, _, D, H, W = t0.shape
+    out = empty_cl(B, sum(t.shape[1] for t in tensors), D, H, W, t0.device)
+    c = 0
+    for t in tensors:
+        copy_cl(t, out[:, c:c + t.shape[1]])
+        c += t.shape[1]
+    return out
+
+
+def subvoxel_scatter_cl(g: torch.Tensor, bias: Optional[torch.Tensor], dst: torch.Tensor):
+    """ConvTranspose3d(k = s = 2) placement: g (B*d*h*w, 8*C) GEMM rows (column s*C + c, s = dz*4
+    + dy*2 + dx) into channels [0, C) of the channel-last dst (B, >=C, 2d, 2h, 2w), + bias."""
+    B, _, D2, H2, W2 = dst.shape
+    d, h, w = D2 // 2, H2 // 2, W2 // 2
+    C = g.shape[1] // 8
+    ldd = cl_ld(dst)
+    if ldd is None or not g.is_contiguous() or g.shape[0] != B * d * h * w or C % 4:
+        raise ValueError("subvoxel_scatter_cl: g must be contiguous (B*d*h*w, 8C), dst channel-last")
+    _lib.call("wf_subvoxel_scatter_cl", g.data_ptr(), 0 if bias is None else bias.data_ptr(),
+              dst.data_ptr(), ldd, B, C, d, h, w, _stream())
+    return dst
+
+
+def convtranspose2_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                      out: torch.Tensor) -> torch.Tensor:
+    """ConvTranspose3d(k = s = 2) of x (B, Cin, d, h, w) into channels [0, Cout) of the
+    channel-last out (B, >= Cout, 2d, 2h, 2w) on the streaming MFMA GEMM with the sub-voxel
+    store epilogue (wf_convtranspose2_cl).  bf16x3 operands: the fp32-faithful precision the
+    fp32 GEMM it replaces had, under every global precision."""
+    B, Cin, d, h, w = x.shape
+    if tuple(weight.shape) != (Cin, weight.shape[1], 2, 2, 2):
+        raise ValueError(f"convtranspose2_cl: weight {tuple(weight.shape)} does not fit Cin={Cin}")
+    Cout = weight.shape[1]
+    ldo = cl_ld(out)
+    if ldo is None or tuple(out.shape) != (B, out.shape[1], 2 * d, 2 * h, 2 * w) \
+            or out.shape[1] < Cout:
+        raise ValueError("convtranspose2_cl: out must be a channel-last (B, >=Cout, 2d, 2h, 2w)")
+    _check(x, "x", contiguous=False)
+    if cl_ld(x) != Cin:
+        x = x.contiguous(memory_format=torch.channels_last_3d)
+    if bias is not None:
+        _check(bias, "bias")
+
+    def make():
+        wt = weight.detach().permute(2, 3, 4, 1, 0).reshape(8 * Cout, Cin).contiguous()
+        wb = torch.empty((2, 8 * Cout, Cin), dtype=torch.bfloat16, device=wt.device)
+        _lib.call("wf_split_f32_to_bf16x2", wt.data_ptr(), wb.data_ptr(), wt.numel(), _stream())
+        return wb
+    wb = per_forward(("ct2", weight.data_ptr(), tuple(weight.shape)), make)
+    _lib.call("wf_convtranspose2_cl", x.data_ptr(), wb.data_ptr(), _ptr(bias), out.data_ptr(),
+              ldo, B, Cin, Cout, d, h, w, PRECISIONS["bf16x3"], _stream())
+    return out
+
+
+def cl_parent(t: torch.Tensor, c0: int) -> Optional[torch.Tensor]:
+    """The channel-last buffer t is the channel slice [c0, c0 + C) of (t._base[:, c0:c0 + C]),
+    or None: lets a producer write a decoder's skip features into its concat buffer."""
+    base = t._base
+    if base is None or base.dim() != 5 or cl_ld(base) != base.shape[1] or c0 < 0:
+        return None
+    if tuple(base.shape[2:]) != tuple(t.shape[2:]) or base.shape[0] != t.shape[0]:
+        return None
+    if c0 + t.shape[1] > base.shape[1] or cl_ld(t) != base.shape[1]:
+        return None
+    if t.data_ptr() != base.data_ptr() + c0 * base.element_size():
+        return None
+    return base
+
+
 def empty_cl(B: int, C: int, D: int, H: int, W: int, device) -> torch.Tensor:
     return torch.empty((B, C, D, H, W), dtype=torch.float32, device=device,
                        memory_format=torch.channels_last_3d)
