@@ -128,7 +128,7 @@ int wf_idwt3d_haar_cl(const float* ll, int64_t ll_bstride, int64_t ll_cstride,
 /* dst[p*ldd + c] = src[p*lds + c] for P positions x C channels (C, lds, ldd multiples of 4,
  * 16-byte aligned): a channel slice of one channels_last_3d tensor into another -- the
  * torch.cat((out, skip), 1) of UnetrUpBlock / UnetrIDWTBlock (monai unetr_block.py:84,
- * idwt_upsample.py:163) and network_backbone.py's torch.cat([up4, up3, dec2], 1).          */
+ * idwt_upsample.py:163) and network_backbone.py:404's torch.cat([..., dec2], 1).   */
 int wf_copy_cl(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t P, int64_t C,
                void* stream);
 /* ConvTranspose3d(k = s = 2) output placement (monai unetr_block.py:73-80): g holds
@@ -218,6 +218,19 @@ int wf_norm_act_cl(const float* a, int64_t lda, const float* stats_a, const floa
                    const float* stats_r, float* out, int64_t ldo, int64_t B, int64_t C, int64_t P,
                    float slope, void* stream);
 
+/* The norm3'ed 1x1 residual of UnetResBlock (monai dynunet_block.py:77-80, 104-108) for few
+ * input channels (K = Cin <= 7; encoder1: 4 -> 48) without materialising it: wf_moments_cl
+ * writes acc (B, K + K*K) fp64 = {sum_p x_k, sum_p x_k x_l} of the channel-last x (zeroed
+ * first); the host folds InstanceNorm's mean_r = W mean_x + b, var_r = W_c^T Cov_x W_c into
+ * per-sample wfold (B, C, K) = rstd_r W and bfold (B, C) = (b - mean_r) rstd_r, and
+ * wf_norm_act_lin_cl applies out = act((a - mean_a) rstd_a + wfold x + bfold).              */
+int wf_moments_cl(const float* x, int64_t ldx, int64_t B, int64_t K, int64_t P, double* acc,
+                  void* stream);
+int wf_norm_act_lin_cl(const float* a, int64_t lda, const float* stats_a, const float* x,
+                       int64_t ldx, int64_t K, const float* wfold, const float* bfold,
+                       float* out, int64_t ldo, int64_t B, int64_t C, int64_t P, float slope,
+                       void* stream);
+
 /* HFRefinementRes (network_models/idwt_upsample.py:12-50, config 5) over the 7 detail
  * tensors of one wavelet level: out_k = x_k * sigmoid(conv1x1(relu(IN_affine(dwconv3(x_k)))))
  * (sigmoid = 0: no sigmoid, hf_refinement.use_sigmoid False).  details: host array of 7
@@ -253,6 +266,15 @@ int wf_norm_act_bwd_cl(const float* dy, int64_t ldd, const float* y, int64_t ldy
 int wf_upsample_trilinear_cl(const float* in, float* out, int64_t B, int64_t C, int64_t d,
                              int64_t h, int64_t w, int64_t D, int64_t H, int64_t W,
                              int align_corners, void* stream);
+/* out += the same resampling (ProjectionUpsample's y + Up(res_conv(x)), wave_helper.py:81). */
+int wf_upsample_trilinear_add_cl(const float* in, float* out, int64_t B, int64_t C, int64_t d,
+                                 int64_t h, int64_t w, int64_t D, int64_t H, int64_t W,
+                                 int align_corners, void* stream);
+/* UnetOutBlock (monai dynunet_block.py:188-210, network_backbone.py:407): 1x1x1 conv of the
+ * channel-last x (B, P positions ldx floats apart, K channels) with weight (N, K) + bias (N)
+ * into the NCDHW out (B, N, P).  K % 4 == 0, K <= 120, N <= 16; fp32 FMAs.                  */
+int wf_conv1x1_head_cl(const float* x, int64_t ldx, const float* weight, const float* bias,
+                       float* out, int64_t B, int64_t K, int64_t N, int64_t P, void* stream);
 
 /* Predictor.predict_raw_probability (light_training/prediction.py:35-63): channel-first
  * (C, d, h, w) fp32 (channel stride ldc) -> (C, D, H, W) per channel

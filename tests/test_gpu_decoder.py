@@ -372,3 +372,70 @@ def test_unetr_up_block_skip_in_place():
         want = blk.conv_block(ref_in)
     assert C.rel_l2(got_free, want) <= 1e-5
     assert C.rel_l2(got_inplace, want) <= 1e-5
+
+
+def test_norm_act_linear_residual_fold():
+    """ops.norm_act_lin (wf_moments_cl + wf_norm_act_lin_cl): the norm3'ed 4 -> 48 1x1
+    residual of encoder1 folded into per-sample weights from x's fp64 moments, against the
+    materialised composition in fp64 (B = 2 samples with different means / scales, written into
+    a channel slice of a wider buffer); and UnetResBlock(4 -> 48) writing through `out=`."""
+    from waveformer_amd import ops
+    from waveformer_amd.blocks import UnetResBlock
+    B, K, Cc, S = 2, 4, 48, 10
+    x = seeded_randn((B, K, S, S, S), 71)
+    x[0] = x[0] * 3.0 + 1.5
+    x[1] = x[1] * 0.5 - 2.0
+    a = seeded_randn((B, Cc, S, S, S), 72)
+    w = seeded_randn((Cc, K, 1, 1, 1), 73) * 0.3
+    bias = seeded_randn((Cc,), 74)
+    xd, ad = x.double(), a.double()
+    r = F.conv3d(xd, w.double(), bias.double())
+    want = F.leaky_relu(F.instance_norm(ad, eps=1e-5) + F.instance_norm(r, eps=1e-5), 0.01)
+    cl = torch.channels_last_3d
+    ac = a.cuda().contiguous(memory_format=cl)
+    buf = torch.full((B, Cc + 8, S, S, S), 7.0, device="cuda").contiguous(memory_format=cl)
+    got = ops.norm_act_lin(ac, ops.instnorm_stats(ac, 1e-5), x.cuda(), w.cuda(), bias.cuda(),
+                           1e-5, slope=0.01, out=buf[:, 8:])
+    assert got.data_ptr() == buf[:, 8:].data_ptr()
+    assert C.rel_l2(got.double().cpu(), want) <= 2e-6
+    assert torch.all(buf[:, :8] == 7.0)
+    torch.manual_seed(0)
+    blk = UnetResBlock(3, K, Cc, 3, 1, "instance").cuda().eval()
+    with torch.no_grad():
+        free = blk(x.cuda())
+        into = blk(x.cuda(), out=buf[:, 8:])
+    assert into.data_ptr() == buf[:, 8:].data_ptr()
+    # the conv epilogue's InstanceNorm sums are fp64 atomics: last-bit run-to-run differences
+    assert C.rel_l2(into, free) <= 1e-6
+
+
+@pytest.mark.parametrize("B,K,N,S", [(2, 48, 3, 9), (1, 8, 16, 17), (1, 96, 1, 5)])
+def test_unet_out_block_head_kernel(B, K, N, S):
+    """wf_conv1x1_head_cl (UnetOutBlock's 1x1x1 conv, channel-last in -> NCDHW logits) vs
+    torch's fp32 conv3d; ragged last position tile (S^3 % 256 != 0); the module's fast path."""
+    from waveformer_amd import ops
+    from waveformer_amd.blocks import UnetOutBlock
+    x = seeded_randn((B, K, S, S, S), 81).cuda().contiguous(memory_format=torch.channels_last_3d)
+    blk = UnetOutBlock(3, K, N).cuda().eval()
+    with torch.no_grad():
+        want = F.conv3d(x.contiguous(), blk.conv.conv.weight, blk.conv.conv.bias)
+        got = blk(x)
+    assert got.is_contiguous()
+    assert C.rel_l2(got, want) <= 1e-6
+    got2 = ops.conv1x1_head(x, blk.conv.conv.weight, None)
+    assert C.rel_l2(got2 + blk.conv.conv.bias.view(1, -1, 1, 1, 1), want) <= 1e-6
+
+
+@pytest.mark.parametrize("src,dst,ac", [((3, 4, 5), (6, 8, 10), True), ((4, 4, 4), (16, 16, 16), True),
+                                        ((5, 3, 4), (7, 9, 8), False)])
+def test_upsample_add_cl(src, dst, ac):
+    """wf_upsample_trilinear_add_cl: out += F.interpolate(x, trilinear), channel-last."""
+    from waveformer_amd import ops
+    cl = torch.channels_last_3d
+    x = seeded_randn((2, 8) + src, 82).cuda().contiguous(memory_format=cl)
+    base = seeded_randn((2, 8) + dst, 83).cuda().contiguous(memory_format=cl)
+    want = base + F.interpolate(x, size=dst, mode="trilinear", align_corners=ac)
+    got = ops.upsample_add_cl(x, base.clone(memory_format=cl), ac)
+    assert C.rel_l2(got, want) <= 1e-6
+    assert C.rel_l2(ops.upsample_cl(x, dst, ac),
+                    F.interpolate(x, size=dst, mode="trilinear", align_corners=ac)) <= 1e-6

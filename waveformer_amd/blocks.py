@@ -146,6 +146,9 @@ class UnetResBlock(nn.Module):
             dst = y if out is None else out
             if self.downsample:
                 c3 = self.conv3.conv
+                if x.shape[1] <= 7:  # few input channels (encoder1): residual on the fly
+                    return ops.norm_act_lin(y, s2, x, c3.weight, c3.bias, self.norm3.eps,
+                                            slope=slope, out=dst)
                 res = ops.conv1x1_cl(x, c3.weight, c3.bias)
                 return ops.norm_act(y, s2, res, ops.instnorm_stats(res, self.norm3.eps),
                                     slope=slope, out=dst)
@@ -223,6 +226,14 @@ class UnetOutBlock(nn.Module):
         self.conv = get_conv_layer(spatial_dims, in_channels, out_channels, 1, 1, bias=True)
 
     def forward(self, inp):
+        c = self.conv.conv if hasattr(self.conv, "conv") else self.conv
+        if (_fast_ok(inp, self) and type(c) is nn.Conv3d and c.kernel_size == (1, 1, 1)
+                and c.stride == (1, 1, 1) and c.padding == (0, 0, 0) and c.dilation == (1, 1, 1)
+                and c.groups == 1 and inp.shape[1] % 4 == 0
+                and inp.shape[1] <= 120 and c.out_channels <= 16
+                and ops.cl_ld(inp) is not None):
+            # channel-last decoder output -> NCDHW logits in one pass (wf_conv1x1_head_cl)
+            return ops.conv1x1_head(inp, c.weight, c.bias)
         return self.conv(inp)
 
 

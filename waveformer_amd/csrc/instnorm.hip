@@ -69,32 +69,156 @@ __global__ void instnorm_finalize_kernel(const double* __restrict__ acc, float* 
   stats[(int64_t)(b * 2 + 1) * C + c] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
-// one thread per (position, 4 channels)
+// grid (chunks, B): a workgroup streams `chunk` positions of sample b; thread (row, g) owns
+// channels 4g..4g+3 (its statistics in registers) and every R-th position (R = 256 / C4), so a
+// wave's accesses are whole contiguous position rows and no per-element index division
 __global__ __launch_bounds__(256) void norm_act_kernel(
     const float* __restrict__ a, int64_t lda, const float* __restrict__ sa,
     const float* __restrict__ r, int64_t ldr, const float* __restrict__ sr,
-    float* __restrict__ out, int64_t ldo, int C, int64_t P, int64_t total, float slope) {
+    float* __restrict__ out, int64_t ldo, int C, int64_t P, int64_t chunk, float slope) {
   const int C4 = C >> 2;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t pos = i / C4;  // over B * P
-    const int c = 4 * (int)(i - pos * C4);
-    const int b = (int)(pos / P);
-    const f32x4 av = *reinterpret_cast<const f32x4*>(a + pos * lda + c);
-    const f32x4 ma = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b) * C + c);
-    const f32x4 ra = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b + 1) * C + c);
-    f32x4 v = (av - ma) * ra;
-    if (r) {
-      f32x4 rv = *reinterpret_cast<const f32x4*>(r + pos * ldr + c);
-      if (sr) {
-        const f32x4 mr = *reinterpret_cast<const f32x4*>(sr + (int64_t)(2 * b) * C + c);
-        const f32x4 rr = *reinterpret_cast<const f32x4*>(sr + (int64_t)(2 * b + 1) * C + c);
-        rv = (rv - mr) * rr;
-      }
-      v += rv;
-    }
+  const int R = 256 / C4;
+  const int row = threadIdx.x / C4, g = threadIdx.x - row * C4;
+  if (row >= R) return;
+  const int b = blockIdx.y, c = 4 * g;
+  const f32x4 ma = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b) * C + c);
+  const f32x4 ra = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b + 1) * C + c);
+  f32x4 mr = {0.f, 0.f, 0.f, 0.f}, rr = {1.f, 1.f, 1.f, 1.f};
+  if (sr) {
+    mr = *reinterpret_cast<const f32x4*>(sr + (int64_t)(2 * b) * C + c);
+    rr = *reinterpret_cast<const f32x4*>(sr + (int64_t)(2 * b + 1) * C + c);
+  }
+  const int64_t p0 = (int64_t)blockIdx.x * chunk, p1 = min(P, p0 + chunk);
+#pragma unroll 2
+  for (int64_t p = p0 + row; p < p1; p += R) {
+    const int64_t pos = (int64_t)b * P + p;
+    f32x4 v = (*reinterpret_cast<const f32x4*>(a + pos * lda + c) - ma) * ra;
+    if (r) v += (*reinterpret_cast<const f32x4*>(r + pos * ldr + c) - mr) * rr;
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = v[j] >= 0.f ? v[j] : v[j] * slope;
+    *reinterpret_cast<f32x4*>(out + pos * ldo + c) = v;
+  }
+}
+
+// (chunks, B) grid of the streaming elementwise kernels: ~4096 workgroups, chunk a multiple of
+// the R rows a workgroup covers per step
+static void stream_grid(int64_t B, int64_t P, int64_t C, int64_t* chunks, int64_t* chunk) {
+  const int64_t R = 256 / (C / 4);
+  int64_t n = cdiv(4096, B);
+  int64_t ch = cdiv(P, n);
+  ch = cdiv(ch, R) * R;
+  if (ch < 4 * R) ch = 4 * R;
+  *chunk = ch;
+  *chunks = cdiv(P, ch);
+}
+
+// ---- a residual r = conv1x1(x) with few input channels (UnetResBlock's conv3 + norm3 when
+// Cin < 8: encoder1, 4 -> 48), never materialised.  InstanceNorm of a linear map of x is fixed
+// by x's per-sample mean and covariance: mean_r = W mean_x + b, var_r = W_c^T Cov_x W_c; the
+// host folds r' = (r - mean_r) * rstd_r into per-sample weights W' = rstd_r W, b' = (b -
+// mean_r) rstd_r (exact in real arithmetic), and norm_act reads K floats of x per position
+// instead of the C-channel residual and its statistics pass.
+// moments: acc (B, K + K*K) fp64 += sum_p x_k, sum_p x_k x_l; grid (chunks, B), 256 threads
+template <int K>
+__global__ __launch_bounds__(256) void moments_kernel(const float* __restrict__ x, int64_t ldx,
+                                                      int64_t P, int64_t chunk,
+                                                      double* __restrict__ acc) {
+  constexpr int NM = K + K * (K + 1) / 2;
+  __shared__ double red[4][NM];
+  const int b = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * chunk;
+  const int64_t p1 = min(P, p0 + chunk);
+  double m[NM];
+#pragma unroll
+  for (int i = 0; i < NM; ++i) m[i] = 0.0;
+  const float* base = x + (int64_t)b * P * ldx;
+  for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+    double v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = (double)base[p * ldx + k];
+    int i = K;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      m[k] += v[k];
+#pragma unroll
+      for (int l = k; l < K; ++l) m[i++] += v[k] * v[l];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    double t = m[i];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    m[i] = t;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) red[w][i] = m[i];
+  }
+  __syncthreads();
+  if (threadIdx.x < NM) {
+    const int i = threadIdx.x;
+    const double t = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    // upper-triangle moment i -> both (k, l) and (l, k) of the K x K block
+    if (i < K) {
+      atomicAdd(acc + (int64_t)b * (K + K * K) + i, t);
+    } else {
+      int j = i - K, k = 0;
+      while (j >= K - k) {
+        j -= K - k;
+        ++k;
+      }
+      const int l = k + j;
+      double* q = acc + (int64_t)b * (K + K * K) + K;
+      atomicAdd(q + k * K + l, t);
+      if (l != k) atomicAdd(q + l * K + k, t);
+    }
+  }
+}
+
+// out = act((a - mean_a) * rstd_a + sum_k wf[b][c][k] x[p][k] + bf[b][c]); the (chunks, B)
+// mapping of norm_act_kernel, the folded weights of the thread's 4 channels in registers
+template <int K>
+__global__ __launch_bounds__(256) void norm_act_lin_kernel(
+    const float* __restrict__ a, int64_t lda, const float* __restrict__ sa,
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ wf,
+    const float* __restrict__ bf, float* __restrict__ out, int64_t ldo, int C, int64_t P,
+    int64_t chunk, float slope, int xvec) {
+  const int C4 = C >> 2;
+  const int R = 256 / C4;
+  const int row = threadIdx.x / C4, g = threadIdx.x - row * C4;
+  if (row >= R) return;
+  const int b = blockIdx.y, c = 4 * g;
+  const f32x4 ma = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b) * C + c);
+  const f32x4 ra = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b + 1) * C + c);
+  const f32x4 bb = *reinterpret_cast<const f32x4*>(bf + (int64_t)b * C + c) - ma * ra;
+  float w[4][K];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < K; ++k) w[j][k] = wf[((int64_t)b * C + c + j) * K + k];
+  const bool x4 = K == 4 && xvec;  // one 16-B load of the position's x
+  const int64_t p0 = (int64_t)blockIdx.x * chunk, p1 = min(P, p0 + chunk);
+#pragma unroll 2
+  for (int64_t p = p0 + row; p < p1; p += R) {
+    const int64_t pos = (int64_t)b * P + p;
+    float xv[K];
+    if (x4) {
+      const f32x4 t = *reinterpret_cast<const f32x4*>(x + pos * ldx);
+#pragma unroll
+      for (int k = 0; k < K; ++k) xv[k] = t[k & 3];
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) xv[k] = x[pos * ldx + k];
+    }
+    f32x4 v = *reinterpret_cast<const f32x4*>(a + pos * lda + c) * ra + bb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) v[j] = fmaf(w[j][k], xv[k], v[j]);
+      v[j] = v[j] >= 0.f ? v[j] : v[j] * slope;
+    }
     *reinterpret_cast<f32x4*>(out + pos * ldo + c) = v;
   }
 }
@@ -333,10 +457,61 @@ extern "C" int wf_norm_act_cl(const float* a, int64_t lda, const float* stats_a,
   WF_REQUIRE_PTR(a);
   WF_REQUIRE_PTR(stats_a);
   WF_REQUIRE_PTR(out);
-  const int64_t total = B * P * (C / 4);
-  int64_t blocks = cdiv(total, 256);
-  if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(norm_act_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                     a, lda, stats_a, r, ldr, stats_r, out, ldo, (int)C, P, total, slope);
+  WF_REQUIRE(C <= 1024, "C must be <= 1024");
+  int64_t chunks, chunk;
+  stream_grid(B, P, C, &chunks, &chunk);
+  hipLaunchKernelGGL(norm_act_kernel, dim3((unsigned)chunks, (unsigned)B), dim3(256), 0,
+                     (hipStream_t)stream, a, lda, stats_a, r, ldr, stats_r, out, ldo, (int)C, P,
+                     chunk, slope);
   return check_launch("wf_norm_act_cl");
+}
+
+extern "C" int wf_moments_cl(const float* x, int64_t ldx, int64_t B, int64_t K, int64_t P,
+                             double* acc, void* stream) {
+  WF_REQUIRE(B >= 1 && P >= 1, "empty tensor");
+  WF_REQUIRE(K >= 1 && K <= 7 && ldx >= K, "K must be in [1, 7] with ldx >= K");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(acc);
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(acc, 0, (size_t)(B * (K + K * K)) * sizeof(double), s) != hipSuccess)
+    return check_launch("wf_moments_cl (memset)");
+  int64_t chunks = cdiv(2048, B);
+  int64_t chunk = cdiv(P, chunks);
+  if (chunk < 1024) chunk = 1024;
+  chunks = cdiv(P, chunk);
+  const dim3 grid((unsigned)chunks, (unsigned)B);
+  switch (K) {
+#define WF_MOM(k) case k: hipLaunchKernelGGL(moments_kernel<k>, grid, dim3(256), 0, s, x, ldx, P, chunk, acc); break;
+    WF_MOM(1) WF_MOM(2) WF_MOM(3) WF_MOM(4) WF_MOM(5) WF_MOM(6) WF_MOM(7)
+#undef WF_MOM
+  }
+  return check_launch("wf_moments_cl");
+}
+
+extern "C" int wf_norm_act_lin_cl(const float* a, int64_t lda, const float* stats_a,
+                                  const float* x, int64_t ldx, int64_t K, const float* wfold,
+                                  const float* bfold, float* out, int64_t ldo, int64_t B,
+                                  int64_t C, int64_t P, float slope, void* stream) {
+  WF_REQUIRE(B >= 1 && P >= 1, "empty tensor");
+  WF_REQUIRE(C >= 4 && C % 4 == 0 && lda >= C && lda % 4 == 0 && ldo >= C && ldo % 4 == 0,
+             "C must be a multiple of 4 and every ld >= C, a multiple of 4");
+  WF_REQUIRE(K >= 1 && K <= 7 && ldx >= K, "K must be in [1, 7] with ldx >= K");
+  WF_REQUIRE_PTR(a);
+  WF_REQUIRE_PTR(stats_a);
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(wfold);
+  WF_REQUIRE_PTR(bfold);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE(C <= 1024, "C must be <= 1024");
+  int64_t chunks, chunk;
+  stream_grid(B, P, C, &chunks, &chunk);
+  const dim3 grid((unsigned)chunks, (unsigned)B);
+  const int xvec = (ldx % 4 == 0) && (((uintptr_t)x & 15) == 0);
+  hipStream_t s = (hipStream_t)stream;
+  switch (K) {
+#define WF_NAL(k) case k: hipLaunchKernelGGL(norm_act_lin_kernel<k>, grid, dim3(256), 0, s, a, lda, stats_a, x, ldx, wfold, bfold, out, ldo, (int)C, P, chunk, slope, xvec); break;
+    WF_NAL(1) WF_NAL(2) WF_NAL(3) WF_NAL(4) WF_NAL(5) WF_NAL(6) WF_NAL(7)
+#undef WF_NAL
+  }
+  return check_launch("wf_norm_act_lin_cl");
 }

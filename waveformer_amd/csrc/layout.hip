@@ -66,6 +66,67 @@ __global__ __launch_bounds__(256) void subvoxel_scatter_cl_kernel(
   }
 }
 
+// UnetOutBlock (monai dynunet_block.py:188-210): 1x1x1 conv, K input channels (channel-last,
+// positions ldx floats apart) -> N <= 16 classes written NCDHW, the layout the network returns.
+// A workgroup stages 256 positions x K channels (coalesced 16-B loads, row stride K + 4 floats)
+// and the (N, K) weights in LDS; lane t then computes position t's N outputs from 16-B LDS
+// reads only (weights as broadcast reads: scalar weight loads would share lgkmcnt with the LDS
+// reads and serialise them), fp32 FMAs; the N stores are coalesced along positions.
+// grid (cdiv(P, 256), B)
+constexpr int HEAD_TP = 256;
+template <int N>
+__global__ __launch_bounds__(256) void conv1x1_head_kernel(
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ wt,
+    const float* __restrict__ bias, float* __restrict__ out, int K, int64_t P) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];  // [HEAD_TP][K + 4], [N][K]
+  const int b = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * HEAD_TP;
+  const int np = (int)min((int64_t)HEAD_TP, P - p0);
+  const int K4 = K >> 2, KS = K + 4;
+  float* wl = tile + HEAD_TP * KS;
+  const float* src = x + ((int64_t)b * P + p0) * ldx;
+  // four 16-B loads in flight per lane before their LDS stores (clamped addresses, guarded
+  // stores): a load-store pair per iteration left one load in flight and ran latency-bound
+  const int tot = np * K4;
+  for (int e0 = threadIdx.x; e0 < tot; e0 += 4 * HEAD_TP) {
+    f32x4 v[4];
+    int off[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = min(e0 + u * HEAD_TP, tot - 1);
+      const int r = e / K4, c = 4 * (e - r * K4);
+      off[u] = r * KS + c;
+      v[u] = *reinterpret_cast<const f32x4*>(src + (int64_t)r * ldx + c);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (e0 + u * HEAD_TP < tot) *reinterpret_cast<f32x4*>(tile + off[u]) = v[u];
+  }
+  for (int e = threadIdx.x; e < N * K4; e += blockDim.x)
+    *reinterpret_cast<f32x4*>(wl + 4 * e) = *reinterpret_cast<const f32x4*>(wt + 4 * e);
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= np) return;
+  float acc[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) acc[n] = bias ? bias[n] : 0.f;
+  const float* xr = tile + t * KS;
+  for (int k = 0; k < K; k += 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + k);
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(wl + n * K + k);
+      acc[n] = fmaf(w.x, v.x, acc[n]);
+      acc[n] = fmaf(w.y, v.y, acc[n]);
+      acc[n] = fmaf(w.z, v.z, acc[n]);
+      acc[n] = fmaf(w.w, v.w, acc[n]);
+    }
+  }
+  float* o = out + (int64_t)b * N * P + p0 + t;
+#pragma unroll
+  for (int n = 0; n < N; ++n) o[(int64_t)n * P] = acc[n];
+}
+
 static unsigned grid_for(int64_t total) {
   int64_t blocks = cdiv(total, 256);
   if (blocks > 65536) blocks = 65536;  // grid-stride beyond: ~256 workgroups per CU
@@ -111,4 +172,27 @@ extern "C" int wf_subvoxel_scatter_cl(const float* g, const float* bias, float* 
                      FastDiv((uint32_t)w), FastDiv((uint32_t)h), FastDiv((uint32_t)d),
                      (uint32_t)total);
   return check_launch("wf_subvoxel_scatter_cl");
+}
+
+extern "C" int wf_conv1x1_head_cl(const float* x, int64_t ldx, const float* weight,
+                                  const float* bias, float* out, int64_t B, int64_t K, int64_t N,
+                                  int64_t P, void* stream) {
+  WF_REQUIRE(B >= 1 && P >= 1, "empty tensor");
+  WF_REQUIRE(K >= 4 && K % 4 == 0 && K <= 120 && ldx >= K && ldx % 4 == 0,
+             "K must be a multiple of 4 in [4, 120], ldx >= K a multiple of 4");
+  WF_REQUIRE(N >= 1 && N <= 16, "N must be in [1, 16]");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(weight);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE(aligned16(x) && aligned16(weight), "x / weight must be 16-byte aligned");
+  const size_t lds = ((size_t)HEAD_TP * (K + 4) + N * K) * sizeof(float);
+  const dim3 grid((unsigned)cdiv(P, HEAD_TP), (unsigned)B);
+  hipStream_t s = (hipStream_t)stream;
+  switch (N) {
+#define WF_HEAD(n) case n: if (lds > 64 * 1024) set_max_lds(reinterpret_cast<const void*>(conv1x1_head_kernel<n>), (int)lds); hipLaunchKernelGGL(conv1x1_head_kernel<n>, grid, dim3(256), lds, s, x, ldx, weight, bias, out, (int)K, P); break;
+    WF_HEAD(1) WF_HEAD(2) WF_HEAD(3) WF_HEAD(4) WF_HEAD(5) WF_HEAD(6) WF_HEAD(7) WF_HEAD(8)
+    WF_HEAD(9) WF_HEAD(10) WF_HEAD(11) WF_HEAD(12) WF_HEAD(13) WF_HEAD(14) WF_HEAD(15) WF_HEAD(16)
+#undef WF_HEAD
+  }
+  return check_launch("wf_conv1x1_head_cl");
 }

@@ -34,31 +34,40 @@ __device__ __forceinline__ Src1 src_index(int dst, int in, int out, bool ac) {
   return s;
 }
 
+// one workgroup per output row (b, z, y): the z / y source rows and weights once per
+// workgroup, lanes over (x, 4 channels) with one 32-bit division; ADD: out += the resampled
+// value (ProjectionUpsample's `y + Up(res)`, wave_helper.py:81, without a separate add pass)
+template <bool ADD>
 __global__ __launch_bounds__(256) void upsample_cl_kernel(const float* __restrict__ in,
                                                           float* __restrict__ out, int C, int d,
                                                           int h, int w, int D, int H, int W,
-                                                          int64_t total, int ac) {
+                                                          int ac) {
   const int C4 = C >> 2;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = 4 * (int)(i % C4);
-    int64_t t = i / C4;
-    const int x = (int)(t % W);
-    t /= W;
-    const int y = (int)(t % H);
-    t /= H;
-    const int z = (int)(t % D);
-    const int64_t b = t / D;
-    const Src1 sz = src_index(z, d, D, ac), sy = src_index(y, h, H, ac), sx = src_index(x, w, W, ac);
-    const float* base = in + b * ((int64_t)d * h * w * C) + c;
-    auto at = [&](int zz, int yy, int xx) {
-      return *reinterpret_cast<const f32x4*>(base + (((int64_t)zz * h + yy) * w + xx) * C);
-    };
-    const f32x4 v0 = sy.l0 * (sx.l0 * at(sz.i0, sy.i0, sx.i0) + sx.l1 * at(sz.i0, sy.i0, sx.i1)) +
-                     sy.l1 * (sx.l0 * at(sz.i0, sy.i1, sx.i0) + sx.l1 * at(sz.i0, sy.i1, sx.i1));
-    const f32x4 v1 = sy.l0 * (sx.l0 * at(sz.i1, sy.i0, sx.i0) + sx.l1 * at(sz.i1, sy.i0, sx.i1)) +
-                     sy.l1 * (sx.l0 * at(sz.i1, sy.i1, sx.i0) + sx.l1 * at(sz.i1, sy.i1, sx.i1));
-    *reinterpret_cast<f32x4*>(out + i * 4) = sz.l0 * v0 + sz.l1 * v1;
+  const int row = blockIdx.x;  // (b * D + z) * H + y
+  const int y = row % H, bz = row / H;
+  const int z = bz % D, b = bz / D;
+  const Src1 sz = src_index(z, d, D, ac), sy = src_index(y, h, H, ac);
+  const float* base = in + (int64_t)b * ((int64_t)d * h * w * C);
+  const float* r00 = base + ((int64_t)sz.i0 * h + sy.i0) * w * C;
+  const float* r01 = base + ((int64_t)sz.i0 * h + sy.i1) * w * C;
+  const float* r10 = base + ((int64_t)sz.i1 * h + sy.i0) * w * C;
+  const float* r11 = base + ((int64_t)sz.i1 * h + sy.i1) * w * C;
+  float* orow = out + (int64_t)row * W * C;
+  const int n = W * C4;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int x = i / C4;
+    const int c = 4 * (i - x * C4);
+    const Src1 sx = src_index(x, w, W, ac);
+    const int o0 = sx.i0 * C + c, o1 = sx.i1 * C + c;
+    auto at = [&](const float* r, int o) { return *reinterpret_cast<const f32x4*>(r + o); };
+    const f32x4 v0 = sy.l0 * (sx.l0 * at(r00, o0) + sx.l1 * at(r00, o1)) +
+                     sy.l1 * (sx.l0 * at(r01, o0) + sx.l1 * at(r01, o1));
+    const f32x4 v1 = sy.l0 * (sx.l0 * at(r10, o0) + sx.l1 * at(r10, o1)) +
+                     sy.l1 * (sx.l0 * at(r11, o0) + sx.l1 * at(r11, o1));
+    f32x4 v = sz.l0 * v0 + sz.l1 * v1;
+    f32x4* op = reinterpret_cast<f32x4*>(orow + (int64_t)x * C + c);
+    if (ADD) v = *op + v;
+    *op = v;
   }
 }
 
@@ -143,18 +152,32 @@ extern "C" int wf_resample_trilinear_cf(const float* in, int64_t ldc, int64_t C,
   return check_launch("wf_resample_trilinear_cf");
 }
 
+static int upsample_cl_launch(const float* in, float* out, int64_t B, int64_t C, int64_t d,
+                              int64_t h, int64_t w, int64_t D, int64_t H, int64_t W,
+                              int align_corners, bool add, void* stream, const char* who) {
+  WF_REQUIRE(B >= 1 && d >= 1 && h >= 1 && w >= 1 && D >= 1 && H >= 1 && W >= 1, "empty tensor");
+  WF_REQUIRE(C >= 4 && C % 4 == 0, "C must be a positive multiple of 4");
+  WF_REQUIRE(B * D * H < ((int64_t)1 << 31) && W * (C / 4) < ((int64_t)1 << 31),
+             "output too large");
+  WF_REQUIRE_PTR(in);
+  WF_REQUIRE_PTR(out);
+  auto k = add ? upsample_cl_kernel<true> : upsample_cl_kernel<false>;
+  hipLaunchKernelGGL(k, dim3((unsigned)(B * D * H)), dim3(256), 0, (hipStream_t)stream, in, out,
+                     (int)C, (int)d, (int)h, (int)w, (int)D, (int)H, (int)W, align_corners);
+  return check_launch(who);
+}
+
 extern "C" int wf_upsample_trilinear_cl(const float* in, float* out, int64_t B, int64_t C,
                                         int64_t d, int64_t h, int64_t w, int64_t D, int64_t H,
                                         int64_t W, int align_corners, void* stream) {
-  WF_REQUIRE(B >= 1 && d >= 1 && h >= 1 && w >= 1 && D >= 1 && H >= 1 && W >= 1, "empty tensor");
-  WF_REQUIRE(C >= 4 && C % 4 == 0, "C must be a positive multiple of 4");
-  WF_REQUIRE_PTR(in);
-  WF_REQUIRE_PTR(out);
-  const int64_t total = B * D * H * W * (C / 4);
-  int64_t blocks = cdiv(total, 256);
-  if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(upsample_cl_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                     in, out, (int)C, (int)d, (int)h, (int)w, (int)D, (int)H, (int)W, total,
-                     align_corners);
-  return check_launch("wf_upsample_trilinear_cl");
+  return upsample_cl_launch(in, out, B, C, d, h, w, D, H, W, align_corners, false, stream,
+                            "wf_upsample_trilinear_cl");
+}
+
+extern "C" int wf_upsample_trilinear_add_cl(const float* in, float* out, int64_t B, int64_t C,
+                                            int64_t d, int64_t h, int64_t w, int64_t D,
+                                            int64_t H, int64_t W, int align_corners,
+                                            void* stream) {
+  return upsample_cl_launch(in, out, B, C, d, h, w, D, H, W, align_corners, true, stream,
+                            "wf_upsample_trilinear_add_cl");
 }

@@ -148,9 +148,11 @@ class ProjectionUpsample(nn.Module):
         rows = y.permute(0, 2, 3, 4, 1).reshape(B, P, C)
         # the 1x1 convs are MFMA GEMMs (wf_linear_fwd); each GELU is applied in the NEXT
         # GEMM's operand loader, so no activation tensor is written twice
-        hid = torch.cat([ops.linear_rows(rows[i], w2s[i], b2s[i].contiguous(), cache=False)
-                         for i in range(B)]) if B > 1 else \
-            ops.linear_rows(rows[0], w2s[0], b2s[0].contiguous(), cache=False)
+        # one GEMM per sample (GroupNorm folded per sample), each into its rows of one buffer
+        hid = torch.empty((B * P, 2 * C), dtype=torch.float32, device=x.device)
+        for i in range(B):
+            ops.linear_rows(rows[i], w2s[i], b2s[i].contiguous(), cache=False,
+                            out=hid[i * P:(i + 1) * P])
         if self.use_double_conv:
             c3a, c3b = self.conv3[0], self.conv3[2]
             hid = ops.linear_rows(hid, c3a.weight, c3a.bias, gelu_in=True)
@@ -163,7 +165,7 @@ class ProjectionUpsample(nn.Module):
         if self.do_res:
             rc = self.res_conv[1]
             r = ops.conv1x1_cl(xc, rc.weight, rc.bias)
-            out = out + ops.upsample_cl(r, size, True)
+            ops.upsample_add_cl(r, out, True)  # out += Up(r), in the upsample kernel
         return out
 
 

@@ -763,10 +763,16 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor
 
 def conv1x1_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None
                ) -> torch.Tensor:
-    """1x1x1 Conv3d of a channel-last tensor as one fp32 GEMM over its position rows."""
+    """1x1x1 Conv3d of a channel-last tensor as one GEMM over its position rows: the streaming
+    MFMA GEMM at bf16x3 (fp32-faithful, under every global precision) when Cin % 8 == 0 and
+    Cout % 4 == 0, else torch's fp32 GEMM."""
     x = to_cl(x)
     B, Cin, D, H, W = x.shape
     Cout = weight.shape[0]
+    if Cin % 8 == 0 and Cout % 4 == 0 and cl_ld(x) == Cin and x.is_cuda:
+        rows = x.permute(0, 2, 3, 4, 1).reshape(-1, Cin)
+        y = linear_rows(rows, weight, bias, prec=PRECISIONS["bf16x3"])
+        return y.view(B, D, H, W, Cout).permute(0, 4, 1, 2, 3)
     rows = x.permute(0, 2, 3, 4, 1).reshape(-1, Cin)
     w2 = weight.reshape(Cout, Cin)
     y = torch.addmm(bias, rows, w2.t()) if bias is not None else torch.mm(rows, w2.t())
@@ -782,6 +788,37 @@ def upsample_cl(x: torch.Tensor, size: Sequence[int], align_corners: bool) -> to
     out = empty_cl(B, C, D, H, W, x.device)
     _lib.call("wf_upsample_trilinear_cl", x.data_ptr(), out.data_ptr(), B, C, d, h, w, D, H, W,
               int(bool(align_corners)), _stream())
+    return out
+
+
+def upsample_add_cl(x: torch.Tensor, out: torch.Tensor, align_corners: bool) -> torch.Tensor:
+    """out += F.interpolate(x, out.shape[2:], mode='trilinear', align_corners) for channel-last
+    x and a dense channel-last out (wf_upsample_trilinear_add_cl)."""
+    x = x if (cl_ld(x) == x.shape[1]) else x.contiguous(memory_format=torch.channels_last_3d)
+    B, C, d, h, w = x.shape
+    if cl_ld(out) != C or tuple(out.shape[:2]) != (B, C):
+        raise ValueError("upsample_add_cl: out must be a dense channel-last (B, C, D, H, W)")
+    D, H, W = out.shape[2:]
+    _lib.call("wf_upsample_trilinear_add_cl", x.data_ptr(), out.data_ptr(), B, C, d, h, w, D, H,
+              W, int(bool(align_corners)), _stream())
+    return out
+
+
+def conv1x1_head(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
+                 ) -> torch.Tensor:
+    """UnetOutBlock's 1x1x1 conv of a channel-last x (K <= 120 channels) into N <= 16 classes,
+    returned NCDHW-contiguous (wf_conv1x1_head_cl, fp32)."""
+    ld = cl_ld(x)
+    if ld is None:
+        raise ValueError("conv1x1_head: channel-last input expected")
+    B, K, D, H, W = x.shape
+    N = weight.shape[0]
+    w2 = weight.detach().reshape(N, K).contiguous()
+    if bias is not None:
+        _check(bias, "bias")
+    out = torch.empty((B, N, D, H, W), dtype=torch.float32, device=x.device)
+    _lib.call("wf_conv1x1_head_cl", x.data_ptr(), ld, w2.data_ptr(), _ptr(bias), out.data_ptr(),
+              B, K, N, D * H * W, _stream())
     return out
 
 
@@ -820,26 +857,32 @@ def conv3d_k3_wgrad(x: torch.Tensor, dy: torch.Tensor, wshape) -> torch.Tensor:
 
 
 def linear_rows(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
-                gelu_in: bool = False, cache: bool = True) -> torch.Tensor:
+                gelu_in: bool = False, cache: bool = True, prec: Optional[int] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bias + act(x2d) . W^T on the MFMA GEMM family (wf_linear_fwd), act = GELU(erf) when
     gelu_in.  weight (N, K) or (N, K, 1, 1, 1); `cache=False` for per-call weights (no split
-    cache on the tensor)."""
+    cache on the tensor); `prec` a WF_PREC_* id overriding the global precision; `out` a
+    contiguous (M, N) destination (e.g. one sample's row slice of a batch buffer)."""
     _check(x2d, "x")
     M, K = x2d.shape
     N = weight.shape[0]
     w2 = weight.reshape(N, K)
+    pr = _prec() if prec is None else prec
     if cache:
-        wb = split_weight(weight, (N, K), _prec())
+        wb = split_weight(weight, (N, K), pr)
     else:
         w2 = w2.contiguous()
         wb = torch.empty((2, N, K), dtype=torch.bfloat16, device=x2d.device)
-        _lib.call("wf_cast_f32_to_f16x2" if _prec() == FP16 else "wf_split_f32_to_bf16x2",
+        _lib.call("wf_cast_f32_to_f16x2" if pr == FP16 else "wf_split_f32_to_bf16x2",
                   w2.data_ptr(), wb.data_ptr(), w2.numel(), _stream())
     if bias is not None:
         _check(bias, "bias")
-    out = torch.empty((M, N), dtype=torch.float32, device=x2d.device)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=x2d.device)
+    elif tuple(out.shape) != (M, N) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise ValueError(f"linear_rows: out must be a contiguous fp32 ({M}, {N}) tensor")
     _lib.call("wf_linear_fwd", x2d.data_ptr(), wb.data_ptr(), _ptr(bias), out.data_ptr(), M, K, N,
-              int(bool(gelu_in)), _prec(), _stream())
+              int(bool(gelu_in)), pr, _stream())
     return out
 
 
@@ -881,6 +924,46 @@ def norm_act(a: torch.Tensor, stats_a: torch.Tensor, r: Optional[torch.Tensor] =
         raise ValueError("norm_act: out must be channel-last and shaped like a")
     _lib.call("wf_norm_act_cl", a.data_ptr(), lda, stats_a.data_ptr(), _ptr(r), ldr,
               _ptr(stats_r), out.data_ptr(), ldo, B, C, P, float(slope), _stream())
+    return out
+
+
+def norm_act_lin(a: torch.Tensor, stats_a: torch.Tensor, x: torch.Tensor,
+                 weight: torch.Tensor, bias: Optional[torch.Tensor], eps: float,
+                 slope: float = 0.01, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """norm_act(a, stats_a, r, instnorm_stats(r, eps)) with r = conv1x1(x; weight, bias) for
+    x with few channels (Cin <= 7), r never materialised: x's fp64 moments (wf_moments_cl) give
+    InstanceNorm(r)'s per-sample mean and variance, folded into per-sample weights that
+    wf_norm_act_lin_cl applies on the fly (exact in real arithmetic)."""
+    lda = cl_ld(a)
+    x = to_cl(x)
+    ldx = cl_ld(x)
+    if lda is None or ldx is None:
+        raise ValueError("norm_act_lin: channel-last inputs expected")
+    B, C = a.shape[:2]
+    K = x.shape[1]
+    if not 1 <= K <= 7 or tuple(x.shape[2:]) != tuple(a.shape[2:]) or x.shape[0] != B:
+        raise ValueError(f"norm_act_lin: x {tuple(x.shape)} does not fit a {tuple(a.shape)}")
+    P = a.shape[2] * a.shape[3] * a.shape[4]
+    acc = torch.empty((B, K + K * K), dtype=torch.float64, device=a.device)
+    _lib.call("wf_moments_cl", x.data_ptr(), ldx, B, K, P, acc.data_ptr(), _stream())
+    mu = acc[:, :K] / P
+    cov = acc[:, K:].view(B, K, K) / P - mu[:, :, None] * mu[:, None, :]
+    W = weight.detach().reshape(C, K).double()
+    bv = bias.detach().double() if bias is not None else torch.zeros(C, dtype=torch.float64,
+                                                                     device=a.device)
+    mean_r = mu @ W.t() + bv                                      # (B, C)
+    var_r = torch.einsum("ck,bkl,cl->bc", W, cov, W).clamp_min(0)  # biased, as InstanceNorm
+    rstd_r = torch.rsqrt(var_r + eps)
+    wfold = (W[None] * rstd_r[..., None]).float().contiguous()     # (B, C, K)
+    bfold = ((bv[None] - mean_r) * rstd_r).float().contiguous()    # (B, C)
+    if out is None:
+        out = empty_cl(*a.shape, device=a.device)
+    ldo = cl_ld(out)
+    if ldo is None or tuple(out.shape) != tuple(a.shape):
+        raise ValueError("norm_act_lin: out must be channel-last and shaped like a")
+    _lib.call("wf_norm_act_lin_cl", a.data_ptr(), lda, stats_a.data_ptr(), x.data_ptr(), ldx, K,
+              wfold.data_ptr(), bfold.data_ptr(), out.data_ptr(), ldo, B, C, P, float(slope),
+              _stream())
     return out
 
 
