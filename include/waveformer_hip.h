@@ -188,6 +188,13 @@ int wf_conv3d_k3_pack_f16(const float* w, uint16_t* packed, int64_t Cin, int64_t
 int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed, const float* bias,
                      float* out, int64_t ldo, double* stats_acc, int64_t B, int64_t Cin,
                      int64_t Cout, int64_t D, int64_t H, int64_t W, int precision, void* stream);
+/* wf_conv3d_k3_fwd at WF_PREC_FP16 with the input already fp16 (channel-last, ldx halves per
+ * position, 8-byte aligned; w packed by wf_conv3d_k3_pack_f16): the operands are those the fp32
+ * path stages after rounding, so the output is bitwise the same for an input written by
+ * wf_norm_act_h_cl.  Half the staging bytes, no conversion.                                 */
+int wf_conv3d_k3_fwd_xh(const uint16_t* x, int64_t ldx, const uint16_t* w_packed_f16,
+                        const float* bias, float* out, int64_t ldo, double* stats_acc, int64_t B,
+                        int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W, void* stream);
 
 /* Weight gradient of wf_conv3d_k3_fwd (training, config 4):
  *   dw[co, ci, kz, ky, kx] (+)= sum_p dy[p, co] * x[p + (kz-1, ky-1, kx-1), ci]
@@ -217,6 +224,11 @@ int wf_instnorm_finalize(const double* acc, float* stats, int64_t B, int64_t C, 
 int wf_norm_act_cl(const float* a, int64_t lda, const float* stats_a, const float* r, int64_t ldr,
                    const float* stats_r, float* out, int64_t ldo, int64_t B, int64_t C, int64_t P,
                    float slope, void* stream);
+/* act((a - mean_a) * rstd_a) stored fp16 (round to nearest even, channel-last, ldo halves per
+ * position): UnetResBlock / UnetBasicBlock's norm1 + lrelu (dynunet_block.py:101-103) feeding an
+ * fp16 conv2 (wf_conv3d_k3_fwd_xh).                                                          */
+int wf_norm_act_h_cl(const float* a, int64_t lda, const float* stats_a, uint16_t* out,
+                     int64_t ldo, int64_t B, int64_t C, int64_t P, float slope, void* stream);
 
 /* The norm3'ed 1x1 residual of UnetResBlock (monai dynunet_block.py:77-80, 104-108) for few
  * input channels (K = Cin <= 7; encoder1: 4 -> 48) without materialising it: wf_moments_cl

@@ -439,3 +439,35 @@ def test_upsample_add_cl(src, dst, ac):
     assert C.rel_l2(got, want) <= 1e-6
     assert C.rel_l2(ops.upsample_cl(x, dst, ac),
                     F.interpolate(x, size=dst, mode="trilinear", align_corners=ac)) <= 1e-6
+
+
+@pytest.mark.parametrize("B,C_,S", [(2, 48, 40), (1, 96, 9), (1, 16, 37)])
+def test_conv3d_k3_fp16_input_bitwise(B, C_, S):
+    """fp16 policy: conv1's norm1 + lrelu stored fp16 (wf_norm_act_h_cl) and conv2 on the
+    fp16-input kernel (wf_conv3d_k3_fwd_xh) give bitwise the output of the fp32 path, whose
+    staging rounds the same values to fp16; the stored operands are torch's fp16 rounding."""
+    from waveformer_amd import ops
+    from waveformer_amd.blocks import UnetResBlock
+    cl = torch.channels_last_3d
+    a = seeded_randn((B, C_, S, S, S), 91).cuda().contiguous(memory_format=cl)
+    w = seeded_randn((48, C_, 3, 3, 3), 92).cuda() * 0.05
+    bias = seeded_randn((48,), 93).cuda()
+    st = ops.instnorm_stats(a, 1e-5)
+    with ops.precision("fp16"):
+        h32 = ops.norm_act(a, st, slope=0.01)
+        h16 = ops.norm_act_h(a, st, slope=0.01)
+        assert h16.dtype == torch.float16 and torch.equal(h16, h32.half())
+        y32, s32 = ops.conv3d_k3(h32, w, bias, norm_eps=1e-5)
+        y16, s16 = ops.conv3d_k3(h16, w, bias, norm_eps=1e-5)
+    if B * S * (S // 4) >= 512:  # no split-K (whose fp32 atomics add in any order): bitwise
+        assert torch.equal(y32, y16)
+    assert C.rel_l2(y16, y32) <= 1e-6
+    assert C.rel_l2(s16, s32) <= 1e-6
+    # the block's fast path at fp16 (norm_act_h inside) vs the same block at bf16x3
+    torch.manual_seed(0)
+    blk = UnetResBlock(3, C_, 48, 3, 1, "instance").cuda().eval()
+    with torch.no_grad():
+        ref = blk(a)
+        with ops.precision("fp16"):
+            got = blk(a)
+    assert C.rel_l2(got, ref) <= 5e-3

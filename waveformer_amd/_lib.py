@@ -40,6 +40,8 @@ SIGNATURES = {
     "wf_subvoxel_scatter_cl": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_convtranspose2_cl": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
     "wf_moments_cl": (_I, [_P, _I64, _I64, _I64, _I64, _P, _P]),
+    "wf_conv3d_k3_fwd_xh": (_I, [_P, _I64, _P, _P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_norm_act_h_cl": (_I, [_P, _I64, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "wf_upsample_trilinear_add_cl": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
     "wf_conv1x1_head_cl": (_I, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "wf_norm_act_lin_cl": (_I, [_P, _I64, _P, _P, _I64, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),

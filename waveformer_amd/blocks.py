@@ -98,6 +98,14 @@ def get_conv_layer(spatial_dims: int, in_channels: int, out_channels: int,
     return Convolution(in_channels, out_channels, kernel_size, stride, pad, bias, is_transposed, op)
 
 
+def _act_for_conv2(h: torch.Tensor, s1: torch.Tensor, slope: float) -> torch.Tensor:
+    """norm1 + lrelu of conv1's output, the input of conv2: stored fp16 when conv2 runs at the
+    fp16 precision (the operands it would round to anyway, half the bytes), else in place."""
+    if ops.prec_id() == ops.FP16 and h.shape[1] % 4 == 0:
+        return ops.norm_act_h(h, s1, slope=slope)
+    return ops.norm_act(h, s1, slope=slope, out=h)
+
+
 def _into(y: torch.Tensor, out: Optional[torch.Tensor]) -> torch.Tensor:
     return y if out is None else out.copy_(y)
 
@@ -140,9 +148,8 @@ class UnetResBlock(nn.Module):
             with ops.op_precision("skip_conv" if self._split_conv1 else "conv"):
                 h, s1 = ops.conv3d_k3(x, self.conv1.conv.weight, self.conv1.conv.bias,
                                       norm_eps=self.norm1.eps)
-            ops.norm_act(h, s1, slope=slope, out=h)
-            y, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
-                                  norm_eps=self.norm2.eps)
+            y, s2 = ops.conv3d_k3(_act_for_conv2(h, s1, slope), self.conv2.conv.weight,
+                                  self.conv2.conv.bias, norm_eps=self.norm2.eps)
             dst = y if out is None else out
             if self.downsample:
                 c3 = self.conv3.conv
@@ -201,9 +208,8 @@ class UnetBasicBlock(nn.Module):
             with ops.op_precision("skip_conv" if self._split_conv1 else "conv"):
                 h, s1 = ops.conv3d_k3(inp, self.conv1.conv.weight, self.conv1.conv.bias,
                                       norm_eps=self.norm1.eps)
-            ops.norm_act(h, s1, slope=slope, out=h)
-            y, s2 = ops.conv3d_k3(h, self.conv2.conv.weight, self.conv2.conv.bias,
-                                  norm_eps=self.norm2.eps)
+            y, s2 = ops.conv3d_k3(_act_for_conv2(h, s1, slope), self.conv2.conv.weight,
+                                  self.conv2.conv.bias, norm_eps=self.norm2.eps)
             return ops.norm_act(y, s2, slope=slope, out=y if out is None else out)
         return _into(self._forward_slow(inp), out)
 

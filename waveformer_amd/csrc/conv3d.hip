@@ -48,14 +48,20 @@ struct Conv3Args {
   double* stats;      // (B, Cout, 2) fp64 {sum, sum of squares} accumulator or nullptr: the
                       // InstanceNorm statistics of the output, fused into the epilogue
   int zfirst;         // tile order: z fastest (1) or x fastest (0)
+  const uint16_t* xh; // XH kernels: the input as fp16 (the operands WF_PREC_FP16 stages; same
+                      // positions / ldx as x)
 };
 
 // RW output rows per wave (wave w: rows w, w + 4, ...): RW = 2 halves the weight-fragment LDS
 // reads per MFMA and the halo staging per output (non-split modes; the split's registers
 // do not allow it)
-template <int CO_T, int NT, int P, bool PIPE = false, int RW = 1>
+// XH: the input is already fp16 in HBM (written by the producing norm_act with the same
+// round-to-nearest-even conversion this kernel's fp16 staging applies, so the operands are
+// bitwise those of the fp32 input): half the staging bytes, no convert
+template <int CO_T, int NT, int P, bool PIPE = false, int RW = 1, bool XH = false>
 __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
+  static_assert(!XH || P == PREC_FP16, "fp16 input only with fp16 operands");
   constexpr int TX = 16 * NT, TY = 4 * RW, HX = TX + 2, HY = TY + 2;
   constexpr int NPOS = 3 * HY * HX;
   constexpr int PS = kConvCC;                       // bf16 per position per plane
@@ -149,15 +155,22 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   // packed global layout is fragment-major too: [step][plane][Cout/16][64][8]
   const int64_t cblk = a.Cout / 16;
 
-  f32x4 sa[NJ];
+  f32x4 sa[XH ? 1 : NJ];
+  bf16x4 sah[XH ? NJ : 1];
   bf16x8 sw[NW];
   auto fetch = [&](int ch) {
     // channels past Cin (the last chunk when Cin % 8 != 0) read channel 0 instead: the
     // address stays inside the tensor, commit() zeroes the value
     const int c = ch * kConvCC + 4 * q;
-    const float* xs = a.x + (c < a.Cin ? c : 0);
+    if constexpr (XH) {
+      const uint16_t* xs = a.xh + (c < a.Cin ? c : 0);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) sa[j] = *reinterpret_cast<const f32x4*>(xs + goff[j]);
+      for (int j = 0; j < NJ; ++j) sah[j] = *reinterpret_cast<const bf16x4*>(xs + goff[j]);
+    } else {
+      const float* xs = a.x + (c < a.Cin ? c : 0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) sa[j] = *reinterpret_cast<const f32x4*>(xs + goff[j]);
+    }
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const int i = min(tid + 256 * w, NFRAG * 64 - 1);
@@ -174,7 +187,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
     for (int j = 0; j < NJ; ++j) {
       const int pos = p0 + PSTEP * j;
       if (j == NJ - 1 && pos >= NPOS) break;
-      f32x4 v = sa[j];
+      if constexpr (XH) {
+        bf16x4 h = sah[j];
+        if (!cok || !((gmask >> j) & 1u)) h = bf16x4{0, 0, 0, 0};
+        *reinterpret_cast<bf16x4*>(s_hi + pos * PS + 4 * q) = h;
+        continue;
+      }
+      f32x4 v = sa[XH ? 0 : j];
       if (!cok || !((gmask >> j) & 1u)) v = f32x4{0, 0, 0, 0};
       bf16x4 h, l;
 #pragma unroll
@@ -358,7 +377,8 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   static const int zf = getenv("WF_CONV_ZFIRST") ? atoi(getenv("WF_CONV_ZFIRST")) : 1;
   a.zfirst = zf;
   {
-    auto kern = prec == PREC_SPLIT  ? conv3d_k3_kernel<CO_T, NT, PREC_SPLIT, false, 1>
+    auto kern = a.xh                ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, false, RW, true>
+                : prec == PREC_SPLIT  ? conv3d_k3_kernel<CO_T, NT, PREC_SPLIT, false, 1>
                 : prec == PREC_FP16 ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, false, RW>
                                     : conv3d_k3_kernel<CO_T, NT, PREC_BF16, false, RW>;
     set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
@@ -428,10 +448,10 @@ extern "C" int wf_conv3d_k3_pack_f16(const float* w, uint16_t* packed, int64_t C
   return conv_pack(w, packed, Cin, Cout, 1, stream);
 }
 
-extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed,
-                                const float* bias, float* out, int64_t ldo, double* stats_acc,
-                                int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H,
-                                int64_t W, int precision, void* stream) {
+static int conv3_fwd(const float* x, const uint16_t* xh, int64_t ldx, const uint16_t* w_packed,
+                     const float* bias, float* out, int64_t ldo, double* stats_acc, int64_t B,
+                     int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W, int precision,
+                     void* stream) {
   WF_REQUIRE(B >= 1 && D >= 1 && H >= 1 && W >= 1, "empty tensor");
   WF_REQUIRE(Cin >= 4 && Cin % 4 == 0 && ldx >= Cin && ldx % 4 == 0,
              "Cin must be a positive multiple of 4 with ldx >= Cin, ldx % 4 == 0");
@@ -440,11 +460,12 @@ extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_p
   WF_REQUIRE(B * D * H * W < ((int64_t)1 << 31) && B * D * H * W * ldx < ((int64_t)1 << 32),
              "input too large (32-bit element offsets)");
   WF_REQUIRE(valid_prec(precision), "unknown precision");
-  WF_REQUIRE_PTR(x);
+  WF_REQUIRE(x || xh, "x is NULL");
   WF_REQUIRE_PTR(w_packed);
   WF_REQUIRE_PTR(out);
   Conv3Args a{};
   a.x = x;
+  a.xh = xh;
   a.w = w_packed;
   a.bias = bias;
   a.out = out;
@@ -465,4 +486,23 @@ extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_p
   if (W > 32) return co3 ? launch_conv3<3, 4>(a, precision, s) : launch_conv3<1, 4>(a, precision, s);
   if (W > 16) return co3 ? launch_conv3<3, 2>(a, precision, s) : launch_conv3<1, 2>(a, precision, s);
   return co3 ? launch_conv3<3, 1>(a, precision, s) : launch_conv3<1, 1>(a, precision, s);
+}
+
+extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed,
+                                const float* bias, float* out, int64_t ldo, double* stats_acc,
+                                int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H,
+                                int64_t W, int precision, void* stream) {
+  WF_REQUIRE_PTR(x);
+  return conv3_fwd(x, nullptr, ldx, w_packed, bias, out, ldo, stats_acc, B, Cin, Cout, D, H, W,
+                   precision, stream);
+}
+
+extern "C" int wf_conv3d_k3_fwd_xh(const uint16_t* x, int64_t ldx, const uint16_t* w_packed_f16,
+                                   const float* bias, float* out, int64_t ldo, double* stats_acc,
+                                   int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H,
+                                   int64_t W, void* stream) {
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE(((uintptr_t)x & 7) == 0, "x must be 8-byte aligned");
+  return conv3_fwd(nullptr, x, ldx, w_packed_f16, bias, out, ldo, stats_acc, B, Cin, Cout, D, H,
+                   W, PREC_FP16, stream);
 }

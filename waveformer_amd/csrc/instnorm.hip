@@ -100,6 +100,30 @@ __global__ __launch_bounds__(256) void norm_act_kernel(
   }
 }
 
+// norm + LeakyReLU (no residual) stored as fp16 (round to nearest even): the input of the next
+// WF_PREC_FP16 convolution, which stages exactly these operands (conv3d_k3_kernel<.., XH>)
+__global__ __launch_bounds__(256) void norm_act_h_kernel(
+    const float* __restrict__ a, int64_t lda, const float* __restrict__ sa,
+    uint16_t* __restrict__ out, int64_t ldo, int C, int64_t P, int64_t chunk, float slope) {
+  const int C4 = C >> 2;
+  const int R = 256 / C4;
+  const int row = threadIdx.x / C4, g = threadIdx.x - row * C4;
+  if (row >= R) return;
+  const int b = blockIdx.y, c = 4 * g;
+  const f32x4 ma = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b) * C + c);
+  const f32x4 ra = *reinterpret_cast<const f32x4*>(sa + (int64_t)(2 * b + 1) * C + c);
+  const int64_t p0 = (int64_t)blockIdx.x * chunk, p1 = min(P, p0 + chunk);
+#pragma unroll 2
+  for (int64_t p = p0 + row; p < p1; p += R) {
+    const int64_t pos = (int64_t)b * P + p;
+    f32x4 v = (*reinterpret_cast<const f32x4*>(a + pos * lda + c) - ma) * ra;
+    bf16x4 h;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h[j] = (short)f2h(v[j] >= 0.f ? v[j] : v[j] * slope);
+    *reinterpret_cast<bf16x4*>(out + pos * ldo + c) = h;
+  }
+}
+
 // (chunks, B) grid of the streaming elementwise kernels: ~4096 workgroups, chunk a multiple of
 // the R rows a workgroup covers per step
 static void stream_grid(int64_t B, int64_t P, int64_t C, int64_t* chunks, int64_t* chunk) {
@@ -514,4 +538,21 @@ extern "C" int wf_norm_act_lin_cl(const float* a, int64_t lda, const float* stat
 #undef WF_NAL
   }
   return check_launch("wf_norm_act_lin_cl");
+}
+
+extern "C" int wf_norm_act_h_cl(const float* a, int64_t lda, const float* stats_a, uint16_t* out,
+                                int64_t ldo, int64_t B, int64_t C, int64_t P, float slope,
+                                void* stream) {
+  WF_REQUIRE(B >= 1 && P >= 1, "empty tensor");
+  WF_REQUIRE(C >= 4 && C % 4 == 0 && C <= 1024 && lda >= C && lda % 4 == 0 && ldo >= C &&
+             ldo % 4 == 0, "C must be a multiple of 4 in [4, 1024], every ld >= C, % 4 == 0");
+  WF_REQUIRE_PTR(a);
+  WF_REQUIRE_PTR(stats_a);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE(((uintptr_t)out & 7) == 0, "out must be 8-byte aligned");
+  int64_t chunks, chunk;
+  stream_grid(B, P, C, &chunks, &chunk);
+  hipLaunchKernelGGL(norm_act_h_kernel, dim3((unsigned)chunks, (unsigned)B), dim3(256), 0,
+                     (hipStream_t)stream, a, lda, stats_a, out, ldo, (int)C, P, chunk, slope);
+  return check_launch("wf_norm_act_h_cl");
 }

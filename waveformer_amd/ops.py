@@ -732,7 +732,10 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor
     """Conv3d(k=3, stride 1, padding 1) of an NCDHW-shaped fp32 tensor on the MFMA implicit-GEMM
     kernel; the result is channels_last_3d (or written into `out`, a channel-last view).
     With `norm_eps` it returns (out, stats): the InstanceNorm (B, 2, C) {mean, rstd} of the
-    output, accumulated in the conv's epilogue."""
+    output, accumulated in the conv's epilogue.  An fp16 channel-last x (from norm_act_h) runs
+    the fp16-input kernel (wf_conv3d_k3_fwd_xh; fp16 precision only)."""
+    if x.dtype == torch.float16:
+        return _conv3d_k3_xh(x, weight, bias, out, norm_eps)
     _check(x, "x", contiguous=False)
     x = to_cl(x)
     B, Cin, D, H, W = x.shape
@@ -759,6 +762,50 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor
     _lib.call("wf_instnorm_finalize", acc.data_ptr(), stats.data_ptr(), B, Cout, D * H * W,
               float(norm_eps), _stream())
     return out, stats
+
+
+def _conv3d_k3_xh(x, weight, bias, out, norm_eps):
+    if _prec() != FP16:
+        raise ValueError("conv3d_k3: an fp16 input needs the fp16 precision")
+    ld = cl_ld(x)
+    if ld is None or not x.is_cuda:
+        raise ValueError("conv3d_k3: fp16 input must be a channel-last CUDA tensor")
+    B, Cin, D, H, W = x.shape
+    Cout = weight.shape[0]
+    if tuple(weight.shape) != (Cout, Cin, 3, 3, 3):
+        raise ValueError(f"conv3d_k3: weight {tuple(weight.shape)} does not fit Cin={Cin}")
+    if bias is not None:
+        _check(bias, "bias")
+    if out is None:
+        out = empty_cl(B, Cout, D, H, W, x.device)
+    ldo = cl_ld(out)
+    if ldo is None or tuple(out.shape) != (B, Cout, D, H, W):
+        raise ValueError("conv3d_k3: out must be a channel-last (B, Cout, D, H, W) tensor")
+    acc = None
+    if norm_eps is not None:
+        acc = torch.zeros((B, Cout, 2), dtype=torch.float64, device=x.device)
+    _lib.call("wf_conv3d_k3_fwd_xh", x.data_ptr(), ld, conv3d_k3_packed(weight, FP16).data_ptr(),
+              _ptr(bias), out.data_ptr(), ldo, _ptr(acc), B, Cin, Cout, D, H, W, _stream())
+    if acc is None:
+        return out
+    stats = torch.empty((B, 2, Cout), dtype=torch.float32, device=x.device)
+    _lib.call("wf_instnorm_finalize", acc.data_ptr(), stats.data_ptr(), B, Cout, D * H * W,
+              float(norm_eps), _stream())
+    return out, stats
+
+
+def norm_act_h(a: torch.Tensor, stats_a: torch.Tensor, slope: float = 0.01) -> torch.Tensor:
+    """act((a - mean) * rstd) as a dense channel-last fp16 tensor (wf_norm_act_h_cl): the input
+    of an fp16 conv3d_k3, rounded exactly as that conv would round the fp32 values."""
+    lda = cl_ld(a)
+    if lda is None:
+        raise ValueError("norm_act_h: channel-last input expected")
+    B, C, D, H, W = a.shape
+    out = torch.empty((B, C, D, H, W), dtype=torch.float16, device=a.device,
+                      memory_format=torch.channels_last_3d)
+    _lib.call("wf_norm_act_h_cl", a.data_ptr(), lda, stats_a.data_ptr(), out.data_ptr(), C, B, C,
+              D * H * W, float(slope), _stream())
+    return out
 
 
 def conv1x1_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None
