@@ -43,7 +43,11 @@ __global__ __launch_bounds__(256) void upsample_cl_kernel(const float* __restric
                                                           int h, int w, int D, int H, int W,
                                                           int ac) {
   const int C4 = C >> 2;
-  const int row = blockIdx.x;  // (b * D + z) * H + y
+  // XCD-contiguous row order (workgroups are dealt round-robin over the 8 XCDs): the
+  // neighbouring output rows that read the same source rows run on one XCD and meet in its L2
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  const int row = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) +
+                  (blockIdx.x >> 3);  // (b * D + z) * H + y
   const int y = row % H, bz = row / H;
   const int z = bz % D, b = bz / D;
   const Src1 sz = src_index(z, d, D, ac), sy = src_index(y, h, H, ac);
@@ -152,6 +156,53 @@ extern "C" int wf_resample_trilinear_cf(const float* in, int64_t ldc, int64_t C,
   return check_launch("wf_resample_trilinear_cf");
 }
 
+// The same resampling with the z / y interpolation done once per source row: the workgroup
+// (one output row) blends its 4 source rows into one (w, C) row in LDS -- each source value
+// read once per workgroup instead of 8 gathered 16-B loads per output -- and each output then
+// reads its two x neighbours from LDS.  Same arithmetic order as upsample_cl_kernel
+// (sy.l0 * (sx...) is not reassociated: z / y first here), so results agree to rounding only.
+template <bool ADD>
+__global__ __launch_bounds__(256) void upsample_cl_lds_kernel(const float* __restrict__ in,
+                                                              float* __restrict__ out, int C,
+                                                              int d, int h, int w, int D, int H,
+                                                              int W, int ac) {
+  extern __shared__ __attribute__((aligned(16))) float rowbuf[];  // [w][C]
+  const int C4 = C >> 2;
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  const int row = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) +
+                  (blockIdx.x >> 3);  // (b * D + z) * H + y
+  const int y = row % H, bz = row / H;
+  const int z = bz % D, b = bz / D;
+  const Src1 sz = src_index(z, d, D, ac), sy = src_index(y, h, H, ac);
+  const float* base = in + (int64_t)b * ((int64_t)d * h * w * C);
+  const float* r00 = base + ((int64_t)sz.i0 * h + sy.i0) * w * C;
+  const float* r01 = base + ((int64_t)sz.i0 * h + sy.i1) * w * C;
+  const float* r10 = base + ((int64_t)sz.i1 * h + sy.i0) * w * C;
+  const float* r11 = base + ((int64_t)sz.i1 * h + sy.i1) * w * C;
+  const int ns = w * C4;
+  for (int i = threadIdx.x; i < ns; i += blockDim.x) {
+    const int o = 4 * i;  // (x' * C + c)
+    auto at = [&](const float* r) { return *reinterpret_cast<const f32x4*>(r + o); };
+    const f32x4 v = sz.l0 * (sy.l0 * at(r00) + sy.l1 * at(r01)) +
+                    sz.l1 * (sy.l0 * at(r10) + sy.l1 * at(r11));
+    *reinterpret_cast<f32x4*>(rowbuf + o) = v;
+  }
+  __syncthreads();
+  float* orow = out + (int64_t)row * W * C;
+  const int n = W * C4;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int x = i / C4;
+    const int c = 4 * (i - x * C4);
+    const Src1 sx = src_index(x, w, W, ac);
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(rowbuf + sx.i0 * C + c);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(rowbuf + sx.i1 * C + c);
+    f32x4 v = sx.l0 * a0 + sx.l1 * a1;
+    f32x4* op = reinterpret_cast<f32x4*>(orow + (int64_t)x * C + c);
+    if (ADD) v = *op + v;
+    *op = v;
+  }
+}
+
 static int upsample_cl_launch(const float* in, float* out, int64_t B, int64_t C, int64_t d,
                               int64_t h, int64_t w, int64_t D, int64_t H, int64_t W,
                               int align_corners, bool add, void* stream, const char* who) {
@@ -161,6 +212,15 @@ static int upsample_cl_launch(const float* in, float* out, int64_t B, int64_t C,
              "output too large");
   WF_REQUIRE_PTR(in);
   WF_REQUIRE_PTR(out);
+  const size_t lds = (size_t)w * C * sizeof(float);
+  static const bool gather = getenv("WF_UPSAMPLE_GATHER") != nullptr;  // A/B: the old kernel
+  if (lds <= 64 * 1024 && !gather) {
+    auto k = add ? upsample_cl_lds_kernel<true> : upsample_cl_lds_kernel<false>;
+    hipLaunchKernelGGL(k, dim3((unsigned)(B * D * H)), dim3(256), lds, (hipStream_t)stream, in,
+                       out, (int)C, (int)d, (int)h, (int)w, (int)D, (int)H, (int)W,
+                       align_corners);
+    return check_launch(who);
+  }
   auto k = add ? upsample_cl_kernel<true> : upsample_cl_kernel<false>;
   hipLaunchKernelGGL(k, dim3((unsigned)(B * D * H)), dim3(256), 0, (hipStream_t)stream, in, out,
                      (int)C, (int)d, (int)h, (int)w, (int)D, (int)H, (int)W, align_corners);
