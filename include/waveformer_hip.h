@@ -287,6 +287,13 @@ int wf_upsample_trilinear_add_cl(const float* in, float* out, int64_t B, int64_t
  * into the NCDHW out (B, N, P).  K % 4 == 0, K <= 120, N <= 16; fp32 FMAs.                  */
 int wf_conv1x1_head_cl(const float* x, int64_t ldx, const float* weight, const float* bias,
                        float* out, int64_t B, int64_t K, int64_t N, int64_t P, void* stream);
+/* Depthwise Conv3d(C, C, 3, padding 1, groups C) + bias of a dense channel-last fp32 tensor
+ * (ProjectionUpsample.conv1, wave_helper.py:43-46) with the per-(sample, channel) fp64 {sum, sum
+ * of squares} of its output accumulated in the epilogue into stats_acc (B, C, 2) (zeroed here)
+ * -- the GroupNorm(C, C) statistics of wave_helper.py:60 without a second pass.  C % 32 == 0. */
+int wf_dwconv3d_stats_cl(const float* in, const float* w, const float* bias, float* out,
+                         double* stats_acc, int64_t B, int64_t C, int64_t D, int64_t H,
+                         int64_t W, void* stream);
 
 /* Predictor.predict_raw_probability (light_training/prediction.py:35-63): channel-first
  * (C, d, h, w) fp32 (channel stride ldc) -> (C, D, H, W) per channel

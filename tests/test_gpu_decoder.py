@@ -471,3 +471,22 @@ def test_conv3d_k3_fp16_input_bitwise(B, C_, S):
         with ops.precision("fp16"):
             got = blk(a)
     assert C.rel_l2(got, ref) <= 5e-3
+
+
+@pytest.mark.parametrize("B,C_,S", [(2, 64, 12), (1, 96, 9), (1, 32, 17)])
+def test_dwconv3d_fused_channel_stats(B, C_, S):
+    """wf_dwconv3d_stats_cl: the depthwise conv's output (same kernel as wf_dwconv3d_cl, bit
+    for bit) and its per-(sample, channel) mean / rstd from the epilogue vs instnorm_stats of
+    the stored output (fp64 sums both ways)."""
+    from waveformer_amd import ops
+    cl = torch.channels_last_3d
+    x = seeded_randn((B, C_, S, S, S), 97).cuda().contiguous(memory_format=cl)
+    w = seeded_randn((C_, 1, 3, 3, 3), 98).cuda() * 0.2
+    b = seeded_randn((C_,), 99).cuda()
+    y0 = ops.dwconv3d_cl(x, w, b)
+    y1, st = ops.dwconv3d_cl(x, w, b, norm_eps=1e-5)
+    assert torch.equal(y0, y1)
+    ref = ops.instnorm_stats(y1, 1e-5)
+    assert C.rel_l2(st, ref) <= 1e-6
+    want = F.conv3d(x.contiguous(), w, b, padding=1, groups=C_)
+    assert C.rel_l2(y1, want) <= 1e-6

@@ -226,7 +226,8 @@ struct Store2<uint16_t> {
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv3d_kernel(
     const T* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias,
-    T* __restrict__ out, float* __restrict__ pstats, int B, int Hd, int D, int H, int W, int ZS) {
+    T* __restrict__ out, float* __restrict__ pstats, int B, int Hd, int D, int H, int W, int ZS,
+    double* __restrict__ cstats) {
   constexpr int CH = DW_CH, TX = DW_TX, TY = DW_TY;
   static_assert(CH == DW_STAT_GROUP, "one statistics group per workgroup channel chunk");
   static_assert(TX * (CH / 2) == 256, "one thread per (column, channel pair)");
@@ -293,6 +294,9 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
 #pragma unroll
   for (int o = 0; o < TY; ++o) accA[o] = accB[o] = accC[o] = f32x2{0.f, 0.f};
   const int xo = x0 + xi;
+  // cstats: per-(sample, channel) sum and sum of squares of the stored outputs (InstanceNorm /
+  // GroupNorm(C, C) statistics of the next layer), fp64 per thread
+  double cs0 = 0.0, cs1 = 0.0, cq0 = 0.0, cq1 = 0.0;
   fetch(z0 - 1);
   commit(0);
   __syncthreads();
@@ -340,6 +344,13 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
           if (yo < H) {
             const int64_t pos = (((int64_t)b * D + zo) * H + yo) * W + xo;
             Store2<T>::put(out + pos * Hd + c0 + 2 * cp, r1[o]);
+            if (cstats) {
+              const double a0 = (double)r1[o].x, a1 = (double)r1[o].y;
+              cs0 += a0;
+              cs1 += a1;
+              cq0 += a0 * a0;
+              cq1 += a1 * a1;
+            }
             if (pstats && cp == 0)
               *reinterpret_cast<float2*>(pstats + (pos * ncc + cc) * 2) = float2{mu[o], m2[o]};
           }
@@ -356,10 +367,27 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
     __syncthreads();
     buf ^= 1;
   }
+  if (cstats) {  // the 16 columns of a channel pair, then one fp64 atomic per (channel, moment)
+    double* red = reinterpret_cast<double*>(&pl[0][0]);  // [TX][CH / 2][4]
+    double* r = red + (xi * (CH / 2) + cp) * 4;
+    r[0] = cs0;
+    r[1] = cs1;
+    r[2] = cq0;
+    r[3] = cq1;
+    __syncthreads();
+    if (tid < CH * 2) {
+      const int pc = tid >> 2, mom = tid & 3;  // mom: {sum c, sum c+1, sq c, sq c+1}
+      double t = 0.0;
+#pragma unroll
+      for (int xx = 0; xx < TX; ++xx) t += red[(xx * (CH / 2) + pc) * 4 + mom];
+      const int c = c0 + 2 * pc + (mom & 1);
+      atomicAdd(cstats + ((int64_t)b * Hd + c) * 2 + (mom >> 1), t);
+    }
+  }
 }
 
 int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, float* pstats,
-                    int B, int Hd, int D, int H, int W, int prec, hipStream_t s) {
+                    int B, int Hd, int D, int H, int W, int prec, hipStream_t s, double* cstats) {
   if (Hd % DW_CH != 0) return fail(WF_E_SHAPE, "dwconv3d: hidden width must be a multiple of 32");
   // z segment: enough workgroups to fill 256 CUs ~8 deep, but long enough that the two halo
   // planes per segment stay a small overhead
@@ -370,11 +398,11 @@ int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, f
   if (store32(prec))
     hipLaunchKernelGGL((dwconv3d_kernel<float>), dim3((unsigned)blocks), dim3(256), 0, s,
                        reinterpret_cast<const float*>(in), w, b, reinterpret_cast<float*>(out),
-                       pstats, B, Hd, D, H, W, ZS);
+                       pstats, B, Hd, D, H, W, ZS, cstats);
   else
     hipLaunchKernelGGL((dwconv3d_kernel<uint16_t>), dim3((unsigned)blocks), dim3(256), 0, s,
                        reinterpret_cast<const uint16_t*>(in), w, b,
-                       reinterpret_cast<uint16_t*>(out), pstats, B, Hd, D, H, W, ZS);
+                       reinterpret_cast<uint16_t*>(out), pstats, B, Hd, D, H, W, ZS, cstats);
   return check_launch("dwconv3d");
 }
 

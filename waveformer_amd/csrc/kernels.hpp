@@ -121,8 +121,10 @@ int launch_dwconv_ln_gelu(const void* in, const float* w, const float* b, const 
 // ---- depthwise 3^3 conv + bias only (the LayerNorm + GELU run in the next GEMM's loader);
 // returns 0 on success, WF_E_SHAPE if the shape is not covered (Hd % 32 != 0)
 // pstats (optional): (M, Hd / 32, 2) {mean, M2} of each 32-channel group of every output row
+// cstats (optional): zeroed (B, Hd, 2) fp64 {sum, sum of squares} of the outputs per channel
 int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, float* pstats,
-                    int B, int Hd, int D, int H, int W, int prec, hipStream_t s);
+                    int B, int Hd, int D, int H, int W, int prec, hipStream_t s,
+                    double* cstats = nullptr);
 constexpr int DW_STAT_GROUP = 32;
 // ---- CCF_FFN back half fused (ffn_dwfc.hip): dwconv + bias + LN2 + GELU + fc + bias + the
 // Block's Q4 residual, for C = 48, hidden = 192 (h1 fp32 for PREC_SPLIT, bf16 for PREC_BF16)

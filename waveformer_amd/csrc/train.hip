@@ -1021,6 +1021,22 @@ extern "C" int wf_dwconv3d_cl(const float* in, const float* w, const float* bias
   return check_launch("wf_dwconv3d_cl");
 }
 
+extern "C" int wf_dwconv3d_stats_cl(const float* in, const float* w, const float* bias,
+                                    float* out, double* stats_acc, int64_t B, int64_t C,
+                                    int64_t D, int64_t H, int64_t W, void* stream) {
+  WF_REQUIRE(C % 32 == 0 && C >= 32, "channels must be a multiple of 32");
+  WF_REQUIRE_PTR(in);
+  WF_REQUIRE_PTR(w);
+  WF_REQUIRE_PTR(bias);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE_PTR(stats_acc);
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(stats_acc, 0, (size_t)(B * C * 2) * sizeof(double), s) != hipSuccess)
+    return check_launch("wf_dwconv3d_stats_cl (memset)");
+  return launch_dwconv3d(in, w, bias, out, nullptr, (int)B, (int)C, (int)D, (int)H, (int)W,
+                         PREC_SPLIT, s, stats_acc);
+}
+
 static int64_t wf_dwconv_wgrad_parts(int64_t positions) {
   int64_t p = cdiv(positions, 512);
   return p > 512 ? 512 : (p < 1 ? 1 : p);

@@ -138,8 +138,13 @@ class ProjectionUpsample(nn.Module):
         P = size[0] * size[1] * size[2]
         xc = ops.to_cl(x)
         dw = self.conv1[1]
-        y = ops.dwconv3d_cl(ops.upsample_cl(xc, size, True), dw.weight, dw.bias)
-        st = ops.instnorm_stats(y, self.norm.eps)                       # (B, 2, C)
+        up = ops.upsample_cl(xc, size, True)
+        if dw.bias is not None and C % 32 == 0:
+            # GroupNorm(C, C) statistics accumulated in the depthwise conv's epilogue
+            y, st = ops.dwconv3d_cl(up, dw.weight, dw.bias, norm_eps=self.norm.eps)
+        else:
+            y = ops.dwconv3d_cl(up, dw.weight, dw.bias)
+            st = ops.instnorm_stats(y, self.norm.eps)                   # (B, 2, C)
         scale = st[:, 1] * self.norm.weight                              # (B, C)
         shift = self.norm.bias - st[:, 0] * scale
         w2 = self.conv2.weight.reshape(2 * C, C)

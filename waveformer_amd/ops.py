@@ -869,8 +869,12 @@ def conv1x1_head(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Ten
     return out
 
 
-def dwconv3d_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
-    """Depthwise Conv3d(C, C, 3, padding=1, groups=C) of a dense channel-last tensor."""
+def dwconv3d_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                norm_eps: Optional[float] = None):
+    """Depthwise Conv3d(C, C, 3, padding=1, groups=C) of a dense channel-last tensor.  With
+    `norm_eps` (bias given, C % 32 == 0) it returns (out, stats): the (B, 2, C) {mean, rstd} of
+    the output per (sample, channel), accumulated in the conv's epilogue
+    (wf_dwconv3d_stats_cl) -- GroupNorm(C, C) / InstanceNorm statistics without a re-read."""
     x = x if (cl_ld(x) == x.shape[1]) else x.contiguous(memory_format=torch.channels_last_3d)
     B, C, D, H, W = x.shape
     if tuple(weight.shape) != (C, 1, 3, 3, 3):
@@ -879,6 +883,16 @@ def dwconv3d_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tens
     if bias is not None:
         _check(bias, "bias")
     out = empty_cl(B, C, D, H, W, x.device)
+    if norm_eps is not None:
+        if bias is None or C % 32:
+            raise ValueError("dwconv3d_cl: fused statistics need a bias and C % 32 == 0")
+        acc = torch.empty((B, C, 2), dtype=torch.float64, device=x.device)
+        _lib.call("wf_dwconv3d_stats_cl", x.data_ptr(), weight.data_ptr(), bias.data_ptr(),
+                  out.data_ptr(), acc.data_ptr(), B, C, D, H, W, _stream())
+        stats = torch.empty((B, 2, C), dtype=torch.float32, device=x.device)
+        _lib.call("wf_instnorm_finalize", acc.data_ptr(), stats.data_ptr(), B, C, D * H * W,
+                  float(norm_eps), _stream())
+        return out, stats
     _lib.call("wf_dwconv3d_cl", x.data_ptr(), weight.data_ptr(), _ptr(bias), 0, out.data_ptr(),
               B, C, D, H, W, _stream())
     return out
