@@ -1,6 +1,6 @@
 """HIP implicit-GEMM conv3d (ops.conv3d_k3) timing at the decoder's shapes, with the MFMA
 roofline fraction (logical fp32 flops; bf16x3 issues 3 MFMAs per product).
-    python tools/kbench_conv_hip.py [ONLY_INDEX]"""
+    python tools/kbench_conv_hip.py [ONLY_INDEX]      (XH=1: fp16 input, with WAVEFORMER_PRECISION=fp16)"""
 import os
 import sys
 import time
@@ -23,6 +23,8 @@ for i, (B, cin, cout, s) in enumerate(SHAPES):
     if only is not None and i != only:
         continue
     x = torch.randn(B, cin, s, s, s, device="cuda").contiguous(memory_format=torch.channels_last_3d)
+    if os.environ.get("XH"):  # fp16 input in HBM (wf_conv3d_k3_fwd_xh; fp16 precision only)
+        x = x.half().contiguous(memory_format=torch.channels_last_3d)
     w = torch.randn(cout, cin, 3, 3, 3, device="cuda") * (cin * 27) ** -0.5
     ops.conv3d_k3(x, w)
     torch.cuda.synchronize()
