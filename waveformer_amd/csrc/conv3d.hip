@@ -478,10 +478,13 @@ static int conv3_fwd(const float* x, const uint16_t* xh, int64_t ldx, const uint
   a.stats = stats_acc;
   hipStream_t s = (hipStream_t)stream;
   const bool co3 = Cout % 48 == 0;
-  // two output rows per wave (WF_CONV_RW=2, non-split modes, W > 32): measured slower, the
-  // larger halo's prefetch registers spill (96->48 at 128^3 fp16: 1.82 vs 1.73 ms)
-  static const int rw = getenv("WF_CONV_RW") ? atoi(getenv("WF_CONV_RW")) : 1;
-  if (W > 32 && precision != PREC_SPLIT && rw == 2 && co3)
+  // two output rows per wave (8-row tiles: halo 10/8 rows instead of 6/4), non-split modes,
+  // W > 32.  Default for fp16 input only: with fp32 input the larger halo's prefetch registers
+  // spill (96->48 at 128^3 fp16: 1.82 vs 1.73 ms); the fp16-input variant fits (240 VGPRs) and
+  // runs 48->48 at 192^3 in 2.42 vs 2.52 ms (profiles/r3_conv/rw2_xh_ab_192.txt).
+  // WF_CONV_RW=1 / 2 forces one or the other
+  static const int rw = getenv("WF_CONV_RW") ? atoi(getenv("WF_CONV_RW")) : 0;
+  if (W > 32 && precision != PREC_SPLIT && co3 && (rw == 2 || (rw == 0 && xh)))
     return launch_conv3<3, 4, 2>(a, precision, s);
   if (W > 32) return co3 ? launch_conv3<3, 4>(a, precision, s) : launch_conv3<1, 4>(a, precision, s);
   if (W > 16) return co3 ? launch_conv3<3, 2>(a, precision, s) : launch_conv3<1, 2>(a, precision, s);
