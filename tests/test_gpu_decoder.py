@@ -351,9 +351,11 @@ def test_convtranspose2_gemm_subvoxel_epilogue(B, Cin, Cout, d, h, w):
 
 
 def test_unetr_up_block_skip_in_place():
-    """UnetrUpBlock's fast path with the skip produced into its concat buffer (ops.cl_parent,
-    as the backbone's encoder1 does) and with a free-standing skip: the same result as the
-    reference composition torch.cat((ConvTranspose3d(x), skip), 1) -> conv block."""
+    """UnetrUpBlock's fast path with the skip produced into its concat buffer (opt-in
+    `skip_in_place=True`, as the backbone's encoder1 does) and with a free-standing skip: the
+    same result as the reference composition torch.cat((ConvTranspose3d(x), skip), 1) -> conv
+    block.  Without the flag a skip that merely views such a buffer leaves the caller's storage
+    untouched."""
     from waveformer_amd import ops
     from waveformer_amd.blocks import UnetrUpBlock
     torch.manual_seed(0)
@@ -365,13 +367,17 @@ def test_unetr_up_block_skip_in_place():
     view = buf[:, 8:]
     assert ops.cl_parent(view, 8) is buf or ops.cl_parent(view, 8).data_ptr() == buf.data_ptr()
     with torch.no_grad():
-        got_inplace = blk(x, view)
+        before = buf.clone()
+        got_view = blk(x, view)                       # no opt-in: buf must not be written
+        assert torch.equal(buf, before)
+        got_inplace = blk(x, view, skip_in_place=True)
         got_free = blk(x, skip)
         tc = blk.transp_conv.conv
         ref_in = torch.cat((tc(x), skip), 1)
         want = blk.conv_block(ref_in)
     assert C.rel_l2(got_free, want) <= 1e-5
     assert C.rel_l2(got_inplace, want) <= 1e-5
+    assert C.rel_l2(got_view, want) <= 1e-5
 
 
 def test_norm_act_linear_residual_fold():

@@ -72,3 +72,56 @@ def test_dicece_loss_vs_reference_monai():
     loss.backward()
     assert abs(loss.item() - C.g("dicece__loss").item()) <= 1e-6
     assert C.rel_l2(logits.grad, C.g("dicece__grad")) <= 1e-6
+
+
+def test_precision_scopes_are_thread_local():
+    """an op-group override (fp16 policy -> bf16x3 for 'skip_conv') inside one
+    thread's forward must not change the precision another thread's forward sees, and
+    overlapping scopes of two threads must not restore each other's value."""
+    import threading
+    default = ops.get_precision()
+    inside, outside = threading.Event(), threading.Event()
+    seen = {}
+
+    def a():
+        with ops.precision("fp16"):
+            with ops.op_precision("skip_conv"):
+                seen["a_inner"] = ops.get_precision()
+                inside.set()
+                outside.wait(10)
+            seen["a_after"] = ops.get_precision()
+
+    def b():
+        inside.wait(10)
+        with ops.precision("fp16"):
+            seen["b"] = ops.get_precision()
+            seen["b_conv"] = ops.op_prec("conv")
+        outside.set()
+
+    ta, tb = threading.Thread(target=a), threading.Thread(target=b)
+    ta.start(), tb.start()
+    ta.join(20), tb.join(20)
+    assert seen == {"a_inner": "bf16x3", "b": "fp16", "b_conv": ops.PRECISIONS["fp16"],
+                    "a_after": "fp16"}
+    assert ops.get_precision() == default
+    with ops.precision("fp16"):
+        assert ops.op_prec("attn") == ops.PRECISIONS["bf16x3"]
+        with ops.op_precision("conv"):
+            assert ops.get_precision() == "fp16"
+    assert ops.get_precision() == default
+
+
+def test_index_formula_tracks_in_place_writes():
+    """an in-place write to relative_position_index after the formula check must
+    turn the in-kernel formula off (the forward then reads the dense bias built from the
+    buffer); loading a state_dict re-validates."""
+    a = NM.Attention(48, num_heads=3, qkv_bias=True, window_size=4)
+    assert a._formula_valid()
+    sd = {k: v.clone() for k, v in a.state_dict().items()}
+    a.relative_position_index.fill_(0)
+    assert not a._formula_valid()
+    a.load_state_dict(sd)
+    assert a._formula_valid()
+    sd["relative_position_index"] = torch.zeros_like(sd["relative_position_index"])
+    a.load_state_dict(sd)
+    assert not a._formula_valid()

@@ -42,3 +42,29 @@ def test_shape_errors_are_reported_without_a_gpu():
     with pytest.raises(RuntimeError, match="wf_proj_out_fwd"):
         _lib.call("wf_proj_out_fwd", None, None, 1, 1e-5, 1, 6, 8, None)
     assert _lib.query("wf_window_attention_workspace_bytes", 1, 48, 32, 32, 32, 0) >= 32768 * 48 * 8
+
+
+def test_no_packed_fp32_in_device_code(tmp_path):
+    """the library is built without VOP3P packed-FP32 instructions (the gfx950
+    hazard behind round 2's stage-2 corruption).  Disassemble every gfx950 code object embedded
+    in the shipped .so and fail on any v_pk_{fma,mul,add}_f32, so a build that drops the
+    Makefile's device feature flag cannot ship."""
+    import glob
+    import shutil
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    so = tmp_path / "lib.so"
+    shutil.copy(_lib.LIB_PATH, so)
+    subprocess.run([objdump, "--offloading", str(so)], cwd=tmp_path, check=True,
+                   capture_output=True)
+    objs = sorted(glob.glob(str(tmp_path / "lib.so.*gfx950*")))
+    assert objs, "no gfx950 code object in the library"
+    bad = []
+    for o in objs:
+        dis = subprocess.run([objdump, "-d", o], check=True, capture_output=True, text=True).stdout
+        for line in dis.splitlines():
+            if re.search(r"\bv_pk_(fma|mul|add)_f32\b", line):
+                bad.append(f"{os.path.basename(o)}: {line.strip()}")
+    assert not bad, "packed-FP32 instructions in device code:\n" + "\n".join(bad[:20])

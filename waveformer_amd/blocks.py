@@ -269,17 +269,21 @@ class UnetrUpBlock(nn.Module):
         self.conv_block = cls(spatial_dims, 2 * out_channels, out_channels, kernel_size, 1,
                               norm_name)
 
-    def forward(self, inp, skip):
+    def forward(self, inp, skip, skip_in_place: bool = False):
+        """`skip_in_place=True` (the backbone's decoder1 only): `skip` is channels [Cout, ...)
+        of a channel-last buffer the caller allocated for this block's concatenation, so the
+        transposed conv writes channels [0, Cout) of that same buffer.  Without the flag the
+        skip is never written through, whatever storage it views."""
         tc = self.transp_conv.conv
         if (_fast_ok(inp, self) and type(tc) is nn.ConvTranspose3d and tc.kernel_size == (2, 2, 2)
                 and tc.stride == (2, 2, 2) and tc.padding == (0, 0, 0)
                 and tc.output_padding == (0, 0, 0) and tc.groups == 1 and tc.dilation == (1, 1, 1)):
-            return self.conv_block(self._upsample_cat(inp, skip, tc))
+            return self.conv_block(self._upsample_cat(inp, skip, tc, skip_in_place))
         out = self.transp_conv(inp)
         return self.conv_block(torch.cat((out, skip), dim=1))
 
     @staticmethod
-    def _upsample_cat(inp, skip, tc):
+    def _upsample_cat(inp, skip, tc, skip_in_place=False):
         """ConvTranspose3d(k=2, s=2) + torch.cat((out, skip), 1) into one channel-last buffer:
         the transposed conv is one fp32 GEMM (positions x Cin) . (Cin x 8 Cout) whose columns
         are the 8 sub-voxels, scattered straight into the buffer's first Cout channels."""
@@ -287,9 +291,9 @@ class UnetrUpBlock(nn.Module):
         Cout = tc.out_channels
         if tuple(skip.shape) != (B, skip.shape[1], 2 * d, 2 * h, 2 * w):
             raise ValueError(f"skip {tuple(skip.shape)} does not match the up-sampled input")
-        # a skip already produced into channels [Cout, ...) of a buffer (the backbone's
-        # encoder1 writes there) needs no copy
-        parent = ops.cl_parent(skip, Cout)
+        # a skip the caller produced into channels [Cout, ...) of the concat buffer it
+        # allocated for this block (the backbone's encoder1, flagged skip_in_place) needs no copy
+        parent = ops.cl_parent(skip, Cout) if skip_in_place else None
         in_place = parent is not None and parent.shape[1] == Cout + skip.shape[1]
         buf = parent if in_place else ops.empty_cl(B, Cout + skip.shape[1], 2 * d, 2 * h, 2 * w,
                                                    inp.device)

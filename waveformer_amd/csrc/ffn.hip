@@ -220,9 +220,10 @@ struct Store2<uint16_t> {
 };
 
 // 256 threads = DW_TX columns x 16 channel PAIRS: each thread owns two adjacent channels of
-// one x column and the TY outputs of that column, so the 27-tap accumulation runs as packed
-// v_pk_fma_f32 on the pair (half the VALU instructions of one-channel-per-thread), and the
-// per-position 32-channel statistics reduce over 16 lanes.
+// one x column and the TY outputs of that column, so the 27-tap accumulation runs on f32x2
+// channel pairs (one 8-B LDS read per tap feeds both; the build has no packed-FP32
+// instructions, DESIGN.md 6.1, so each pair FMA is two v_fma_f32), and the per-position
+// 32-channel statistics reduce over 16 lanes.
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv3d_kernel(
     const T* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias,
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
         const int o = r - ky;  // output row fed by input row r through tap ky
         if (o < 0 || o >= TY) continue;
         const f32x2* w0 = w2 + ky * 3;
-        // one packed FMA per tap into the running sum
+        // one pair FMA per tap into the running sum
         accC[o] = w0[2] * v2 + (w0[1] * v1 + (w0[0] * v0 + accC[o]));
         accB[o] = w0[11] * v2 + (w0[10] * v1 + (w0[9] * v0 + accB[o]));
         accA[o] = w0[20] * v2 + (w0[19] * v1 + (w0[18] * v0 + accA[o]));

@@ -15,10 +15,11 @@
 //   2. every thread owns two channels of one x column (768 threads = 96 channel pairs x 8
 //      columns; 12 waves, the register-file limit at ~160 VGPRs) and scatters each input row
 //      into the three output planes it feeds (rolling
-//      accumulators, packed v_pk_fma_f32 on the channel pair, the 27 weight pairs in
+//      accumulators, f32x2 FMAs on the channel pair (two v_fma_f32: no packed FP32 in this
+//      build), the 27 weight pairs in
 //      registers): 27 FMAs per output and no re-reads of a plane;
 //   3. when an output plane is complete its 32 x 192 h2 tile goes to LDS (25 KB);
-//      16 lanes per position take the LayerNorm statistics, apply LN2 + GELU (packed) and
+//      16 lanes per position take the LayerNorm statistics, apply LN2 + GELU (f32x2 pairs) and
 //      rewrite the row in place as bf16 hi/lo halves (the split MFMA operand);
 //   4. six waves run the fc GEMM as 2 position tiles x 3 output-channel tiles of
 //      v_mfma_f32_16x16x32_bf16 (x3 for the fp32-faithful split), the fc weight hi/lo planes
@@ -224,7 +225,7 @@ __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_ke
         for (int ky = 0; ky < 3; ++ky) {
           const int o = r - ky;
           if (o < 0 || o >= TY) continue;
-          // one packed FMA per tap into the running sum
+          // one pair FMA per tap into the running sum
           const f32x2* w0 = w2 + ky * 3;
           accC[o] = w0[2] * v2 + (w0[1] * v1 + (w0[0] * v0 + accC[o]));
           accB[o] = w0[11] * v2 + (w0[10] * v1 + (w0[9] * v0 + accB[o]));

@@ -12,7 +12,7 @@
 // (gemm_rows writes h1, ffn_dwfc reads it back).  A workgroup owns a 4 x 8 (y, x) tile and
 // marches z through a segment of ZS output planes.  Per input plane p (3 barriers):
 //   S1  every thread (two channels of one x column) scatters the u1 plane p from LDS into the
-//       three output planes it feeds (rolling accumulators, packed FMAs, 27 weight pairs in
+//       three output planes it feeds (rolling accumulators, f32x2 pair FMAs, 27 weight pairs in
 //       registers), exactly as ffn_dwfc;
 //   S2  the haloed 6 x 10 positions of plane p+1 run the pw GEMM on MFMA: wave w takes 16
 //       positions (w & 3) x 64 hidden channels (w >> 2).  Its B operand is built in registers

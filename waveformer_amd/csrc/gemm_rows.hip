@@ -268,8 +268,8 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
       sv_p0 = (((int64_t)b * 2 * g.mD + 2 * z) * (2 * g.mH) + 2 * y) * (2 * g.mW) + 2 * x;
     }
     if (EPI == EPI_LN_GELU) {  // full row in this wave (NCOL == N): the 4 lanes of a position
-      // moments on packed pairs straight off the accumulator registers (v_pk_add / v_pk_fma
-      // on .xy / .zw: no repacking moves, half the instructions of per-element scalar code)
+      // moments on f32x2 pairs straight off the accumulator registers (.xy / .zw: no
+      // repacking moves; scalar v_add / v_fma pairs in this build)
       f32x2 s2 = {0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < NT; ++t) s2 += lo2(acc[t]) + hi2(acc[t]);

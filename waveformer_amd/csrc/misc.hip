@@ -113,7 +113,7 @@ __global__ __launch_bounds__(256) void patch_embed_stream_kernel(
   float* buf0 = slab;
   float* buf1 = slab + R * rowf;
 
-  // thread = (4-channel group, x group): weights as channel pairs, packed FMAs (as above)
+  // thread = (4-channel group, x group): weights as channel pairs, pair FMAs (as above)
   const int C4 = Cout >> 2;
   const int XG = blockDim.x / C4;
   const int cq = tid % C4, xg = tid / C4;
@@ -251,8 +251,9 @@ __global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restric
   }
   if (CIN > 0 && (Cout & 3) == 0) {
     // thread = (4-channel group, x group): the 4 x 8 CIN weights in registers as channel
-    // pairs, packed FMAs (v_pk_fma_f32) over two channel pairs per slab value -- per output
-    // 4 LDS reads and 16 packed FMAs instead of 16 and 32 -- and one 16-byte store
+    // pairs, f32x2 pair FMAs over two channel pairs per slab value -- per output 4 LDS reads
+    // instead of 16 (each pair FMA is two v_fma_f32: no packed FP32 in this build, DESIGN.md
+    // 6.1) -- and one 16-byte store
     constexpr int NK = CIN > 0 ? CIN * 8 : 1;
     const int C4 = Cout >> 2;
     const int XG = blockDim.x / C4;

@@ -64,13 +64,14 @@ __device__ __forceinline__ float gelu_erf(float x) {
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-// the register pairs of an f32x4 (operands of v_pk_*_f32 without repacking)
+// the register pairs of an f32x4 (f32x2 arithmetic on them compiles to scalar v_*_f32 pairs:
+// the build disables packed FP32)
 __device__ __forceinline__ f32x2 lo2(f32x4 v) { return __builtin_shufflevector(v, v, 0, 1); }
 __device__ __forceinline__ f32x2 hi2(f32x4 v) { return __builtin_shufflevector(v, v, 2, 3); }
 // GELU on a pair given HALF its input, hx = x / 2:  GELU(x) = x Phi(x) = hx + |hx| erf(sqrt2 |hx|)
 // (no sign restore: x erf(x / sqrt2) = |x| erf(|x| / sqrt2)).  erf by Abramowitz & Stegun 7.1.26
 // as in gelu_erf, with the polynomial's coefficients negated so 1 - p e is one FMA, and the
-// sqrt2 folded into its constants; the FMA-class steps are packed v_pk_*_f32 ops.  A caller
+// sqrt2 folded into its constants; the FMA-class steps are f32x2 pair ops.  A caller
 // whose input comes out of an affine step (LayerNorm) folds the 1/2 into that step for free.
 __device__ __forceinline__ f32x2 gelu_half2(f32x2 hx) {
   const f32x2 a = f32x2{fabsf(hx.x), fabsf(hx.y)};

@@ -48,8 +48,13 @@ class Attention(nn.Module):
             torch.zeros((2 * window_size - 1) ** 3, num_heads))
         self.register_buffer("relative_position_index", relative_position_index(window_size))
         # the index equals the reference's formula (re-checked when a state_dict is loaded):
-        # the table-bias kernel then evaluates the formula in-kernel instead of reading it
+        # the table-bias kernel then evaluates the formula in-kernel instead of reading it.
+        # Valid for the buffer version it was checked at: an in-place write afterwards
+        # (copy_ / fill_) bumps the version and the forward falls back to the dense bias built
+        # from the buffer's contents (no host sync in the forward).  A device move keeps the
+        # contents and starts the new tensor at version 0, like the checked one.
         self._index_formula = True
+        self._index_version = self.relative_position_index._version
         nn.init.trunc_normal_(self.relative_position_bias_table, std=.02)
         self.softmax = nn.Softmax(dim=-1)
 
@@ -57,6 +62,11 @@ class Attention(nn.Module):
         super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
         self._index_formula = ops.index_is_formula(self.relative_position_index,
                                                    self.window_size)
+        self._index_version = self.relative_position_index._version
+
+    def _formula_valid(self) -> bool:
+        return (self._index_formula
+                and self.relative_position_index._version == self._index_version)
 
     def _check_train(self):
         if self.training and (self.attn_drop.p > 0 or self.proj_drop.p > 0):
@@ -81,7 +91,7 @@ class Attention(nn.Module):
                                      self.relative_position_bias_table,
                                      self.relative_position_index, self.proj.weight,
                                      self.proj.bias, self.window_size, self.num_heads,
-                                     float(self.scale), prec, train, self._index_formula)
+                                     float(self.scale), prec, train, self._formula_valid())
         return out
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

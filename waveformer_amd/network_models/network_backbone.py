@@ -166,8 +166,10 @@ class Waveformer(nn.Module):
             buf1 = ops.empty_cl(B, fs0 + self.encoder1.layer.conv1.conv.out_channels, D, H, W,
                                 x_in.device)
             enc0 = self.encoder1(x_in, out=buf1[:, fs0:])
+            enc0_in_place = True
         else:
             enc0 = self.encoder1(x_in)
+            enc0_in_place = False
         enc1 = self.encoder2(outs[0])
         enc2 = self.encoder3(outs[1])
         enc3 = self.encoder4(outs[2])
@@ -181,7 +183,7 @@ class Waveformer(nn.Module):
             cat = torch.cat([up4, up3, dec2], dim=1)
         else:  # inference: one channel-last buffer, the layout decoder1's kernels read
             cat = ops.cat_cl([up4, up3, dec2])
-        dec1 = self.decoder1(cat, enc0)
+        dec1 = self.decoder1(cat, enc0, skip_in_place=enc0_in_place)
         # the HIP decoder path is channel-last; hand the caller the reference's NCDHW layout
         return self.out(dec1).contiguous()
 

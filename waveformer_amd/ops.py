@@ -50,16 +50,21 @@ def _check(t: torch.Tensor, name: str, dtype=torch.float32, contiguous=True) -> 
 # ------------------------------------------------------------------------------------------
 PRECISIONS = {"bf16": 0, "bf16x3": 1, "fp16": 2}
 FP16 = PRECISIONS["fp16"]
-_precision = os.environ.get("WAVEFORMER_PRECISION", "bf16x3")
+_precision = os.environ.get("WAVEFORMER_PRECISION", "bf16x3")  # the process default
 if _precision not in PRECISIONS:
     raise ValueError(f"WAVEFORMER_PRECISION={_precision!r}: expected one of {sorted(PRECISIONS)}")
+# Scoped overrides (`precision`, `op_precision`) live in thread-local state: a forward that
+# switches an op group to bf16x3 never changes what another thread's forward sees, and
+# overlapping scopes of two threads cannot restore each other's value.
+_prec_tls = threading.local()
 
 
 def set_precision(p: str) -> None:
     """'bf16x3' (default): fp32-faithful split-bf16 MFMA operands, fp32 intermediates.
     'bf16': plain bf16 operands and bf16 GEMM-to-GEMM intermediates (fastest).
     'fp16': fp16 operands (10-bit mantissa) on the f16 MFMA pipes, fp32 intermediates
-    (config 5's fp16 MFMA path)."""
+    (config 5's fp16 MFMA path).  Sets the process-wide default; a `precision` scope of the
+    calling thread still takes precedence inside it."""
     global _precision
     if p not in PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {p!r}")
@@ -67,30 +72,35 @@ def set_precision(p: str) -> None:
 
 
 def get_precision() -> str:
-    return _precision
+    """The precision in effect on this thread: its innermost scope, else the default."""
+    o = getattr(_prec_tls, "override", None)
+    return _precision if o is None else o
 
 
 class precision:
-    """Context manager: `with ops.precision("bf16"): model(x)`."""
+    """Context manager: `with ops.precision("bf16"): model(x)` -- for the calling thread only."""
 
     def __init__(self, p: str):
+        if p not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {p!r}")
         self.p = p
 
     def __enter__(self):
-        self.prev = get_precision()
-        set_precision(self.p)
+        self.prev = getattr(_prec_tls, "override", None)
+        _prec_tls.override = self.p
+        return self
 
     def __exit__(self, *exc):
-        set_precision(self.prev)
+        _prec_tls.override = self.prev
 
 
 def _prec() -> int:
-    return PRECISIONS[_precision]
+    return PRECISIONS[get_precision()]
 
 
 def prec_id() -> int:
-    """WF_PREC_* id of the current global precision."""
-    return PRECISIONS[_precision]
+    """WF_PREC_* id of the precision in effect on this thread."""
+    return PRECISIONS[get_precision()]
 
 
 # The fp16 precision policy (config 5).  fp16 operands everywhere except the ops whose rounding
@@ -105,26 +115,26 @@ FP16_SPLIT_OPS = frozenset({"attn", "skip_conv"})
 
 
 def op_prec(kind: str) -> int:
-    """WF_PREC_* id an op of `kind` runs at under the current global precision."""
-    if _precision == "fp16" and kind in FP16_SPLIT_OPS:
+    """WF_PREC_* id an op of `kind` runs at under the precision in effect on this thread."""
+    cur = get_precision()
+    if cur == "fp16" and kind in FP16_SPLIT_OPS:
         return PRECISIONS["bf16x3"]
-    return PRECISIONS[_precision]
+    return PRECISIONS[cur]
 
 
-class op_precision:
-    """`with ops.op_precision("skip_conv"): ...` -- the global precision an op of `kind` runs
-    at (the fp16 policy's exceptions switch to bf16x3 inside; otherwise a no-op)."""
+class op_precision(precision):
+    """`with ops.op_precision("skip_conv"): ...` -- the precision an op of `kind` runs at
+    (the fp16 policy's exceptions switch this thread to bf16x3 inside; otherwise a no-op)."""
 
     def __init__(self, kind: str):
         self.kind = kind
 
     def __enter__(self):
-        self.prev = _precision
-        if op_prec(self.kind) != PRECISIONS[_precision]:
-            set_precision("bf16x3")
-
-    def __exit__(self, *exc):
-        set_precision(self.prev)
+        self.prev = getattr(_prec_tls, "override", None)
+        cur = get_precision()
+        self.p = "bf16x3" if op_prec(self.kind) != PRECISIONS[cur] else cur
+        _prec_tls.override = self.p
+        return self
 
 
 # ------------------------------------------------------------------------------------------
@@ -234,7 +244,7 @@ class weight_scope:
             # the operand format this forward's kernels read: fp16 for an fp16 inference
             # forward, else bf16 hi / lo (training always runs fp32-faithful bf16x3)
             train = torch.is_grad_enabled() and any(p.requires_grad for p in params)
-            f16 = _precision == "fp16" and not train
+            f16 = get_precision() == "fp16" and not train
             arenas = getattr(self.module, "_wf_arenas", None)
             if arenas is None:
                 arenas = {}
