@@ -222,8 +222,10 @@ def pmc_traffic(kernel_substr, batch):
 
 
 def pmc_valu(kernel_substr, batch):
-    """(VALU issue fraction, source file) of a kernel from the newest profiles/*valu*.json
-    written by tools/pmc_valu.py at this per-GPU batch; (None, None) when none matches."""
+    """(counter entry, source file) of a kernel from the newest profiles/*valu*.json written by
+    tools/pmc_valu.py at this per-GPU batch; (None, None) when none matches.  The entry's
+    valu_issue_frac is priced at 2 cycles per wave64 VALU instruction (the SIMD-32 throughput);
+    files written before that fix (no valu_cycles_per_inst key, 4-cycle pricing) are halved."""
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*valu*.json")), reverse=True):
         try:
             d = json.load(open(f))
@@ -233,7 +235,10 @@ def pmc_valu(kernel_substr, batch):
             continue
         for k, v in d["kernels"].items():
             if kernel_substr in k:
-                return v["valu_issue_frac"], os.path.relpath(f, REPO)
+                v = dict(v)
+                if v.get("valu_cycles_per_inst") != 2:
+                    v["valu_issue_frac"] = round(v["valu_issue_frac"] / 2, 4)
+                return v, os.path.relpath(f, REPO)
         return None, None
     return None, None
 
@@ -706,11 +711,11 @@ def main():
                  "algorithmic_bytes_per_launch": r["work_per_launch"],
                  "avg_launch_us": round(r["avg_ms"] * 1e3, 2), "launches_timed": r["launches"]}
             if name == "ccf_ffn_dwconv":
-                # the kernel is FP32-VALU-bound: its VALU issue fraction from
-                # the committed counter pass of the same bench command
+                # its VALU issue fraction (2-cycle SIMD-32 ceiling) from the committed
+                # counter pass of the same bench command
                 vf, src = pmc_valu(PMC_KERNEL[name], args.batch)
                 if vf is not None:
-                    d["valu_issue_frac"], d["valu_source"] = vf, src
+                    d["valu_issue_frac"], d["valu_source"] = vf["valu_issue_frac"], src
             return d
 
         if roofs.get(roof_op):
@@ -721,8 +726,11 @@ def main():
         if "window_attention" in out["rooflines"]:
             vf, src = pmc_valu("attn_tbl_kernel", args.batch)
             if vf is not None:
-                out["rooflines"]["window_attention"]["core_valu_issue_frac"] = vf
-                out["rooflines"]["window_attention"]["valu_source"] = src
+                wa = out["rooflines"]["window_attention"]
+                wa["core_valu_issue_frac"] = vf["valu_issue_frac"]
+                if "mfma_busy_frac" in vf:  # SQ_VALU_MFMA_BUSY_CYCLES: the pipe, not the spec
+                    wa["core_mfma_busy_frac"] = vf["mfma_busy_frac"]
+                wa["valu_source"] = src
         if args.parity:
             try:
                 out["parity"] = parity_dice(dev, "full192hf" if hf else "full128")
