@@ -243,20 +243,27 @@ def pmc_valu(kernel_substr, batch):
     return None, None
 
 
-def idwt_roofline(batch, dev):
+def idwt_roofline(batch, dev, layout="cl"):
     """The decoder's level-0 Haar IDWT (UnetrIDWTBlock's waverec3 replacement,
     idwt_upsample.py:160, §8a row a11) at the encoder's stage-0 band shape: 8 bands of
     (B, 48, 64^3) -> (B, 48, 128^3), written into the first half of a 96-channel concat buffer
-    as the decoder does.  Algorithmic bytes: read 8 bands + write the output, 8 B per output
-    element.  HIP events on the launch stream around REPS back-to-back launches."""
+    as the decoder does.  layout "cl" is the inference decoder's path (idwt_upsample.py's
+    channel-last LL and concat buffer, idwt3d_haar_cl4_kernel); "ncdhw" the autograd path's
+    (NCDHW LL and output, idwt3d_haar_nc4_kernel).  Algorithmic bytes: read 8 bands + write the
+    output, 8 B per output element.  HIP events on the launch stream around REPS back-to-back
+    launches."""
     from waveformer_amd import ops
     g = torch.Generator(device=dev).manual_seed(7)
     # the decoder's inputs: detail bands as the channel-last views of the DWT's (8, B, d, h,
-    # w, C) output (ops.dwt3d_haar), the LL as an NCDHW tensor
+    # w, C) output (ops.dwt3d_haar)
     bands = torch.randn(8, batch, 64, 64, 64, 48, device=dev, generator=g)
-    ll = bands[0].permute(0, 4, 1, 2, 3).contiguous()
     det = [{k: bands[i + 1].permute(0, 4, 1, 2, 3) for i, k in enumerate(ops.DETAIL_KEYS)}]
-    out = torch.empty(batch, 96, 128, 128, 128, device=dev)
+    if layout == "cl":
+        ll = bands[0].permute(0, 4, 1, 2, 3)                     # channel-last view
+        out = ops.empty_cl(batch, 96, 128, 128, 128, dev)
+    else:
+        ll = bands[0].permute(0, 4, 1, 2, 3).contiguous()
+        out = torch.empty(batch, 96, 128, 128, 128, device=dev)
     ops.idwt3d_haar(ll, det, out=out)
     reps = 10
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -269,12 +276,13 @@ def idwt_roofline(batch, dev):
     alg = 8 * batch * 48 * 128 ** 3  # 8 B per output element (4 B of bands read + 4 B written)
     ach = alg / (us * 1e-6) / 1e9
     del bands, ll, det, out
-    return {"bound": "hbm", "kernel": "idwt3d_haar", "achieved": round(ach, 1),
+    kname = "idwt3d_haar_cl4" if layout == "cl" else "idwt3d_haar_nc4"
+    return {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic("idwt3d_haar", batch), "algorithmic_bytes_per_launch": alg,
+            "traffic": pmc_traffic(kname, batch), "algorithmic_bytes_per_launch": alg,
             "avg_launch_us": round(us, 2), "launches_timed": reps,
-            "shape": f"channel-last bands 8 x ({batch}, 64^3, 48) -> ({batch}, 48, 128^3) NCDHW "
-                     f"into a 96-channel buffer"}
+            "shape": f"channel-last bands 8 x ({batch}, 64^3, 48) -> ({batch}, 48, 128^3) "
+                     f"{'channel-last' if layout == 'cl' else 'NCDHW'} into a 96-channel buffer"}
 
 
 def build_encoder(img, device):
@@ -722,7 +730,8 @@ def main():
             out["roofline"] = roofline(roof_op, roofs[roof_op])
         out["rooflines"] = {n: roofline(n, r) for n, r in roofs.items() if r and n != roof_op}
         if args.op_timers and not full:
-            out["rooflines"]["idwt3d_haar"] = idwt_roofline(args.batch, dev)
+            out["rooflines"]["idwt3d_haar"] = idwt_roofline(args.batch, dev, "cl")
+            out["rooflines"]["idwt3d_haar_ncdhw"] = idwt_roofline(args.batch, dev, "ncdhw")
         if "window_attention" in out["rooflines"]:
             vf, src = pmc_valu("attn_tbl_kernel", args.batch)
             if vf is not None:

@@ -19,6 +19,7 @@ Tolerances (stated per check):
     argmax labels at 128^3 x 4 >= 1 - 1e-3 against the reference's labels.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -95,6 +96,39 @@ def test_idwt_multilevel_vs_oracle_and_roundtrip(levels, C_, base):
         ops.idwt3d_haar(llcl, dets_cl, out=bcl)
         assert torch.equal(bcl[:, :C_], buf[:, :C_])
         assert torch.all(bcl[:, C_:] == 7.0)
+
+
+@pytest.mark.parametrize("levels,C_,base", [(1, 48, (4, 4, 8)), (3, 16, (1, 2, 3)), (2, 12, (2, 1, 2))])
+def test_idwt_vector_paths_match_scalar(levels, C_, base):
+    """The 16-B kernels (channel-last output: idwt3d_haar_cl4; NCDHW output:
+    idwt3d_haar_nc4) against the one-channel-per-lane kernel (WF_IDWT_SCALAR=1), bit for bit:
+    the same additions in the same order."""
+    from waveformer_amd import ops
+    B = 2
+    full = tuple(b * 2 ** levels for b in base)
+    co = R.wavedec3(seeded_randn((B, C_) + full, 11), "db1", levels)
+    ll = cuda(co[0])
+    dets = [{k: cuda(v).permute(0, 2, 3, 4, 1).contiguous().permute(0, 4, 1, 2, 3)
+             for k, v in d.items()} for d in co[1:]]
+    llcl = ll.contiguous(memory_format=torch.channels_last_3d)
+
+    def run():
+        nc = torch.full((B, C_ + 4) + full, 3.0, device=DEV)
+        ops.idwt3d_haar(ll, dets, out=nc)
+        cl = torch.full((B, C_ + 4) + full, 3.0, device=DEV).contiguous(
+            memory_format=torch.channels_last_3d)
+        ops.idwt3d_haar(llcl, dets, out=cl)
+        return nc, cl
+
+    nc, cl = run()
+    os.environ["WF_IDWT_SCALAR"] = "1"
+    try:
+        nc0, cl0 = run()
+    finally:
+        del os.environ["WF_IDWT_SCALAR"]
+    assert torch.equal(nc, nc0) and torch.equal(cl, cl0)
+    assert torch.equal(nc, cl)
+    assert torch.all(nc[:, C_:] == 3.0) and torch.all(cl[:, C_:] == 3.0)
 
 
 def test_encoder_hf_feed_idwt_roundtrip():

@@ -5,7 +5,12 @@ the same command, written to a JSON summary that bench.py reads (roofline.traffi
 
 Per MI355X_MICROARCH.md (HBM [CDNA4]): FETCH_SIZE and WRITE_SIZE are kilobytes at the L2's
 memory side (Infinity-Cache hits included); on gfx950 FETCH_SIZE reports half the bytes of a
-16 B/lane streaming read, so it is doubled here; WRITE_SIZE is exact for 16 B/lane stores.
+16 B/lane streaming read, and WRITE_SIZE is exact for 16 B/lane stores.  Other access widths
+are uncalibrated (the guide says so), so the x2 read correction is applied ONLY to the kernels
+listed in WIDE16 -- their bulk reads are 16 B per lane (f32x4 / b128 loads, checked in the
+source) -- and every other kernel's FETCH_SIZE is reported raw with rule "raw-uncalibrated"
+(the old scalar IDWT read its bands 4 B per lane and the blanket x2
+inflated its traffic to 1.44x).  Each kernel's entry records the rule it got.
 For each kernel the largest launch (max fetch) is reported."""
 import collections
 import csv
@@ -28,6 +33,18 @@ def load(root, counter):
     return per
 
 
+# kernels whose bulk reads are 16 B per lane (name prefixes; see the module docstring)
+WIDE16 = ("dwt3d_haar_fwd_kernel", "idwt3d_haar_cl4_kernel", "idwt3d_haar_nc4_kernel",
+          "msfuse_row_kernel", "ffn_dwfc_sb_kernel", "ffn_dwfc_ws_kernel", "ffn_dwfc2_kernel",
+          "gemm_rows_kernel", "gemm_kc_kernel", "gemm_lnw_kernel", "dwconv_ln_gelu_kernel",
+          "proj_out_kernel")
+
+
+def rule_of(name):
+    short = name.split("<")[0].split("::")[-1].strip()
+    return "x2-fetch-16B" if short.startswith(WIDE16) else "raw-uncalibrated"
+
+
 def main():
     fetch_root, write_root, dst = sys.argv[1], sys.argv[2], sys.argv[3]
     batch = int(sys.argv[4]) if len(sys.argv) > 4 else 4  # bench --batch of the PMC passes
@@ -38,15 +55,19 @@ def main():
             continue
         wv = write.get(name, [0.0])
         f_kb, w_kb = max(fv), max(wv)
+        rule = rule_of(name)
         kernels[name] = {
             "launches": len(fv),
             "fetch_size_kb_largest": f_kb,
             "write_size_kb_largest": w_kb,
-            "hbm_bytes_per_launch_largest": int(2 * f_kb * 1024 + w_kb * 1024),
+            "rule": rule,
+            "hbm_bytes_per_launch_largest": int((2 if rule == "x2-fetch-16B" else 1) * f_kb * 1024
+                                                + w_kb * 1024),
         }
     json.dump({"source": [fetch_root, write_root], "per_gpu_batch": batch,
-               "correction": "bytes = 2 * FETCH_SIZE[KB] * 1024 + WRITE_SIZE[KB] * 1024 (gfx950 "
-                             "FETCH_SIZE halving, MI355X_MICROARCH.md)",
+               "correction": "bytes = k * FETCH_SIZE[KB] * 1024 + WRITE_SIZE[KB] * 1024, k = 2 for "
+                             "rule x2-fetch-16B (gfx950 FETCH_SIZE halving of 16 B/lane reads, "
+                             "MI355X_MICROARCH.md), k = 1 for raw-uncalibrated",
                "kernels": kernels}, open(dst, "w"), indent=1)
     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch_largest"])[:12]:
         print(f"{v['hbm_bytes_per_launch_largest'] / 1e6:10.1f} MB  {k}")

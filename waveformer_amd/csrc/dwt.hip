@@ -212,6 +212,175 @@ __global__ __launch_bounds__(256) void idwt3d_haar_kernel(IdwtArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Channel-last in, channel-last out (the decoder's path: LL from the previous decoder stage,
+// details = channel-last views of the DWT's band tensor, output = the concat buffer): a pure
+// per-position stream, so no LDS.  One thread = one finest-level cube (b, z1, y1, x1) x 4
+// channels, channels fastest: every load and store is 16 B per lane and consecutive lanes
+// touch consecutive 16 B (LL row, each band row, each output position row).  The coarser
+// levels (L > 1) are re-read by the 8^l descendants of a coefficient; they are 1/8 of the
+// level below and hit L2.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void idwt3d_haar_cl4_kernel(IdwtArgs a, int64_t total) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int L = a.levels, C4 = a.C >> 2;
+  const int w1 = a.w << (L - 1), h1 = a.h << (L - 1), d1 = a.d << (L - 1);
+  int64_t r = t;
+  const int c = 4 * (int)(r % C4);
+  r /= C4;
+  const int x1 = (int)(r % w1);
+  r /= w1;
+  const int y1 = (int)(r % h1);
+  r /= h1;
+  const int z1 = (int)(r % d1);
+  const int b = (int)(r / d1);
+  auto coef4 = [&](int l, int k, int z, int y, int x) {
+    const int64_t Wl = (int64_t)a.w << l;
+    const int64_t off = b * a.ds[4 * l] + c + z * a.ds[4 * l + 2] + ((int64_t)y * Wl + x) * a.ds[4 * l + 3];
+    return *reinterpret_cast<const f32x4*>(a.det[l * 7 + k] + off);
+  };
+  const int zc = z1 >> (L - 1), yc = y1 >> (L - 1), xc = x1 >> (L - 1);
+  f32x4 ll = *reinterpret_cast<const f32x4*>(
+      a.ll + b * a.ll_bstride + c + (((int64_t)zc * a.h + yc) * a.w + xc) * a.ll_ps);
+  for (int l = 0; l < L - 1; ++l) {
+    const int sh = L - 1 - l;
+    const int zl = z1 >> sh, yl = y1 >> sh, xl = x1 >> sh;
+    const int sz = (z1 >> (sh - 1)) & 1, sy = (y1 >> (sh - 1)) & 1, sx = (x1 >> (sh - 1)) & 1;
+    f32x4 cv[7];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) cv[k - 1] = coef4(l, k - 1, zl, yl, xl);
+    f32x4 acc = ll;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const int neg = (((k >> 2) & 1) & sz) ^ (((k >> 1) & 1) & sy) ^ ((k & 1) & sx);
+      acc = neg ? acc - cv[k - 1] : acc + cv[k - 1];
+    }
+    ll = acc * kHaar3;
+  }
+  f32x4 v[8];
+  v[0] = ll;
+#pragma unroll
+  for (int k = 1; k < 8; ++k) v[k] = coef4(L - 1, k - 1, z1, y1, x1);
+#pragma unroll
+  for (int bit = 1; bit < 8; bit <<= 1) {
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      if (!(n & bit)) {
+        const f32x4 s0 = v[n], s1 = v[n | bit];
+        v[n] = s0 + s1;
+        v[n | bit] = s0 - s1;
+      }
+    }
+  }
+  const int Wo = 2 * w1, Ho = 2 * h1;
+  float* ob = a.out + b * a.out_bstride + c;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const int zo = 2 * z1 + (n >> 2), yo = 2 * y1 + ((n >> 1) & 1), xo = 2 * x1 + (n & 1);
+    *reinterpret_cast<f32x4*>(ob + (((int64_t)zo * Ho + yo) * Wo + xo) * a.ldo) = v[n] * kHaar3;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Channel-last details, NCDHW LL and NCDHW output (the autograd path and wfa.idwt3d_haar
+// without an output buffer).  One workgroup = one finest row (b, z1, y1) x a block of CB
+// channels (a multiple of 4):
+//   1. the CB LL rows are read coalesced along x (NCDHW rows) into LDS [CB][w1 + 1];
+//   2. item = (x1, channel quad), quads fastest: the 7 finest bands as 16-B loads (consecutive
+//      lanes on consecutive 16 B of a band row), coarser levels likewise, LL from LDS; the 8
+//      outputs x 4 channels go to the LDS image [2][2][CB][Wo + 2] as 8-B (x pair) stores
+//      (channel rows Wo + 2 floats apart: consecutive quads land 8 banks apart, <= 3-way);
+//   3. the image's rows (Wo floats per (z, y, channel)) go out as 16-B stores.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void idwt3d_haar_nc4_kernel(IdwtArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds_nc[];
+  const int L = a.levels;
+  const int w1 = a.w << (L - 1), h1 = a.h << (L - 1), d1 = a.d << (L - 1);
+  const int Wo = 2 * w1, Ho = 2 * h1, Do = 2 * d1, WP = Wo + 2, LP = w1 + 1;
+  int row = blockIdx.x;
+  const int y1 = row % h1;
+  row /= h1;
+  const int z1 = row % d1;
+  const int b = row / d1;
+  const int c0 = blockIdx.y * a.CB;
+  const int CB = min(a.CB, a.C - c0);
+  const int CB4 = CB >> 2;
+  float* lds_ll = lds_nc + (size_t)a.CB * 4 * WP;
+  // 1. LL rows of the coarsest ancestor row (x varies by x1 >> (L-1))
+  const int zc = z1 >> (L - 1), yc = y1 >> (L - 1);
+  for (int i = threadIdx.x; i < CB * a.w; i += blockDim.x) {
+    const int cl = i / a.w, xc = i - cl * a.w;
+    lds_ll[cl * LP + xc] =
+        a.ll[b * a.ll_bstride + (int64_t)(c0 + cl) * a.ll_cs + ((int64_t)zc * a.h + yc) * a.w + xc];
+  }
+  __syncthreads();
+  for (int item = threadIdx.x; item < CB4 * w1; item += blockDim.x) {
+    const int q = item % CB4, x1 = item / CB4;
+    const int cl = 4 * q, c = c0 + cl;
+    auto coef4 = [&](int l, int k, int z, int y, int x) {
+      const int64_t Wl = (int64_t)a.w << l;
+      const int64_t off = b * a.ds[4 * l] + c + z * a.ds[4 * l + 2] + ((int64_t)y * Wl + x) * a.ds[4 * l + 3];
+      return *reinterpret_cast<const f32x4*>(a.det[l * 7 + k] + off);
+    };
+    const int xc = x1 >> (L - 1);
+    f32x4 ll = f32x4{lds_ll[cl * LP + xc], lds_ll[(cl + 1) * LP + xc], lds_ll[(cl + 2) * LP + xc],
+                     lds_ll[(cl + 3) * LP + xc]};
+    for (int l = 0; l < L - 1; ++l) {
+      const int sh = L - 1 - l;
+      const int zl = z1 >> sh, yl = y1 >> sh, xl = x1 >> sh;
+      const int sz = (z1 >> (sh - 1)) & 1, sy = (y1 >> (sh - 1)) & 1, sx = (x1 >> (sh - 1)) & 1;
+      f32x4 cv[7];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) cv[k - 1] = coef4(l, k - 1, zl, yl, xl);
+      f32x4 acc = ll;
+#pragma unroll
+      for (int k = 1; k < 8; ++k) {
+        const int neg = (((k >> 2) & 1) & sz) ^ (((k >> 1) & 1) & sy) ^ ((k & 1) & sx);
+        acc = neg ? acc - cv[k - 1] : acc + cv[k - 1];
+      }
+      ll = acc * kHaar3;
+    }
+    f32x4 v[8];
+    v[0] = ll;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v[k] = coef4(L - 1, k - 1, z1, y1, x1);
+#pragma unroll
+    for (int bit = 1; bit < 8; bit <<= 1) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        if (!(n & bit)) {
+          const f32x4 s0 = v[n], s1 = v[n | bit];
+          v[n] = s0 + s1;
+          v[n | bit] = s0 - s1;
+        }
+      }
+    }
+    // slot n = (sz, sy, sx); the sx pair is adjacent in a row: one 8-B store per channel
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const f32x4 e = v[2 * r] * kHaar3, o = v[2 * r + 1] * kHaar3;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<f32x2*>(lds_nc + (r * a.CB + cl + j) * WP + 2 * x1) = f32x2{e[j], o[j]};
+    }
+  }
+  __syncthreads();
+  // 3. rows: (cl, r) x Wo floats, 16 B per lane
+  float* obase = a.out + b * a.out_bstride;
+  const int64_t plane = (int64_t)Do * Ho * Wo;
+  const int V4 = Wo >> 2;
+  for (int item = threadIdx.x; item < CB * 4 * V4; item += blockDim.x) {
+    const int xv = item % V4, rr = item / V4;
+    const int cl = rr % CB, r = rr / CB;
+    const int zo = 2 * z1 + (r >> 1), yo = 2 * y1 + (r & 1);
+    const float* src = lds_nc + (r * a.CB + cl) * WP + 4 * xv;
+    const f32x2 lo = *reinterpret_cast<const f32x2*>(src), hi = *reinterpret_cast<const f32x2*>(src + 2);
+    *reinterpret_cast<f32x4*>(obase + (int64_t)(c0 + cl) * plane + ((int64_t)zo * Ho + yo) * Wo + 4 * xv) =
+        f32x4{lo.x, lo.y, hi.x, hi.y};
+  }
+}
+
 }  // namespace wf
 
 using namespace wf;
@@ -282,6 +451,36 @@ static int idwt_launch(const float* ll, int64_t ll_bstride, int64_t ll_cs, int64
   const bool cl = ldo > 0;
   const int64_t w1 = w << (levels - 1), h1 = h << (levels - 1), d1 = d << (levels - 1);
   WF_REQUIRE(w1 <= 4096, "row too long");
+  // 16-B paths: channel quads contiguous in every band (and in the LL / output where they are
+  // channel-last), every base and stride a multiple of 4 floats
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  bool vec = C % 4 == 0 && getenv("WF_IDWT_SCALAR") == nullptr;
+  for (int l = 0; l < levels && vec; ++l) {
+    vec = det_s[4 * l + 1] == 1 && det_s[4 * l] % 4 == 0 && det_s[4 * l + 2] % 4 == 0 &&
+          det_s[4 * l + 3] % 4 == 0;
+    for (int k = 0; k < 7 && vec; ++k) vec = al16(det[l * 7 + k]);
+  }
+  vec = vec && al16(out) && out_bstride % 4 == 0;
+  if (vec && cl && ll_cs == 1 && ll_ps % 4 == 0 && ll_bstride % 4 == 0 && al16(ll) && ldo % 4 == 0) {
+    const int64_t total = B * d1 * h1 * w1 * (C / 4);
+    hipLaunchKernelGGL(idwt3d_haar_cl4_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                       (hipStream_t)stream, a, total);
+    return check_launch("wf_idwt3d_haar_cl");
+  }
+  if (vec && !cl && ll_ps == 1 && (2 * w1) % 4 == 0) {
+    // LDS: [4][CB][2 w1 + 2] output image + [CB][w1 + 1] LL rows, ~40 KB (4 workgroups / CU)
+    const int64_t per_c = 4 * (4 * (2 * w1 + 2)) + 4 * (w1 + 1);
+    int64_t cb = (40 * 1024 / per_c) / 4 * 4;
+    if (cb < 4) cb = 4;
+    if (cb > C) cb = C;
+    if (cb * per_c <= 64 * 1024) {
+      a.CB = (int)cb;
+      dim3 grid((unsigned)(B * d1 * h1), (unsigned)cdiv(C, cb));
+      hipLaunchKernelGGL(idwt3d_haar_nc4_kernel, grid, dim3(256), (size_t)(cb * per_c),
+                         (hipStream_t)stream, a);
+      return check_launch("wf_idwt3d_haar");
+    }
+  }
   // LDS budget 48 KB: CB * 8 * w1 floats (+ 8 * w1 of padding in the channel-last image)
   int64_t cb = (48 * 1024 / 4) / (8 * w1) - (cl ? 1 : 0);
   if (cb < 1) cb = 1;
