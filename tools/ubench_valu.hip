@@ -48,6 +48,16 @@ __global__ void ub_kernel(float* out, unsigned long long* cyc, int n, float s) {
         if (u + 2 < U) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[u + 2]) : "v"(v2), "v"(s));
       }
     }
+  } else if (MODE == 4) {  // v_fmac_f32 with three VGPR sources (acc += x * w), the scatter's form
+    float w[U], x0 = s * lane;
+#pragma unroll
+    for (int u = 0; u < U; ++u) w[u] = s + u * 1e-3f;
+    for (int it = 0; it < n; ++it) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(a[u]) : "v"(x0), "v"(w[u]));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] += w[u];
   } else if (MODE == 3) {  // v_pk_fma_f32 on pairs (compiler packs float2 fma)
     typedef float f2 __attribute__((ext_vector_type(2)));
     f2 b[U / 2];
@@ -108,6 +118,7 @@ int main() {
   for (int w = 1; w <= 4; ++w) run<0, 16>("fma", w, n, 16);
   for (int w = 1; w <= 4; ++w) run<0, 4>("fma", w, n, 4);
   for (int w = 1; w <= 4; ++w) run<3, 16>("pk_fma", w, n, 8);
+  for (int w = 1; w <= 4; ++w) run<4, 16>("fmac3v", w, n, 16);
   for (int w = 1; w <= 3; ++w) run<1, 8>("exp", w, n / 4, 8);
   for (int w = 1; w <= 3; ++w) run<2, 18>("lds+fma", w, n, 18);
   return 0;
