@@ -53,28 +53,6 @@ struct DwFcCfg {
                                       (size_t)(2 * HID + 3 * C) * 4;
 };
 
-template <typename T>
-struct H1Load;
-template <>
-struct H1Load<float> {
-  typedef f32x4 raw;
-  static __device__ __forceinline__ raw load(const float* p, int64_t i) {
-    return *reinterpret_cast<const f32x4*>(p + i);
-  }
-  static __device__ __forceinline__ f32x4 up(raw u) { return u; }
-};
-template <>
-struct H1Load<uint16_t> {
-  typedef bf16x4 raw;
-  static __device__ __forceinline__ raw load(const uint16_t* p, int64_t i) {
-    return *reinterpret_cast<const bf16x4*>(p + i);
-  }
-  static __device__ __forceinline__ f32x4 up(raw u) {
-    return f32x4{bf2f((uint16_t)u[0]), bf2f((uint16_t)u[1]), bf2f((uint16_t)u[2]),
-                 bf2f((uint16_t)u[3])};
-  }
-};
-
 template <int C, int HID, int TY, int TX, int P, typename T>
 __global__ __launch_bounds__((HID / 2) * TX, (TX == 4 ? 3 : 1)) void ffn_dwfc_kernel(DwFcArgs a) {
   constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
@@ -781,6 +759,9 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_sb_kernel(DwFcArgs a) {
   constexpr int NLDE = (K::PP * K::NV + NE - 1) / NE;  // staged vectors per E thread (12)
   constexpr int H2F = K::NPOS * K::HS;
   constexpr int LNL = 16, LNC = HID / LNL;             // LN2: 16 lanes x 12 channels / position
+#ifndef WF_SB_LN2T
+#define WF_SB_LN2T 0
+#endif
 #ifndef WF_SB_SPLIT
 #define WF_SB_SPLIT 0
 #endif
@@ -853,6 +834,22 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_sb_kernel(DwFcArgs a) {
       v[4 * j + 2] = u.z;
       v[4 * j + 3] = u.w;
     }
+#if WF_SB_LN2T
+    // short dependency chains: three-way column sums (depth 3 + 2 instead of 12), four
+    // variance partials, the raw v_rsq_f32 (var + eps >= eps is a normal number)
+    float s4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s4[j] = (v[j] + v[j + 4]) + v[j + 8];
+    const float mean = group_sum<LNL>((s4[0] + s4[1]) + (s4[2] + s4[3])) * (1.f / HID);
+    float q4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d0 = v[j] - mean, d1 = v[j + 4] - mean, d2 = v[j + 8] - mean;
+      q4[j] = d2 * d2 + (d1 * d1 + d0 * d0);
+    }
+    const float rstd = __builtin_amdgcn_rsqf(
+        group_sum<LNL>((q4[0] + q4[1]) + (q4[2] + q4[3])) * (1.f / HID) + a.eps2);
+#else
     float sm = 0.f;
 #pragma unroll
     for (int j = 0; j < LNC; ++j) sm += v[j];
@@ -864,6 +861,7 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_sb_kernel(DwFcArgs a) {
       q += d * d;
     }
     const float rstd = rsqrtf(group_sum<LNL>(q) * (1.f / HID) + a.eps2);
+#endif
     const float nmr = -mean * rstd;
     uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
 #pragma unroll
@@ -1558,6 +1556,10 @@ static int go_dwfc_ws(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks
   g.dbg = dbg;  // timing experiments only: bit mask of phases skipped (results invalid)
   // WF_FFN_DWFC_WS=1: the round-2 wave-specialised kernel (A/B); default the SIMD-balanced one
   static const bool ws = getenv("WF_FFN_DWFC_WS") != nullptr;
+  // WF_FFN_DWFC_TB=1: three VALU waves per SIMD, one barrier per plane (ffn_dwfc_tb.hip;
+  // round 4, under tuning)
+  static const bool tb = getenv("WF_FFN_DWFC_TB") != nullptr;
+  if (!ws && tb) return launch_ffn_dwfc_tb(a, prec, s);
   void (*kern)(DwFcArgs) =
       ws ? (prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>
             : prec == PREC_FP16 ? ffn_dwfc_ws_kernel<PREC_FP16, float>

@@ -1,0 +1,465 @@
+// ffn_dwfc_tb.hip -- the stage-1 CCF_FFN back half (C = 48, hidden = 192; SURVEY 8a a8, 8f
+// row 1) with three VALU waves per SIMD and ONE barrier per plane (round 4, the default).
+//
+//   h2  = dwconv3x3x3(h1) + b          (wave_helper.py:285, groups = hidden, pad 1)
+//   g   = GELU(LN_eps2(h2))            (:286-287)
+//   ffn = fc(g) + fc_b                 (:289)
+//   out = x + (n2 + ffn) * bs          (Block residual + CCF_FFN residual, quirk Q4, :293/:509)
+//
+// Why a new kernel (tools/ubench_valu.hip, profiles/r4_ubench_valu.txt): on gfx950 one wave
+// issues a VALU instruction only every ~12 cycles, two waves of a SIMD together every ~3
+// (v_fma_f32) to ~5.3 (v_fmac_f32 fed by ds_read_b32), and only three or more reach the
+// SIMD-32 rate of 2 cycles.  ffn_dwfc_sb ran two VALU waves per SIMD (its 27 weights x 3
+// channels per lane held 160 VGPRs): its D waves issued at ~4.4 cycles per instruction.
+// Here every lane owns ONE channel, so a VALU wave fits 128 VGPRs and a SIMD holds three of
+// them plus the staging / fc wave (16 waves, 1024 threads):
+//
+//   tile 3 (y) x 8 (x) positions, z-marching through ZS output planes;
+//   D waves (12 = 3 per SIMD): lane = (channel c, column pair cp = the SIMD): the 27 taps of
+//        channel c in VGPRs, per input row 4 ds_read_b32 (consecutive lanes = consecutive
+//        channels: conflict-free) feed 2 columns x up to 3 output rows x 3 output planes;
+//        then LN2 + GELU + the bf16 hi / lo split of 2 positions per wave (32 lanes x 6
+//        channels per position: channel pairs 2g, 64 + 2g, 128 + 2g -> 8-B reads); and the
+//        haloed 5 x 10 x 192 h1 plane staging through a buffer descriptor (<= 4 16-B vectors
+//        per lane, fetched two planes ahead, committed one ahead; out-of-volume positions and
+//        planes read as zero).  96 VGPRs without the staging, 112 with it;
+//   E waves (4 = 1 per SIMD, s_setprio 3): the fc of one 16-channel output column tile
+//        (waves 0..2) over the 24 positions on v_mfma_f32_16x16x32 (x3 for bf16x3; weight hi
+//        in VGPRs, lo in LDS in fragment order), bias + Q4 residual + 16-B stores.  (With the
+//        staging on the E waves as well they needed > 128 VGPRs and spilled.)
+//
+// Per iteration p (one barrier), with three h2 tiles rotating:
+//   D: commit plane p+1, fetch plane p+2;  LN2 of h2 tile (p-2) in place;  scatter of
+//      plane p -> output plane p-1 complete -> h2 tile (p-1)
+//   E: fc + epilogue of tile (p-3) -> output plane p-3
+// Every producer -> consumer hand-off crosses exactly one barrier, so the phases of the D and
+// E waves overlap freely inside an iteration.
+//
+// LDS: 2 x 38.4 KB planes + 3 x 18.8 KB h2 tiles + 18 KB fc lo fragments + vectors = 152 KB.
+#include "kernels.hpp"
+
+namespace wf {
+
+namespace tb {
+constexpr int C = 48, HID = 192, TY = 3, TX = 8;
+constexpr int PY = TY + 2, PX = TX + 2, PP = PY * PX;  // haloed plane: 5 x 10
+constexpr int NPOS = TY * TX;                          // 24
+constexpr int HS = HID + 4;                            // h2 row stride (floats)
+constexpr int PLANE_F = PP * HID;
+constexpr int H2F = NPOS * HS;
+constexpr int NV = HID / 4;                            // 16-B vectors per h1 row
+constexpr int ND = 768;                                // D lanes
+constexpr int NLDD = (PP * NV + ND - 1) / ND;          // staged vectors per D lane (4)
+constexpr int KS = HID / 32;                           // fc k steps
+constexpr int FWL_BYTES = (C / 16) * KS * 64 * 16;     // lo fragments [ct][ks][lane][8]
+constexpr size_t LDS_BYTES = (size_t)(2 * PLANE_F + 3 * H2F + 2 * HID + 3 * C) * 4 + FWL_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+}  // namespace tb
+
+// sum over each 32-lane half: the DPP butterflies of group_sum<16>, then the two 16-lane rows
+// exchanged by v_permlane16_swap (VALU; ds_swizzle would put an LDS round trip on the
+// LayerNorm's dependency chain).  Every lane gets the same bits (lo + hi in both rows).
+__device__ __forceinline__ float sum32(float v) {
+  v = group_sum<16>(v);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+#ifdef WF_TB_PROBE
+// diagnostic builds only: per-wave cycles of workgroup 0 by phase (read by wf_debug_tb_probe,
+// tools/tb_phase_times.py); slots 6 / 7 = role / SIMD * 16 + arrival slot (+256 if balanced)
+__device__ long long g_tb_probe[16 * 8];
+extern "C" int wf_debug_tb_probe(long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tb_probe), sizeof(g_tb_probe));
+}
+#define TB_PROBE_DECL                                                           \
+  const bool probe_on = blockIdx.x == 0;                                        \
+  long long pr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pr_last = __builtin_amdgcn_s_memtime();
+#define TB_PROBE(i)                                                             \
+  if (probe_on) {                                                               \
+    const long long t_ = __builtin_amdgcn_s_memtime();                          \
+    pr_acc[i] += t_ - pr_last;                                                  \
+    pr_last = t_;                                                               \
+  }
+#define TB_PROBE_DUMP                                                           \
+  if (probe_on && lane == 0) {                                                  \
+    pr_acc[6] = role;                                                           \
+    pr_acc[7] = simd * 16 + slot + (even ? 256 : 0);                            \
+    for (int i_ = 0; i_ < 8; ++i_) g_tb_probe[wid * 8 + i_] = pr_acc[i_];       \
+  }
+#else
+#define TB_PROBE_DECL
+#define TB_PROBE(i)
+#define TB_PROBE_DUMP
+#endif
+
+__device__ __forceinline__ int tb_simd_id() {
+  // HW_ID (hwreg 4) bits [5:4]: the SIMD the wave runs on
+  return (int)((__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4)) & 3);
+}
+
+template <int P, typename T>
+__global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
+  using namespace tb;
+  constexpr bool SPLIT = P == PREC_SPLIT;
+  typedef H1Load<T> L;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* planes = lds;                     // [2][PP][HID]
+  float* h2b = lds + 2 * PLANE_F;          // [3][NPOS][HS]
+  float* lnw = h2b + 3 * H2F;              // [HID] (halved: GELU from x / 2)
+  float* lnb = lnw + HID;
+  float* fcb = lnb + HID;                  // [C]
+  float* n2w = fcb + C;
+  float* n2b = n2w + C;
+  bf16x8* fwlo = reinterpret_cast<bf16x8*>(n2b + C);  // [C/16][KS][64] fragments
+  __shared__ int simd_cnt[4];
+
+  const int tid = threadIdx.x;
+  const int wid = tid >> 6, lane = tid & 63;
+  const int D = a.D, H = a.H, W = a.W;
+  const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY, nzs = (D + a.ZS - 1) / a.ZS;
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int xt = t % ntx;
+  t /= ntx;
+  const int yt = t % nty;
+  t /= nty;
+  const int zt = t % nzs;
+  const int b = t / nzs;
+  const int x0 = xt * TX, y0 = yt * TY, z0 = zt * a.ZS, z1 = min(z0 + a.ZS, D);
+  const int64_t plane_sz = (int64_t)H * W;
+
+  if (tid < 4) simd_cnt[tid] = 0;
+  for (int i = tid; i < HID; i += 1024) {
+    lnw[i] = 0.5f * a.ln2_w[i];
+    lnb[i] = 0.5f * a.ln2_b[i];
+  }
+  for (int i = tid; i < C; i += 1024) {
+    fcb[i] = a.fc_b ? a.fc_b[i] : 0.f;
+    n2w[i] = a.stats ? a.n2_w[i] : 1.f;
+    n2b[i] = a.stats ? a.n2_b[i] : 0.f;
+  }
+  if (SPLIT) {
+    // lo plane in MFMA A-fragment order: fragment (ct, ks, l) = row ct*16 + (l & 15),
+    // k = ks*32 + 8*(l >> 4): each fc lane later reads its own 16 contiguous bytes
+    for (int i = tid; i < (C / 16) * KS * 64; i += 1024) {
+      const int l = i & 63, ks = (i >> 6) % KS, ct = (i >> 6) / KS;
+      fwlo[i] = *reinterpret_cast<const bf16x8*>(a.fc + (size_t)C * HID +
+                                                 (size_t)(ct * 16 + (l & 15)) * HID + ks * 32 + 8 * (l >> 4));
+    }
+  }
+  // depthwise weights and bias, coalesced into the (not yet used) plane buffer
+  for (int i = tid; i < HID * 27; i += 1024) planes[i] = a.dw_w[i];
+  for (int i = tid; i < HID; i += 1024) planes[HID * 27 + i] = a.dw_b[i];
+  __syncthreads();
+  // ---- roles: per SIMD, arrival slots 0..2 -> D waves, slot 3 -> the E wave
+  const int simd = tb_simd_id();
+  int slot = 0;
+  if (lane == 0) slot = atomicAdd(&simd_cnt[simd], 1);
+  slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0, 64));
+  __syncthreads();
+  const bool even = simd_cnt[0] == 4 && simd_cnt[1] == 4 && simd_cnt[2] == 4 && simd_cnt[3] == 4;
+  // D role d = 3 * cp + k (cp = column pair, k = channel block of 64); E role 12 + e
+  int role = even ? (slot < 3 ? 3 * simd + slot : 12 + simd) : wid;
+  role = __builtin_amdgcn_readfirstlane(role);
+  TB_PROBE_DECL
+
+  if (role < 12) {
+    // ================================ D waves ===========================================
+    const int cp = role / 3, c = (role % 3) * 64 + lane;
+    float w[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) w[k] = planes[c * 27 + k];
+    const float bias = planes[HID * 27 + c];
+    float acc[3][TY][2];  // output-plane accumulators, slot (o - z0 + 2) mod 3
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int o = 0; o < TY; ++o) acc[s][o][0] = acc[s][o][1] = 0.f;
+    // LN2 lanes: positions 2 * role + (lane >> 5), channel pairs 2g, 64 + 2g, 128 + 2g
+    const int lpos = 2 * role + (lane >> 5), lg = lane & 31;
+    // input rows scattered before the LayerNorm: 0, 2 or all 5 by the wave's slot on its SIMD
+    const int rsplit = __builtin_amdgcn_readfirstlane(role % 3 == 0 ? 0 : role % 3 == 1 ? 2 : PY);
+    // h1 staging: vector i = j * 768 + dt of the haloed plane; byte offsets inside one plane,
+    // loaded through a per-plane buffer descriptor (32-bit voffsets).  Halo positions outside
+    // the volume get an offset past the descriptor's range and planes outside [0, D) a
+    // zero-range descriptor: the loads return the zero padding, the commit is a plain copy.
+    const int dt = role * 64 + lane;
+    const T* src = reinterpret_cast<const T*>(a.h1) + (int64_t)b * D * H * W * HID;
+    const int64_t plane_elems = (int64_t)H * W * HID;
+    uint32_t off[NLDD];
+#pragma unroll
+    for (int j = 0; j < NLDD; ++j) {
+      const int i = min(j * ND + dt, PP * NV - 1);
+      const int pos = i / NV, v = i - pos * NV;
+      const int yy = y0 - 1 + pos / PX, xx = x0 - 1 + pos % PX;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      off[j] = ok ? (uint32_t)(((yy * W + xx) * HID + 4 * v) * (int)sizeof(T)) : 0x80000000u;
+    }
+    typename L::raw stg[NLDD];
+    auto fetch = [&](int p) {
+      const bool pz = p >= 0 && p < D;
+      const T* base = src + (int64_t)min(max(p, 0), D - 1) * plane_elems;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<T*>(base), 0, pz ? (int)(plane_elems * (int64_t)sizeof(T)) : 0, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < NLDD; ++j) {
+        if constexpr (sizeof(T) == 4)
+          stg[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[j], 0, 0));
+        else
+          stg[j] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(rs, off[j], 0, 0));
+      }
+    };
+    auto commit = [&](float* dst) {
+      float* d0 = dst + dt * 4;
+#pragma unroll
+      for (int j = 0; j < NLDD; ++j)
+        if ((j + 1) * ND <= PP * NV || j * ND + dt < PP * NV)
+          *reinterpret_cast<f32x4*>(d0 + j * ND * 4) = L::up(stg[j]);
+    };
+    fetch(z0 - 1);
+    __syncthreads();  // (prologue) weights read out of the plane buffer
+    commit(planes);
+    fetch(z0);
+    __syncthreads();  // (prologue) plane z0-1 committed
+
+    auto ln2_tile = [&](float* h2t) {
+      float* row = h2t + lpos * HS;
+      f32x2 v[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const f32x2*>(row + 64 * j + 2 * lg);
+      const float s = (v[0].x + v[0].y) + ((v[1].x + v[1].y) + (v[2].x + v[2].y));
+      const float mean = sum32(s) * (1.f / HID);
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float d0 = v[j].x - mean, d1 = v[j].y - mean;
+        q += d0 * d0 + d1 * d1;
+      }
+      const float rstd = __builtin_amdgcn_rsqf(sum32(q) * (1.f / HID) + a.eps2);
+      const float nmr = -mean * rstd;
+      uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int cc = 64 * j + 2 * lg;
+        const f32x2 lw2 = *reinterpret_cast<const f32x2*>(lnw + cc);
+        const f32x2 lb2 = *reinterpret_cast<const f32x2*>(lnb + cc);
+        const f32x2 y = gelu_half2((v[j] * rstd + nmr) * lw2 + lb2);
+        const uint16_t h0 = op_cvt<P>(y.x), h1 = op_cvt<P>(y.y);
+        *reinterpret_cast<uint32_t*>(rowh + cc) = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        if (SPLIT)
+          *reinterpret_cast<uint32_t*>(rowh + HID + cc) =
+              (uint32_t)(uint16_t)op_lo<P>(y.x, h0) | ((uint32_t)(uint16_t)op_lo<P>(y.y, h1) << 16);
+      }
+    };
+    // input rows of plane `cur` into A = acc[SA] (kz 2), B = acc[SB] (kz 1), C = acc[SC]
+    // (kz 0, first touch assigns); each row's 4 LDS reads issued one row ahead
+    auto scatter = [&](const float* cur, auto SAc, auto SBc, auto SCc, int r_lo, int r_hi) {
+      constexpr int SA = decltype(SAc)::value, SB = decltype(SBc)::value,
+                    SC = decltype(SCc)::value;
+      const float* q0 = cur + 2 * cp * HID + c;
+      float nx[4];
+      if (r_lo < r_hi) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nx[k] = q0[(r_lo * PX + k) * HID];
+      }
+#pragma unroll
+      for (int r = 0; r < PY; ++r) {
+        if (r < r_lo || r >= r_hi) continue;
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = nx[k];
+        if (r + 1 < r_hi) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) nx[k] = q0[((r + 1) * PX + k) * HID];
+        }
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int o = r - ky;
+          if (o < 0 || o >= TY) continue;
+          const float* w0 = w + ky * 3;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (ky == 0)
+              acc[SC][o][j] = w0[2] * v[j + 2] + (w0[1] * v[j + 1] + w0[0] * v[j]);
+            else
+              acc[SC][o][j] = w0[2] * v[j + 2] + (w0[1] * v[j + 1] + (w0[0] * v[j] + acc[SC][o][j]));
+            acc[SB][o][j] = w0[11] * v[j + 2] + (w0[10] * v[j + 1] + (w0[9] * v[j] + acc[SB][o][j]));
+            acc[SA][o][j] = w0[20] * v[j + 2] + (w0[19] * v[j + 1] + (w0[18] * v[j] + acc[SA][o][j]));
+          }
+        }
+      }
+    };
+    // one iteration p; R = (p - z0 + 1) mod 3 at compile time.  h2 tile of output plane z is
+    // buffer (z - z0) mod 3: tile p-1 -> (R + 1) % 3, tile p-2 -> R
+    auto step = [&](int p, auto Rc) {
+      constexpr int R = decltype(Rc)::value;
+      typedef std::integral_constant<int, R> SA;
+      typedef std::integral_constant<int, (R + 1) % 3> SB;
+      typedef std::integral_constant<int, (R + 2) % 3> SC;
+#pragma unroll
+      for (int j = 0; j < NLDD; ++j) asm volatile("" ::"v"(stg[j]));
+      if (p + 1 <= z1 && !(a.dbg & 8)) commit(planes + ((p + 2 - z0) & 1) * PLANE_F);
+      if (p + 2 <= z1 && !(a.dbg & 8)) fetch(p + 2);
+      TB_PROBE(0)
+      // the three D waves of a SIMD place their LayerNorm (a latency-bound chain of
+      // reductions) at different points of the scatter, so two of them issue independent
+      // FMAs while the third waits on it
+      const float* cur = planes + ((p - z0 + 1) & 1) * PLANE_F;
+      const bool live = p <= z1 && !(a.dbg & 1);
+      if (live) scatter(cur, SA(), SB(), SC(), 0, rsplit);
+      TB_PROBE(1)
+      if (p - 2 >= z0 && p - 2 < z1 && !(a.dbg & 2)) ln2_tile(h2b + R * H2F);
+      TB_PROBE(2)
+      if (live) {
+        scatter(cur, SA(), SB(), SC(), rsplit, PY);
+        if (p - 1 >= z0) {
+          float* h2t = h2b + ((R + 1) % 3) * H2F;
+#pragma unroll
+          for (int o = 0; o < TY; ++o)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              float h = acc[R][o][j] + bias;
+              if (sizeof(T) == 2) h = bf2f(f2bf(h));
+              h2t[(o * TX + 2 * cp + j) * HS + c] = h;
+            }
+        }
+      }
+      TB_PROBE(3)
+      __syncthreads();
+      TB_PROBE(4)
+    };
+    for (int p = z0 - 1; p <= z1 + 2; p += 3) {
+      step(p, std::integral_constant<int, 0>());
+      if (p + 1 <= z1 + 2) step(p + 1, std::integral_constant<int, 1>());
+      if (p + 2 <= z1 + 2) step(p + 2, std::integral_constant<int, 2>());
+    }
+    TB_PROBE_DUMP
+    return;
+  }
+
+  // ================================== E waves ============================================
+  __builtin_amdgcn_s_setprio(3);
+  const int e = role - 12;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const bool has_fc = e < C / 16;  // E waves 0..2: one output column tile each
+  const int ct = has_fc ? e : 0;
+  const float bs = a.bscale ? a.bscale[b] : 1.f;
+
+  bf16x8 fwh[KS];
+  {
+    const uint16_t* wr = a.fc + (size_t)(ct * 16 + l15) * HID + 8 * g4;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) fwh[ks] = *reinterpret_cast<const bf16x8*>(wr + ks * 32);
+  }
+  const bf16x8* fwl = fwlo + ct * KS * 64 + lane;
+  const int col = ct * 16 + 4 * g4;
+  const float* sbase = a.stats ? a.stats : a.x;
+  auto gpos_of = [&](int zo, int rt, bool clamp) {
+    const int lp = min(rt * 16 + l15, NPOS - 1);
+    int yo = y0 + lp / TX, xo = x0 + lp % TX;
+    if (clamp) {
+      yo = min(yo, H - 1);
+      xo = min(xo, W - 1);
+    }
+    return (int64_t)b * D * plane_sz + (int64_t)zo * plane_sz + (int64_t)yo * W + xo;
+  };
+  auto row_ok = [&](int rt) {
+    const int lp = rt * 16 + l15;
+    return lp < NPOS && y0 + lp / TX < H && x0 + lp % TX < W;
+  };
+  f32x4 xr[2];
+  f32x2 es[2];
+  auto load_resid = [&](int zo, int rt) {
+    const int64_t g = gpos_of(zo, rt, true);
+    xr[rt] = *reinterpret_cast<const f32x4*>(a.x + g * C + col);
+    es[rt] = *reinterpret_cast<const f32x2*>(sbase + 2 * g);
+  };
+  auto fc_store = [&](const float* h2t, int zo, int rt) {
+    const int lp = min(rt * 16 + l15, NPOS - 1);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)lp * (2 * HS);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = ks * 32 + 8 * g4;
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bh + k);
+      if (SPLIT) {
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
+        acc = mma32<P>(fwh[ks], bl, acc);
+        acc = mma32<P>(fwl[ks * 64], bh, acc);
+      }
+      acc = mma32<P>(fwh[ks], bh, acc);
+    }
+    f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+    const f32x4 xv = xr[rt];
+    if (a.stats) {
+      const f32x4 lw = *reinterpret_cast<const f32x4*>(n2w + col);
+      const f32x4 lb = *reinterpret_cast<const f32x4*>(n2b + col);
+      const float em = es[rt].x, er = es[rt].y;
+      const f32x4 n2 = (xv - em) * er * lw + lb;
+      v = xv + (n2 + v) * bs;
+    } else {
+      v = xv + v * bs;
+    }
+    if (row_ok(rt)) *reinterpret_cast<f32x4*>(a.out + gpos_of(zo, rt, false) * C + col) = v;
+  };
+
+  __syncthreads();  // (prologue) weights read out of the plane buffer
+  __syncthreads();  // (prologue) plane z0-1 visible
+  for (int p = z0 - 1; p <= z1 + 2; ++p) {
+    const int zo = p - 3;  // output plane this iteration stores
+    if (has_fc && zo >= z0 && zo < z1 && !(a.dbg & 4)) {
+      const float* h2t = h2b + ((zo - z0) % 3) * H2F;
+      fc_store(h2t, zo, 0);
+      fc_store(h2t, zo, 1);
+    }
+    TB_PROBE(0)
+    // the next iteration's residual / norm2-statistics rows, in flight across the barrier
+    if (has_fc && zo + 1 >= z0 && zo + 1 < z1) {
+      load_resid(zo + 1, 0);
+      load_resid(zo + 1, 1);
+    }
+    TB_PROBE(1)
+    __syncthreads();
+    TB_PROBE(4)
+  }
+  TB_PROBE_DUMP
+}
+
+int launch_ffn_dwfc_tb(const DwFcArgs& a, int prec, hipStream_t s) {
+  using namespace tb;
+  DwFcArgs g = a;
+  // z segments: minimise (rounds of workgroups over the CUs) x (planes + 4 pipeline steps)
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int64_t base = (int64_t)g.B * cdiv(g.H, TY) * cdiv(g.W, TX);
+  int best_zs = g.D;
+  int64_t best = -1;
+  for (int nz = 1; nz <= 8 && nz <= g.D; ++nz) {
+    const int zs = (int)cdiv(g.D, nz);
+    const int64_t cost = cdiv(base * cdiv(g.D, zs), cus) * (zs + 4);
+    if (best < 0 || cost < best) {
+      best = cost;
+      best_zs = zs;
+    }
+  }
+  g.ZS = best_zs;
+  static const int dbg = getenv("WF_FFN_DBG") ? atoi(getenv("WF_FFN_DBG")) : 0;
+  g.dbg = dbg;  // timing experiments only: bit mask of phases skipped (results invalid)
+  const int64_t blocks = base * cdiv(g.D, g.ZS);
+  void (*kern)(DwFcArgs) = prec == PREC_SPLIT  ? ffn_dwfc_tb_kernel<PREC_SPLIT, float>
+                           : prec == PREC_FP16 ? ffn_dwfc_tb_kernel<PREC_FP16, float>
+                                               : ffn_dwfc_tb_kernel<PREC_BF16, uint16_t>;
+  set_max_lds(reinterpret_cast<const void*>(kern), (int)LDS_BYTES);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), LDS_BYTES, s, g);
+  return check_launch("ffn_dwfc_tb");
+}
+
+}  // namespace wf

@@ -154,6 +154,31 @@ struct DwFcArgs {
   int ws_split;          // wave-specialised ffn_dwfc: D rows of a plane in phase 1 (1..5)
 };
 int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s);
+// stage-1 shape, three VALU waves per SIMD and one barrier per plane (ffn_dwfc_tb.hip)
+int launch_ffn_dwfc_tb(const DwFcArgs& a, int prec, hipStream_t s);
+// h1 plane staging: fp32 (SPLIT / FP16 workspaces) or bf16 (BF16) rows widened to fp32
+template <typename T>
+struct H1Load;
+template <>
+struct H1Load<float> {
+  typedef f32x4 raw;
+  static __device__ __forceinline__ raw load(const float* p, int64_t i) {
+    return *reinterpret_cast<const f32x4*>(p + i);
+  }
+  static __device__ __forceinline__ f32x4 up(raw u) { return u; }
+};
+template <>
+struct H1Load<uint16_t> {
+  typedef bf16x4 raw;
+  static __device__ __forceinline__ raw load(const uint16_t* p, int64_t i) {
+    return *reinterpret_cast<const bf16x4*>(p + i);
+  }
+  static __device__ __forceinline__ f32x4 up(raw u) {
+    return f32x4{bf2f((uint16_t)u[0]), bf2f((uint16_t)u[1]), bf2f((uint16_t)u[2]),
+                 bf2f((uint16_t)u[3])};
+  }
+};
+
 // the same for C = 96, hidden = 384 (4 x 4 tiles, one plane buffer, fc weight hi in LDS)
 int launch_ffn_dwfc2(const DwFcArgs& a, int prec, hipStream_t s);
 // ---- the whole CCF_FFN + norm2 + Q4 residual in one kernel for C = 48, hidden = 192: the

@@ -65,8 +65,13 @@ class Attention(nn.Module):
         self._index_version = self.relative_position_index._version
 
     def _formula_valid(self) -> bool:
-        return (self._index_formula
-                and self.relative_position_index._version == self._index_version)
+        if not self._index_formula:
+            return False
+        if torch.compiler.is_compiling():
+            # a traced graph sees tensor versions as data-dependent symbols: the check stays
+            # with eager mode (a compiled forward does not write the buffer in place)
+            return True
+        return self.relative_position_index._version == self._index_version
 
     def _check_train(self):
         if self.training and (self.attn_drop.p > 0 or self.proj_drop.p > 0):
