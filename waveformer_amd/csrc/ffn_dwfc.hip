@@ -1559,7 +1559,7 @@ static int go_dwfc_ws(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks
   // WF_FFN_DWFC_TB=1: three VALU waves per SIMD, one barrier per plane (ffn_dwfc_tb.hip;
   // round 4, under tuning)
   static const bool tb = getenv("WF_FFN_DWFC_TB") != nullptr;
-  if (!ws && tb) return launch_ffn_dwfc_tb(a, prec, s);
+  if (!ws && tb && prec != PREC_BF16) return launch_ffn_dwfc_tb(a, prec, s);
   void (*kern)(DwFcArgs) =
       ws ? (prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>
             : prec == PREC_FP16 ? ffn_dwfc_ws_kernel<PREC_FP16, float>

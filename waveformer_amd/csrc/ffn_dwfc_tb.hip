@@ -18,20 +18,25 @@
 //   D waves (12 = 3 per SIMD): lane = (channel c, column pair cp = the SIMD): the 27 taps of
 //        channel c in VGPRs, per input row 4 ds_read_b32 (consecutive lanes = consecutive
 //        channels: conflict-free) feed 2 columns x up to 3 output rows x 3 output planes;
-//        then LN2 + GELU + the bf16 hi / lo split of 2 positions per wave (32 lanes x 6
-//        channels per position: channel pairs 2g, 64 + 2g, 128 + 2g -> 8-B reads); and the
-//        haloed 5 x 10 x 192 h1 plane staging through a buffer descriptor (<= 4 16-B vectors
-//        per lane, fetched two planes ahead, committed one ahead; out-of-volume positions and
-//        planes read as zero).  96 VGPRs without the staging, 112 with it;
-//   E waves (4 = 1 per SIMD, s_setprio 3): the fc of one 16-channel output column tile
-//        (waves 0..2) over the 24 positions on v_mfma_f32_16x16x32 (x3 for bf16x3; weight hi
-//        in VGPRs, lo in LDS in fragment order), bias + Q4 residual + 16-B stores.  (With the
-//        staging on the E waves as well they needed > 128 VGPRs and spilled.)
+//        and LN2 + GELU + the bf16 hi / lo split of 2 positions per wave (32 lanes x 6
+//        channels per position: channel pairs 2g, 64 + 2g, 128 + 2g -> 8-B reads), placed
+//        before, inside or after the scatter by the wave's slot so that the three waves of a
+//        SIMD are not all in the LayerNorm's reduction chain at once.  96 VGPRs;
+//   E waves (4 = 1 per SIMD, s_setprio 3): the haloed 5 x 10 x 192 h1 plane staged by
+//        LDS-DMA (buffer_load_dwordx4 ... lds through a per-plane buffer descriptor, one plane
+//        ahead; out-of-volume positions and planes come back as zeros), the fc of one
+//        16-channel output column tile (waves 0..2) over the 24 positions on
+//        v_mfma_f32_16x16x32 (x3 for bf16x3; weight hi in VGPRs, lo in LDS in fragment order),
+//        bias + Q4 residual + 16-B stores.
+// Probes (tools/tb_phase_times.py, -DWF_TB_PROBE): staging on the D waves through registers
+// cost them 800-1400 cycles of a ~5600-cycle plane (12 waves' ds_write_b128 at once) and
+// needed 112 VGPRs; on the E waves by registers it needed > 128 VGPRs (spills).  LDS-DMA
+// needs neither.  fp32 h1 only (bf16x3, fp16 modes); the bf16 mode keeps ffn_dwfc_sb.
 //
 // Per iteration p (one barrier), with three h2 tiles rotating:
-//   D: commit plane p+1, fetch plane p+2;  LN2 of h2 tile (p-2) in place;  scatter of
-//      plane p -> output plane p-1 complete -> h2 tile (p-1)
-//   E: fc + epilogue of tile (p-3) -> output plane p-3
+//   D: LN2 of h2 tile (p-2) in place;  scatter of plane p -> output plane p-1 complete ->
+//      h2 tile (p-1)
+//   E: LDS-DMA of plane p+1;  fc + epilogue of tile (p-3) -> output plane p-3
 // Every producer -> consumer hand-off crosses exactly one barrier, so the phases of the D and
 // E waves overlap freely inside an iteration.
 //
@@ -39,6 +44,13 @@
 #include "kernels.hpp"
 
 namespace wf {
+
+#ifndef WF_TB_STAGGER
+#define WF_TB_STAGGER 0
+#endif
+#ifndef WF_TB_EPRIO
+#define WF_TB_EPRIO 3
+#endif
 
 namespace tb {
 constexpr int C = 48, HID = 192, TY = 3, TX = 8;
@@ -48,8 +60,8 @@ constexpr int HS = HID + 4;                            // h2 row stride (floats)
 constexpr int PLANE_F = PP * HID;
 constexpr int H2F = NPOS * HS;
 constexpr int NV = HID / 4;                            // 16-B vectors per h1 row
-constexpr int ND = 768;                                // D lanes
-constexpr int NLDD = (PP * NV + ND - 1) / ND;          // staged vectors per D lane (4)
+constexpr int NPC = (PP * NV + 63) / 64;               // 1-KiB LDS-DMA pieces per plane (38)
+constexpr int NPCE = (NPC + 3) / 4;                    // pieces per E wave
 constexpr int KS = HID / 32;                           // fc k steps
 constexpr int FWL_BYTES = (C / 16) * KS * 64 * 16;     // lo fragments [ct][ks][lane][8]
 constexpr size_t LDS_BYTES = (size_t)(2 * PLANE_F + 3 * H2F + 2 * HID + 3 * C) * 4 + FWL_BYTES;
@@ -102,8 +114,8 @@ __device__ __forceinline__ int tb_simd_id() {
 template <int P, typename T>
 __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
   using namespace tb;
+  static_assert(sizeof(T) == 4, "the LDS-DMA staging copies fp32 h1 rows");
   constexpr bool SPLIT = P == PREC_SPLIT;
-  typedef H1Load<T> L;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* planes = lds;                     // [2][PP][HID]
   float* h2b = lds + 2 * PLANE_F;          // [3][NPOS][HS]
@@ -180,50 +192,9 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
       for (int o = 0; o < TY; ++o) acc[s][o][0] = acc[s][o][1] = 0.f;
     // LN2 lanes: positions 2 * role + (lane >> 5), channel pairs 2g, 64 + 2g, 128 + 2g
     const int lpos = 2 * role + (lane >> 5), lg = lane & 31;
-    // input rows scattered before the LayerNorm: 0, 2 or all 5 by the wave's slot on its SIMD
-    const int rsplit = __builtin_amdgcn_readfirstlane(role % 3 == 0 ? 0 : role % 3 == 1 ? 2 : PY);
-    // h1 staging: vector i = j * 768 + dt of the haloed plane; byte offsets inside one plane,
-    // loaded through a per-plane buffer descriptor (32-bit voffsets).  Halo positions outside
-    // the volume get an offset past the descriptor's range and planes outside [0, D) a
-    // zero-range descriptor: the loads return the zero padding, the commit is a plain copy.
-    const int dt = role * 64 + lane;
-    const T* src = reinterpret_cast<const T*>(a.h1) + (int64_t)b * D * H * W * HID;
-    const int64_t plane_elems = (int64_t)H * W * HID;
-    uint32_t off[NLDD];
-#pragma unroll
-    for (int j = 0; j < NLDD; ++j) {
-      const int i = min(j * ND + dt, PP * NV - 1);
-      const int pos = i / NV, v = i - pos * NV;
-      const int yy = y0 - 1 + pos / PX, xx = x0 - 1 + pos % PX;
-      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-      off[j] = ok ? (uint32_t)(((yy * W + xx) * HID + 4 * v) * (int)sizeof(T)) : 0x80000000u;
-    }
-    typename L::raw stg[NLDD];
-    auto fetch = [&](int p) {
-      const bool pz = p >= 0 && p < D;
-      const T* base = src + (int64_t)min(max(p, 0), D - 1) * plane_elems;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<T*>(base), 0, pz ? (int)(plane_elems * (int64_t)sizeof(T)) : 0, 0x00020000);
-#pragma unroll
-      for (int j = 0; j < NLDD; ++j) {
-        if constexpr (sizeof(T) == 4)
-          stg[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[j], 0, 0));
-        else
-          stg[j] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(rs, off[j], 0, 0));
-      }
-    };
-    auto commit = [&](float* dst) {
-      float* d0 = dst + dt * 4;
-#pragma unroll
-      for (int j = 0; j < NLDD; ++j)
-        if ((j + 1) * ND <= PP * NV || j * ND + dt < PP * NV)
-          *reinterpret_cast<f32x4*>(d0 + j * ND * 4) = L::up(stg[j]);
-    };
-    fetch(z0 - 1);
+    const int kslot = __builtin_amdgcn_readfirstlane(role % 3);
     __syncthreads();  // (prologue) weights read out of the plane buffer
-    commit(planes);
-    fetch(z0);
-    __syncthreads();  // (prologue) plane z0-1 committed
+    __syncthreads();  // (prologue) plane z0-1 staged
 
     auto ln2_tile = [&](float* h2t) {
       float* row = h2t + lpos * HS;
@@ -254,27 +225,15 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
               (uint32_t)(uint16_t)op_lo<P>(y.x, h0) | ((uint32_t)(uint16_t)op_lo<P>(y.y, h1) << 16);
       }
     };
-    // input rows of plane `cur` into A = acc[SA] (kz 2), B = acc[SB] (kz 1), C = acc[SC]
-    // (kz 0, first touch assigns); each row's 4 LDS reads issued one row ahead
-    auto scatter = [&](const float* cur, auto SAc, auto SBc, auto SCc, int r_lo, int r_hi) {
+    // input rows [LO, HI) of the plane (vin: all 5 rows x 4 columns, read at the start of the
+    // step) into A = acc[SA] (kz 2), B = acc[SB] (kz 1), C = acc[SC] (kz 0, first touch
+    // assigns)
+    auto rows = [&](const float (&vin)[PY][4], auto SAc, auto SBc, auto SCc, auto LOc, auto HIc) {
       constexpr int SA = decltype(SAc)::value, SB = decltype(SBc)::value,
-                    SC = decltype(SCc)::value;
-      const float* q0 = cur + 2 * cp * HID + c;
-      float nx[4];
-      if (r_lo < r_hi) {
+                    SC = decltype(SCc)::value, LO = decltype(LOc)::value, HI = decltype(HIc)::value;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) nx[k] = q0[(r_lo * PX + k) * HID];
-      }
-#pragma unroll
-      for (int r = 0; r < PY; ++r) {
-        if (r < r_lo || r >= r_hi) continue;
-        float v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = nx[k];
-        if (r + 1 < r_hi) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) nx[k] = q0[((r + 1) * PX + k) * HID];
-        }
+      for (int r = LO; r < HI; ++r) {
+        const float* v = vin[r];
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
           const int o = r - ky;
@@ -292,6 +251,9 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
         }
       }
     };
+    typedef std::integral_constant<int, 0> I0;
+    typedef std::integral_constant<int, 2> I2;
+    typedef std::integral_constant<int, PY> IP;
     // one iteration p; R = (p - z0 + 1) mod 3 at compile time.  h2 tile of output plane z is
     // buffer (z - z0) mod 3: tile p-1 -> (R + 1) % 3, tile p-2 -> R
     auto step = [&](int p, auto Rc) {
@@ -299,33 +261,47 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
       typedef std::integral_constant<int, R> SA;
       typedef std::integral_constant<int, (R + 1) % 3> SB;
       typedef std::integral_constant<int, (R + 2) % 3> SC;
-#pragma unroll
-      for (int j = 0; j < NLDD; ++j) asm volatile("" ::"v"(stg[j]));
-      if (p + 1 <= z1 && !(a.dbg & 8)) commit(planes + ((p + 2 - z0) & 1) * PLANE_F);
-      if (p + 2 <= z1 && !(a.dbg & 8)) fetch(p + 2);
       TB_PROBE(0)
-      // the three D waves of a SIMD place their LayerNorm (a latency-bound chain of
-      // reductions) at different points of the scatter, so two of them issue independent
-      // FMAs while the third waits on it
-      const float* cur = planes + ((p - z0 + 1) & 1) * PLANE_F;
       const bool live = p <= z1 && !(a.dbg & 1);
-      if (live) scatter(cur, SA(), SB(), SC(), 0, rsplit);
-      TB_PROBE(1)
-      if (p - 2 >= z0 && p - 2 < z1 && !(a.dbg & 2)) ln2_tile(h2b + R * H2F);
-      TB_PROBE(2)
+      const bool ln = p - 2 >= z0 && p - 2 < z1 && !(a.dbg & 2);
+      float* h2ln = h2b + R * H2F;
+      // the whole plane's 20 inputs of this lane first (10 ds_read2st64_b32 in flight)
+      float vin[PY][4];
       if (live) {
-        scatter(cur, SA(), SB(), SC(), rsplit, PY);
-        if (p - 1 >= z0) {
-          float* h2t = h2b + ((R + 1) % 3) * H2F;
+        const float* q0 = planes + ((p - z0 + 1) & 1) * PLANE_F + 2 * cp * HID + c;
 #pragma unroll
-          for (int o = 0; o < TY; ++o)
+        for (int r = 0; r < PY; ++r)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              float h = acc[R][o][j] + bias;
-              if (sizeof(T) == 2) h = bf2f(f2bf(h));
-              h2t[(o * TX + 2 * cp + j) * HS + c] = h;
-            }
-        }
+          for (int k = 0; k < 4; ++k) vin[r][k] = q0[(r * PX + k) * HID];
+      }
+      // the three D waves of a SIMD place their LayerNorm (a latency-bound chain of
+      // reductions) at different points of the scatter (slot 0: first, 1: after two input
+      // rows, 2: last), so two of them issue independent FMAs while the third waits on it
+#if WF_TB_STAGGER
+      if (kslot == 0) {
+        if (ln) ln2_tile(h2ln);
+        if (live) rows(vin, SA(), SB(), SC(), I0(), IP());
+      } else if (kslot == 1) {
+        if (live) rows(vin, SA(), SB(), SC(), I0(), I2());
+        if (ln) ln2_tile(h2ln);
+        if (live) rows(vin, SA(), SB(), SC(), I2(), IP());
+      } else
+#endif
+      {
+        if (live) rows(vin, SA(), SB(), SC(), I0(), IP());
+        if (ln) ln2_tile(h2ln);
+      }
+      TB_PROBE(2)
+      if (live && p - 1 >= z0) {
+        float* h2t = h2b + ((R + 1) % 3) * H2F;
+#pragma unroll
+        for (int o = 0; o < TY; ++o)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            float h = acc[R][o][j] + bias;
+            if (sizeof(T) == 2) h = bf2f(f2bf(h));
+            h2t[(o * TX + 2 * cp + j) * HS + c] = h;
+          }
       }
       TB_PROBE(3)
       __syncthreads();
@@ -341,7 +317,7 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
   }
 
   // ================================== E waves ============================================
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(WF_TB_EPRIO);
   const int e = role - 12;
   const int l15 = lane & 15, g4 = lane >> 4;
   const bool has_fc = e < C / 16;  // E waves 0..2: one output column tile each
@@ -355,6 +331,35 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
     for (int ks = 0; ks < KS; ++ks) fwh[ks] = *reinterpret_cast<const bf16x8*>(wr + ks * 32);
   }
   const bf16x8* fwl = fwlo + ct * KS * 64 + lane;
+  // h1 plane staging by LDS-DMA (buffer_load_dwordx4 ... lds: no VGPR destination): piece
+  // j = 4 k + e (1 KiB = 64 lanes x 16 B, lane-linear in the plane image [PP][HID]) of the
+  // haloed plane; a halo position outside the volume gets an offset past the descriptor's
+  // range and a plane outside [0, D) a zero-range descriptor, so the DMA writes the zero
+  // padding itself
+  const T* src = reinterpret_cast<const T*>(a.h1) + (int64_t)b * D * H * W * HID;
+  const int64_t plane_elems = (int64_t)H * W * HID;
+  uint32_t off[NPCE];
+#pragma unroll
+  for (int k = 0; k < NPCE; ++k) {
+    const int i = min((4 * k + e) * 64 + lane, PP * NV - 1);
+    const int pos = i / NV, v = i - pos * NV;
+    const int yy = y0 - 1 + pos / PX, xx = x0 - 1 + pos % PX;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    off[k] = ok ? (uint32_t)(((yy * W + xx) * HID + 4 * v) * 4) : 0x80000000u;
+  }
+  auto stage = [&](int p, float* dst) {
+    const bool pz = p >= 0 && p < D;
+    const T* base = src + (int64_t)min(max(p, 0), D - 1) * plane_elems;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(base), 0, pz ? (int)(plane_elems * 4) : 0, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < NPCE; ++k) {
+      const int j = 4 * k + e;
+      if (j * 64 < PP * NV && (j * 64 + lane < PP * NV))
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(dst + j * 256), 16, off[k], 0, 0, 0);
+    }
+  };
   const int col = ct * 16 + 4 * g4;
   const float* sbase = a.stats ? a.stats : a.x;
   auto gpos_of = [&](int zo, int rt, bool clamp) {
@@ -407,9 +412,13 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
   };
 
   __syncthreads();  // (prologue) weights read out of the plane buffer
-  __syncthreads();  // (prologue) plane z0-1 visible
+  stage(z0 - 1, planes);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // (prologue) plane z0-1 staged
   for (int p = z0 - 1; p <= z1 + 2; ++p) {
     const int zo = p - 3;  // output plane this iteration stores
+    // plane p+1 into the buffer plane p-1 left (scattered last iteration)
+    if (p + 1 <= z1 && !(a.dbg & 8)) stage(p + 1, planes + ((p + 2 - z0) & 1) * PLANE_F);
     if (has_fc && zo >= z0 && zo < z1 && !(a.dbg & 4)) {
       const float* h2t = h2b + ((zo - z0) % 3) * H2F;
       fc_store(h2t, zo, 0);
@@ -422,6 +431,8 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
       load_resid(zo + 1, 1);
     }
     TB_PROBE(1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged plane has landed
+    TB_PROBE(2)
     __syncthreads();
     TB_PROBE(4)
   }
@@ -454,9 +465,9 @@ int launch_ffn_dwfc_tb(const DwFcArgs& a, int prec, hipStream_t s) {
   static const int dbg = getenv("WF_FFN_DBG") ? atoi(getenv("WF_FFN_DBG")) : 0;
   g.dbg = dbg;  // timing experiments only: bit mask of phases skipped (results invalid)
   const int64_t blocks = base * cdiv(g.D, g.ZS);
-  void (*kern)(DwFcArgs) = prec == PREC_SPLIT  ? ffn_dwfc_tb_kernel<PREC_SPLIT, float>
-                           : prec == PREC_FP16 ? ffn_dwfc_tb_kernel<PREC_FP16, float>
-                                               : ffn_dwfc_tb_kernel<PREC_BF16, uint16_t>;
+  if (prec != PREC_SPLIT && prec != PREC_FP16) return fail(WF_E_SHAPE, "ffn_dwfc_tb: fp32 h1 only");
+  void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_dwfc_tb_kernel<PREC_SPLIT, float>
+                                              : ffn_dwfc_tb_kernel<PREC_FP16, float>;
   set_max_lds(reinterpret_cast<const void*>(kern), (int)LDS_BYTES);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), LDS_BYTES, s, g);
   return check_launch("ffn_dwfc_tb");
