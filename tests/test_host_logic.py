@@ -125,3 +125,18 @@ def test_index_formula_tracks_in_place_writes():
     sd["relative_position_index"] = torch.zeros_like(sd["relative_position_index"])
     a.load_state_dict(sd)
     assert not a._formula_valid()
+
+
+def test_index_formula_survives_device_moves():
+    """A module that loaded a state_dict (buffer version > 0) and is then moved (.to / .cuda:
+    a fresh copy of the buffer at version 0) keeps the in-kernel formula -- the round-4
+    regression where eager fell back to the dense bias after .cuda() while a torch.compile
+    trace kept the formula (test_compile_block_fullgraph_matches_eager)."""
+    a = NM.Attention(48, num_heads=3, qkv_bias=True, window_size=4)
+    a.load_state_dict({k: v.clone() for k, v in a.state_dict().items()})
+    assert a.relative_position_index._version > 0 and a._formula_valid()
+    a._apply(lambda t: t.clone())  # what Module.to(device) does to every buffer
+    assert a.relative_position_index._version == 0
+    assert a._formula_valid()
+    a.relative_position_index.fill_(0)
+    assert not a._formula_valid()

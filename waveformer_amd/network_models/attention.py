@@ -52,7 +52,7 @@ class Attention(nn.Module):
         # Valid for the buffer version it was checked at: an in-place write afterwards
         # (copy_ / fill_) bumps the version and the forward falls back to the dense bias built
         # from the buffer's contents (no host sync in the forward).  A device move keeps the
-        # contents and starts the new tensor at version 0, like the checked one.
+        # contents and starts the new tensor at a fresh version counter: _apply re-records it.
         self._index_formula = True
         self._index_version = self.relative_position_index._version
         nn.init.trunc_normal_(self.relative_position_bias_table, std=.02)
@@ -63,6 +63,13 @@ class Attention(nn.Module):
         self._index_formula = ops.index_is_formula(self.relative_position_index,
                                                    self.window_size)
         self._index_version = self.relative_position_index._version
+
+    def _apply(self, fn, *args, **kwargs):
+        # .to() / .cuda() / .half() replace the buffer by a copy of the same contents (at a
+        # fresh version counter): the formula check still holds for the new tensor
+        ret = super()._apply(fn, *args, **kwargs)
+        self._index_version = self.relative_position_index._version
+        return ret
 
     def _formula_valid(self) -> bool:
         if not self._index_formula:
