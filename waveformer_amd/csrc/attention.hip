@@ -486,6 +486,13 @@ __device__ __forceinline__ int kswz(int row) {  // 16-B chunk XOR of a K row (se
   return (0x78 >> (2 * ((row >> 2) & 3))) & 3;  // {0, 2, 3, 1}[(row >> 2) & 3]
 }
 
+// WF_ATTN_MFMA_SUM=0: the softmax row sums as fp32 VALU adds instead of the ones-operand
+// MFMAs (4 of the 18 MFMAs per 64-key tile); measured slower -- 191 vs 171 us per B = 8
+// stage-1 launch (profiles/r4_attention_rowsum_ab.txt): the kernel's VALU, not its MFMA
+// pipe, is the tighter resource, so the default keeps the sums on the MFMA.
+#ifndef WF_ATTN_MFMA_SUM
+#define WF_ATTN_MFMA_SUM 1
+#endif
 template <int P>
 __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict__ qkv,
                                                           const float* __restrict__ table,
@@ -558,7 +565,11 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
     const int rb = (TBLN - 1) - ((qz + 7) * 23 + (qy + 7) * 15 + (qx + 7)) +
                    ((g4 >> 1) * 15 + 4 * (g4 & 1));
     f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+#if WF_ATTN_MFMA_SUM
     f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#else
+    float lsum = 0.f;  // this lane's 16 keys of each tile; the 4 key groups are summed at the end
+#endif
     float mrun = -INFINITY;
 #pragma unroll 2
     for (int t = 0; t < 8; ++t) {  // 64-key tiles (one z slice of the window each)
@@ -582,6 +593,9 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
       const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
       mrun = mnew;
       bf16x4 ph[4], pl[4];
+#if !WF_ATTN_MFMA_SUM
+      float ps[4];
+#endif
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
@@ -590,10 +604,18 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
           const uint16_t hb = op_cvt<P>(p);
           ph[kt][i] = (short)hb;
           pl[kt][i] = op_lo<P>(p, hb);
+#if !WF_ATTN_MFMA_SUM
+          ps[i] = kt == 0 ? p : ps[i] + p;  // 4 chains over the key sub-tiles
+#endif
         }
       }
+#if !WF_ATTN_MFMA_SUM
+      lsum = lsum * alpha + ((ps[0] + ps[1]) + (ps[2] + ps[3]));
+#endif
       o *= alpha;
+#if WF_ATTN_MFMA_SUM
       l4 *= alpha;
+#endif
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const bf16x8 pb = bf16x8{ph[2 * j][0], ph[2 * j][1], ph[2 * j][2], ph[2 * j][3],
@@ -612,13 +634,23 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
           const bf16x8 vl = bf16x8{w1[0], w1[1], w1[2], w1[3], w2[0], w2[1], w2[2], w2[3]};
           o = mma32<P>(vl, pb, o);
           o = mma32<P>(vh, plb, o);
+#if WF_ATTN_MFMA_SUM
           l4 = mma32<P>(ones, plb, l4);
+#endif
         }
         o = mma32<P>(vh, pb, o);
+#if WF_ATTN_MFMA_SUM
         l4 = mma32<P>(ones, pb, l4);
+#endif
       }
     }
+#if WF_ATTN_MFMA_SUM
     const float inv = 1.f / l4[0];
+#else
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    const float inv = 1.f / lsum;
+#endif
     const int64_t off = (row0 + q) * C + h * HD + 4 * g4;
     if (store32(P)) {
       *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off) = o * inv;
