@@ -279,6 +279,44 @@ def test_ccf_ffn_stage2_vs_oracle(shape, block):
         assert C.rel_l2(out, ref) <= tol, prec
 
 
+@pytest.mark.parametrize("C_,shape", [(192, (2, 8, 8, 8)), (192, (1, 5, 6, 11)),
+                                      (192, (1, 20, 4, 4)), (384, (2, 4, 4, 4)),
+                                      (384, (1, 3, 5, 2))])
+@pytest.mark.parametrize("block", [False, True])
+def test_ccf_ffn_stage34_vs_oracle(C_, shape, block):
+    """C = 192 / 384, hidden = 4C (encoder stages 3 / 4): the pwconv on gemm_kc with LN1
+    partials in its epilogue, the per-row finalize, the depthwise conv applying LN1 + GELU
+    while it stages its planes (round 4: no separate LayerNorm + GELU pass over h1; ragged
+    tiles, z segments and volume edges whose zero padding must stay zero), then the fc with
+    LN2 + GELU in its loader and the Q4 residual -- same bars as stages 1 / 2."""
+    import waveformer_amd.network_models as NM
+    from oracle.weight_rule import rule_state_dict
+    from waveformer_amd import ops
+    B = shape[0]
+    mlp = NM.CCF_FFN(C_, 4 * C_, img_size=shape[1:])
+    sd = rule_state_dict(mlp.state_dict())
+    mlp.load_state_dict(sd)
+    mlp = mlp.eval().to(DEV)
+    norm2 = torch.nn.LayerNorm(C_, eps=1e-6)
+    with torch.no_grad():
+        norm2.weight.copy_(seeded_randn((C_,), 37) * 0.2 + 1)
+        norm2.bias.copy_(seeded_randn((C_,), 38) * 0.1)
+    norm2 = norm2.to(DEV)
+    x = seeded_randn(shape + (C_,), 39)
+    bs = torch.tensor([0.5, 2.0, 1.0][:B])
+    if block:
+        n2 = F.layer_norm(x, [C_], norm2.weight.detach().cpu(), norm2.bias.detach().cpu(), 1e-6)
+        ref = x + R.ccf_ffn(sd, "", n2) * bs.view(-1, 1, 1, 1, 1)
+    else:
+        ref = x + (R.ccf_ffn(sd, "", x) - x) * bs.view(-1, 1, 1, 1, 1)
+    for prec, tol in (("bf16x3", 5e-5), ("bf16", 1e-2), ("fp16", 2e-3)):
+        with torch.no_grad(), ops.precision(prec):
+            xc = cuda(x)
+            stats = ops.msfuse([], xc, 1e-6)[1] if block else None
+            out = ops.ccf_ffn(xc, stats, norm2 if block else None, mlp, cuda(bs))
+        assert C.rel_l2(out, ref) <= tol, prec
+
+
 @pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11)])
 @pytest.mark.parametrize("block", [False, True])
 def test_ccf_ffn_stage2_staged_path_vs_oracle(shape, block, monkeypatch):

@@ -224,11 +224,17 @@ struct Store2<uint16_t> {
 // channel pairs (one 8-B LDS read per tap feeds both; the build has no packed-FP32
 // instructions, DESIGN.md 6.1, so each pair FMA is two v_fma_f32), and the per-position
 // 32-channel statistics reduce over 16 lanes.
-template <typename T>
+// LN1 (fp32 only): the input is the pwconv's raw output and h1 = GELU(LN1(.)) is formed in
+// the plane staging -- ln1_stats (M, 2) {mean, rstd} per position, ln1_w / ln1_b (Hd) -- so
+// the separate LayerNorm + GELU pass over h1 (read + write of the whole tensor) is gone
+// (stages 3 / 4 of the encoder); halo positions outside the volume stay zero.
+template <typename T, bool LN1>
 __global__ __launch_bounds__(256) void dwconv3d_kernel(
     const T* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias,
     T* __restrict__ out, float* __restrict__ pstats, int B, int Hd, int D, int H, int W, int ZS,
-    double* __restrict__ cstats) {
+    double* __restrict__ cstats, const float* __restrict__ ln1_stats,
+    const float* __restrict__ ln1_w, const float* __restrict__ ln1_b) {
+  static_assert(!LN1 || sizeof(T) == 4, "LN1 staging: fp32 h1");
   constexpr int CH = DW_CH, TX = DW_TX, TY = DW_TY;
   static_assert(CH == DW_STAT_GROUP, "one statistics group per workgroup channel chunk");
   static_assert(TX * (CH / 2) == 256, "one thread per (column, channel pair)");
@@ -237,6 +243,7 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
   constexpr int NV = CH / V::N;                  // 16-byte vectors per tile position
   constexpr int NLD = (PY * PX * NV + 255) / 256;
   __shared__ __attribute__((aligned(16))) float pl[2][PY * PX * CH];
+  __shared__ __attribute__((aligned(16))) float l1w[LN1 ? CH : 1], l1b[LN1 ? CH : 1];
 
   const int ncc = Hd / CH, ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY;
   const int nzs = (D + ZS - 1) / ZS;
@@ -265,8 +272,17 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
     w2[k] = f32x2{w[(c0 + 2 * cp) * 27 + k], w[(c0 + 2 * cp + 1) * 27 + k]};
   const f32x2 bv = f32x2{bias[c0 + 2 * cp], bias[c0 + 2 * cp + 1]};
 
+  if (LN1) {
+    for (int i = tid; i < CH; i += 256) {
+      l1w[i] = ln1_w[c0 + i];
+      l1b[i] = ln1_b[c0 + i];
+    }
+    __syncthreads();
+  }
   // staging of one input plane: item i -> (tile position i / NV, vector i % NV)
   typename V::raw stg[NLD];
+  f32x2 st1[LN1 ? NLD : 1];
+  bool ok1[LN1 ? NLD : 1];
   const T* src = in + (int64_t)b * D * H * W * Hd + c0;
   auto fetch = [&](int p) {
     const bool pz = p >= 0 && p < D;
@@ -278,16 +294,29 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
       const int yy = y0 - 1 + pos / PX, xx = x0 - 1 + pos % PX;
       const bool ok = pz && yy >= 0 && yy < H && xx >= 0 && xx < W;
       const int yc = min(max(yy, 0), H - 1), xc = min(max(xx, 0), W - 1);
-      const typename V::raw u = *reinterpret_cast<const typename V::raw*>(
-          src + (((int64_t)pc * H + yc) * W + xc) * Hd + V::N * v);
+      const int64_t gp = ((int64_t)pc * H + yc) * W + xc;
+      const typename V::raw u = *reinterpret_cast<const typename V::raw*>(src + gp * Hd + V::N * v);
       stg[j] = ok ? u : V::zero();
+      if constexpr (LN1) {
+        st1[j] = *reinterpret_cast<const f32x2*>(ln1_stats + ((int64_t)b * D * H * W + gp) * 2);
+        ok1[j] = ok;
+      }
     }
   };
   auto commit = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
       const int i = j * 256 + tid;
-      if (i < PY * PX * NV) V::put(pl[buf] + (size_t)i * V::N, stg[j]);
+      if (i < PY * PX * NV) {
+        if constexpr (LN1) {
+          const int v = i % NV;
+          const f32x4 lw = *reinterpret_cast<const f32x4*>(l1w + 4 * v);
+          const f32x4 lb = *reinterpret_cast<const f32x4*>(l1b + 4 * v);
+          const f32x4 y = gelu_erf4((stg[j] - st1[j].x) * st1[j].y * lw + lb);
+          stg[j] = ok1[j] ? y : V::zero();
+        }
+        V::put(pl[buf] + (size_t)i * V::N, stg[j]);
+      }
     }
   };
 
@@ -388,7 +417,8 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
 }
 
 int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, float* pstats,
-                    int B, int Hd, int D, int H, int W, int prec, hipStream_t s, double* cstats) {
+                    int B, int Hd, int D, int H, int W, int prec, hipStream_t s, double* cstats,
+                    const float* ln1_stats, const float* ln1_w, const float* ln1_b) {
   if (Hd % DW_CH != 0) return fail(WF_E_SHAPE, "dwconv3d: hidden width must be a multiple of 32");
   // z segment: enough workgroups to fill 256 CUs ~8 deep, but long enough that the two halo
   // planes per segment stay a small overhead
@@ -396,15 +426,47 @@ int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, f
   int ZS = D;
   while (ZS > 8 && base * cdiv(D, ZS) < 2048) ZS = (ZS + 1) / 2;
   const int64_t blocks = base * cdiv(D, ZS);
-  if (store32(prec))
-    hipLaunchKernelGGL((dwconv3d_kernel<float>), dim3((unsigned)blocks), dim3(256), 0, s,
+  if (ln1_stats) {
+    if (!store32(prec) || !ln1_w || !ln1_b)
+      return fail(WF_E_SHAPE, "dwconv3d: the LN1 staging needs fp32 h1 and LN1 weights");
+    hipLaunchKernelGGL((dwconv3d_kernel<float, true>), dim3((unsigned)blocks), dim3(256), 0, s,
                        reinterpret_cast<const float*>(in), w, b, reinterpret_cast<float*>(out),
-                       pstats, B, Hd, D, H, W, ZS, cstats);
+                       pstats, B, Hd, D, H, W, ZS, cstats, ln1_stats, ln1_w, ln1_b);
+  } else if (store32(prec))
+    hipLaunchKernelGGL((dwconv3d_kernel<float, false>), dim3((unsigned)blocks), dim3(256), 0, s,
+                       reinterpret_cast<const float*>(in), w, b, reinterpret_cast<float*>(out),
+                       pstats, B, Hd, D, H, W, ZS, cstats, nullptr, nullptr, nullptr);
   else
-    hipLaunchKernelGGL((dwconv3d_kernel<uint16_t>), dim3((unsigned)blocks), dim3(256), 0, s,
-                       reinterpret_cast<const uint16_t*>(in), w, b,
-                       reinterpret_cast<uint16_t*>(out), pstats, B, Hd, D, H, W, ZS, cstats);
+    hipLaunchKernelGGL((dwconv3d_kernel<uint16_t, false>), dim3((unsigned)blocks), dim3(256), 0,
+                       s, reinterpret_cast<const uint16_t*>(in), w, b,
+                       reinterpret_cast<uint16_t*>(out), pstats, B, Hd, D, H, W, ZS, cstats,
+                       nullptr, nullptr, nullptr);
   return check_launch("dwconv3d");
+}
+
+__global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float* __restrict__ ps,
+                                                                int np, int group, float eps,
+                                                                float* __restrict__ out,
+                                                                int64_t M) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= M) return;
+  const float2* p = reinterpret_cast<const float2*>(ps) + r * np;
+  float mu = 0.f;
+  for (int i = 0; i < np; ++i) mu += p[i].x;
+  mu *= 1.f / np;
+  float m2 = 0.f;
+  for (int i = 0; i < np; ++i) {
+    const float d = p[i].x - mu;
+    m2 += p[i].y + (float)group * d * d;
+  }
+  *reinterpret_cast<float2*>(out + 2 * r) = float2{mu, rsqrtf(m2 / ((float)np * group) + eps)};
+}
+
+int launch_ln_stats_finalize(const float* pstats, int np, int group, float eps, float* out,
+                             int64_t M, hipStream_t s) {
+  hipLaunchKernelGGL(ln_stats_finalize_kernel, dim3((unsigned)cdiv(M, 256)), dim3(256), 0, s,
+                     pstats, np, group, eps, out, M);
+  return check_launch("ln_stats_finalize");
 }
 
 template <typename T>
@@ -462,7 +524,10 @@ extern "C" int64_t wf_ccf_ffn_workspace_bytes(int64_t B, int64_t C, int64_t hidd
   const int64_t one = ((B * D * H * W * hidden * e) + 255) & ~(int64_t)255;
   // + the dwconv's per-32-channel-group {mean, M2} of every position (LN2 in the fc loader)
   const int64_t st = B * D * H * W * (hidden / DW_STAT_GROUP) * 2 * 4;
-  return 2 * one + ((st + 255) & ~(int64_t)255);
+  // + the pwconv's per-column-chunk LN1 partials (<= hidden / 32 chunks) and their per-row
+  // {mean, rstd} (stages 3 / 4: LN1 + GELU applied in the dwconv staging)
+  const int64_t s1 = B * D * H * W * 2 * 4;
+  return 2 * one + 2 * ((st + 255) & ~(int64_t)255) + ((s1 + 255) & ~(int64_t)255);
 }
 
 extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
@@ -568,8 +633,31 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
     d.eps1 = eps1;
     return launch_ffn_fused(d, precision, s);
   }
+  // stages 3 / 4 at inference: the pwconv epilogue writes LN1 partials, a finalize pass makes
+  // the per-row {mean, rstd}, and the dwconv applies LN1 + GELU while staging its planes --
+  // no separate LayerNorm + GELU pass over h1 (WF_FFN_LN1_PASS=1: the round-3 pass, A/B).
+  // Training (keep) stores h1 = GELU(LN1(.)) for the backward: the pass stays.
+  static const bool ln1_pass = getenv("WF_FFN_LN1_FUSE") == nullptr;  // (pending GPU A/B)
+  const int64_t stq = ((M * (hidden / DW_STAT_GROUP) * 2 * 4) + 255) & ~(int64_t)255;
+  float* pw_pst = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 2 * one + stq);
+  float* ln1_st = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 2 * one + 2 * stq);
+  int pw_np = 0;
+  if (split_ln1 && !keep && !ln1_pass && hidden % DW_STAT_GROUP == 0 &&
+      getenv("WF_FFN_FUSED_DW") == nullptr) {
+    GemmArgs g2 = g;
+    g2.epi = EPI_STORE;
+    const int nt = gemm_kc_pick_nt(g2);
+    if (nt > 0 && hidden % (16 * nt) == 0) pw_np = (int)(hidden / (16 * nt));
+  }
   if (stage == 0 || stage == 1) {
-    if (split_ln1) {
+    if (split_ln1 && pw_np > 0) {
+      GemmArgs g2 = g;
+      g2.epi = EPI_STORE;
+      g2.o_pstats = pw_pst;
+      rc = launch_gemm(g2, s, "wf_ccf_ffn_fwd(pwconv)");
+      if (!rc)
+        rc = launch_ln_stats_finalize(pw_pst, pw_np, (int)(hidden / pw_np), eps1, ln1_st, M, s);
+    } else if (split_ln1) {
       GemmArgs g2 = g;
       g2.epi = EPI_STORE;
       rc = launch_gemm(g2, s, "wf_ccf_ffn_fwd(pwconv)");
@@ -614,7 +702,10 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   WF_REQUIRE(!keep || split_ln, "training needs hidden % 32 == 0 (h2 kept pre-LayerNorm)");
   float* pst = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 2 * one);
   if (stage == 0 || stage == 2) {
-    if (split_ln)
+    if (split_ln && split_ln1 && pw_np > 0)  // LN1 + GELU in the staging
+      rc = launch_dwconv3d(h1, dw_w, dw_b, h2, pst, (int)B, (int)hidden, (int)D, (int)H,
+                           (int)W, precision, s, nullptr, ln1_st, ln1_w, ln1_b);
+    else if (split_ln)
       rc = launch_dwconv3d(h1, dw_w, dw_b, h2, pst, (int)B, (int)hidden, (int)D, (int)H,
                            (int)W, precision, s);
     else

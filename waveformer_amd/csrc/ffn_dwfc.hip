@@ -759,8 +759,8 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc_sb_kernel(DwFcArgs a) {
   constexpr int NLDE = (K::PP * K::NV + NE - 1) / NE;  // staged vectors per E thread (12)
   constexpr int H2F = K::NPOS * K::HS;
   constexpr int LNL = 16, LNC = HID / LNL;             // LN2: 16 lanes x 12 channels / position
-#ifndef WF_SB_LN2T
-#define WF_SB_LN2T 0
+#ifndef WF_SB_LN2T  // LN2 statistics by short chains (round 4: 1009-1012 vs 1020-1027 us)
+#define WF_SB_LN2T 1
 #endif
 #ifndef WF_SB_SPLIT
 #define WF_SB_SPLIT 0

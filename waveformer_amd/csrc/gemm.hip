@@ -321,6 +321,11 @@ int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who) {
   // gemm_ares takes the remaining shapes.  (WF_GEMM_ARES_ONLY / WF_GEMM_NO_KC: A/B switches)
   static const bool ares_only = getenv("WF_GEMM_ARES_ONLY") != nullptr;
   static const bool no_kc = getenv("WF_GEMM_NO_KC") != nullptr;
+  if (g.o_pstats) {  // LayerNorm partials in the epilogue: gemm_kc only
+    if (g.epi == EPI_STORE && !g.out_bf16 && !g.a_bf16 && try_launch_gemm_kc(g, s))
+      return check_launch(who);
+    return fail(WF_E_SHAPE, std::string(who) + ": LN-partial epilogue needs the gemm_kc shape");
+  }
   if (!ares_only) {
     if (try_launch_gemm_lnw(g, s)) return check_launch(who);
     if (try_launch_gemm_rows(g, s, !no_kc)) return check_launch(who);

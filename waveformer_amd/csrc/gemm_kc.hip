@@ -275,6 +275,28 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
         rs_ = g.r_stats[2 * rowc + 1];
       }
       if (g.r_scale) bs = g.r_scale[rowc / (int)g.rows_per_sample];
+    } else if (EPI == EPI_STORE && !ABF16) {
+      // LayerNorm partials of this row's NC stored columns (fp32 stores only: the statistics
+      // are those of the stored values): {mean, M2} over the 4 lanes of the row
+      if (g.o_pstats) {
+        float sm = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) sm += (acc[rt][t].x + acc[rt][t].y) + (acc[rt][t].z + acc[rt][t].w);
+        sm += __shfl_xor(sm, 16, 64);
+        sm += __shfl_xor(sm, 32, 64);
+        const float mu = sm * (1.f / NC);
+        float q = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const f32x4 d = acc[rt][t] - mu;
+          q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+        }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (rv && g4 == 0)
+          *reinterpret_cast<float2*>(g.o_pstats + ((int64_t)row * gridDim.y + blockIdx.y) * 2) =
+              float2{mu, q};
+      }
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -348,7 +370,8 @@ static void dispatch_kc(int nt, const GemmArgs& g, hipStream_t s) {
   }
 }
 
-int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s) {
+// column tiles per workgroup gemm_kc would use for g (0: it does not take the shape)
+int gemm_kc_pick_nt(const GemmArgs& g) {
   if (g.N % 32 != 0 || g.K < 8 || g.M >= ((int64_t)1 << 31)) return 0;
   const bool known = (g.a_map == MAP_WINDOW && g.epi == EPI_STORE) ||
                      (g.a_map == MAP_IDENTITY) || (g.a_map == MAP_MERGE && g.epi == EPI_STORE);
@@ -369,6 +392,11 @@ int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s) {
     if (nt == 0 || (g.epi != EPI_LN_GELU && blocks(nt) < 512 && c >= 3)) nt = c;
     if (blocks(nt) >= 512) break;
   }
+  return nt;
+}
+
+int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s) {
+  const int nt = gemm_kc_pick_nt(g);
   if (nt == 0) return 0;
   if (g.a_map == MAP_WINDOW) dispatch_kc<MAP_WINDOW, EPI_STORE>(nt, g, s);
   else if (g.a_map == MAP_MERGE) dispatch_kc<MAP_MERGE, EPI_STORE>(nt, g, s);

@@ -20,8 +20,12 @@
 
 namespace wf {
 
-template <int NT, int P, int MAP, int EPI, bool ABF16>
-__global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
+// NTH = 768 (LN + GELU epilogue with fp32 output, WF_GEMM_ROWS_12W=1): 12 waves per
+// workgroup, three per SIMD -- the epilogue's LayerNorm / GELU VALU work needs three waves to
+// reach the SIMD's issue rate (tools/ubench_valu.hip); the output restaging then goes through
+// LDS 8 rows at a time so 12 waves' staging buffers fit next to the weight chunk
+template <int NT, int P, int MAP, int EPI, bool ABF16, int NTH = 512>
+__global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
   constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   extern __shared__ __attribute__((aligned(16))) uint16_t Wl[];  // [NB][NT*16][KP]
   const int K = g.K, N = g.N;
@@ -65,7 +69,8 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
   // tile's 16 contiguous rows (the accumulator layout writes 16 rows x 64 B per instruction)
   constexpr bool STAGE = EPI == EPI_LN_GELU && P != PREC_BF16;
   constexpr int OST = NCOL + 4;  // staged row stride in floats (16-B pad)
-  float* ostg = elb + NCOL + (STAGE ? (threadIdx.x >> 6) * 16 * OST : 0);
+  constexpr int SROWS = NTH > 512 ? 8 : 16;  // rows staged per pass
+  float* ostg = elb + NCOL + (STAGE ? (threadIdx.x >> 6) * SROWS * OST : 0);
   for (int i = tid; i < K32; i += blockDim.x) {
     const bool ok = a_ln != LN_NONE && i < K;
     lnw[i] = ok ? g.a_ln_w[i] : 0.f;
@@ -337,7 +342,10 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), orsrc,
                                                 (int)((row * g.ldo + col) * 2), 0, 0);
         } else if (STAGE) {
-          *reinterpret_cast<f32x4*>(ostg + l15 * OST + t * 16 + 4 * g4) = v;
+          if constexpr (SROWS == 16)
+            *reinterpret_cast<f32x4*>(ostg + l15 * OST + t * 16 + 4 * g4) = v;
+          else
+            acc[t] = v;  // staged below, 8 rows per pass
         } else {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), orsrc,
                                                  (int)((row * g.ldo + col) * 4), 0, 0);
@@ -363,20 +371,31 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
     if constexpr (STAGE) {
       // one wave's LDS operations complete in issue order; the fences only keep the compiler
       // from moving the lanes' exchange
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       constexpr int RC = NCOL / 4;  // 16-B chunks per row
 #pragma unroll
-      for (int j = 0; j < 16 * RC / 64; ++j) {
-        const int c = j * 64 + lane, r = c / RC, c4 = c - r * RC;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(ostg + r * OST + 4 * c4);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), orsrc,
-                                               (int)(((tile * 16 + r) * g.ldo + 4 * c4) * 4), 0, 0);
+      for (int half = 0; half < 16 / SROWS; ++half) {
+        if constexpr (SROWS < 16) {
+          if ((l15 >> 3) == half) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+              *reinterpret_cast<f32x4*>(ostg + (l15 & 7) * OST + t * 16 + 4 * g4) = acc[t];
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < SROWS * RC / 64; ++j) {
+          const int c = j * 64 + lane, r = c / RC, c4 = c - r * RC;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(ostg + r * OST + 4 * c4);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(u32x4, v), orsrc,
+              (int)(((tile * 16 + half * SROWS + r) * g.ldo + 4 * c4) * 4), 0, 0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     arow_c = arow_n;
     rm = rmn;
@@ -386,6 +405,19 @@ __global__ __launch_bounds__(512) void gemm_rows_kernel(GemmArgs g) {
 template <int NT, int MAP, int EPI>
 static void go_rows(const GemmArgs& g, dim3 grid, size_t lds, hipStream_t s) {
   void (*kern)(GemmArgs);
+  if constexpr (EPI == EPI_LN_GELU && MAP == MAP_IDENTITY) {
+    static const bool w12 = getenv("WF_GEMM_ROWS_12W") != nullptr;
+    if (w12 && !g.a_bf16 && g.prec != PREC_BF16) {
+      kern = g.prec == PREC_SPLIT ? gemm_rows_kernel<NT, PREC_SPLIT, MAP, EPI, false, 768>
+                                  : gemm_rows_kernel<NT, PREC_FP16, MAP, EPI, false, 768>;
+      // the 16-row staging of 8 waves (the host's lds) -> 8 rows of 12 waves
+      const size_t lds12 = lds - (size_t)8 * 16 * (NT * 16 + 4) * 4 + (size_t)12 * 8 * (NT * 16 + 4) * 4;
+      set_max_lds(reinterpret_cast<const void*>(kern), (int)lds12);
+      const unsigned gx = (unsigned)std::min<int64_t>(cdiv((g.M + 15) / 16, 12), 256);
+      hipLaunchKernelGGL(kern, dim3(gx, grid.y), dim3(768), lds12, s, g);
+      return;
+    }
+  }
   if (g.a_bf16)  // bf16 activations only exist in PREC_BF16
     kern = gemm_rows_kernel<NT, PREC_BF16, MAP, EPI, true>;
   else if (g.prec == PREC_SPLIT)

@@ -96,9 +96,13 @@ struct GemmArgs {
   const float* r_ln_b;
   const float* r_scale;  //   per-sample factor on the added branch (DropPath) or NULL
   int64_t rows_per_sample; // M / B for r_scale
+  float* o_pstats;       // EPI_STORE (gemm_kc): if non-NULL, per (row, column chunk) {mean, M2}
+                         //   of the stored values, (M, N / chunk, 2) -- LN statistics partials
 };
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);
+// column tiles (of 16) per workgroup gemm_kc would use for g, 0 if it does not take the shape
+int gemm_kc_pick_nt(const GemmArgs& g);
 // InstanceNorm partial sums (sum, sum of squares per (b, c)) of a channel-last tensor into a
 // zeroed (B, C, 2) fp64 accumulator (instnorm.hip)
 int launch_instnorm_partial(const float* x, int64_t ldx, int64_t B, int64_t C, int64_t P,
@@ -124,7 +128,11 @@ int launch_dwconv_ln_gelu(const void* in, const float* w, const float* b, const 
 // cstats (optional): zeroed (B, Hd, 2) fp64 {sum, sum of squares} of the outputs per channel
 int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, float* pstats,
                     int B, int Hd, int D, int H, int W, int prec, hipStream_t s,
-                    double* cstats = nullptr);
+                    double* cstats = nullptr, const float* ln1_stats = nullptr,
+                    const float* ln1_w = nullptr, const float* ln1_b = nullptr);
+// per-row {mean, rstd} from np equal-size {mean, M2} partials (Chan et al.), (M, 2)
+int launch_ln_stats_finalize(const float* pstats, int np, int group, float eps, float* out,
+                             int64_t M, hipStream_t s);
 constexpr int DW_STAT_GROUP = 32;
 // ---- CCF_FFN back half fused (ffn_dwfc.hip): dwconv + bias + LN2 + GELU + fc + bias + the
 // Block's Q4 residual, for C = 48, hidden = 192 (h1 fp32 for PREC_SPLIT, bf16 for PREC_BF16)
