@@ -258,31 +258,37 @@ def idwt_roofline(batch, dev, layout="cl"):
     # w, C) output (ops.dwt3d_haar)
     bands = torch.randn(8, batch, 64, 64, 64, 48, device=dev, generator=g)
     det = [{k: bands[i + 1].permute(0, 4, 1, 2, 3) for i, k in enumerate(ops.DETAIL_KEYS)}]
-    if layout == "cl":
+    skip = None
+    if layout in ("cl", "cat"):
         ll = bands[0].permute(0, 4, 1, 2, 3)                     # channel-last view
         out = ops.empty_cl(batch, 96, 128, 128, 128, dev)
+        if layout == "cat":  # + torch.cat((out, skip), 1) in the same kernel
+            skip = ops.empty_cl(batch, 48, 128, 128, 128, dev).normal_(generator=g)
     else:
         ll = bands[0].permute(0, 4, 1, 2, 3).contiguous()
         out = torch.empty(batch, 96, 128, 128, 128, device=dev)
-    ops.idwt3d_haar(ll, det, out=out)
+    ops.idwt3d_haar(ll, det, out=out, skip=skip)
     reps = 10
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
-        ops.idwt3d_haar(ll, det, out=out)
+        ops.idwt3d_haar(ll, det, out=out, skip=skip)
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / reps * 1e3
     alg = 8 * batch * 48 * 128 ** 3  # 8 B per output element (4 B of bands read + 4 B written)
+    if layout == "cat":
+        alg *= 2  # + the skip: 4 B read + 4 B written per element
     ach = alg / (us * 1e-6) / 1e9
-    del bands, ll, det, out
-    kname = "idwt3d_haar_cl4" if layout == "cl" else "idwt3d_haar_nc4"
+    del bands, ll, det, out, skip
+    kname = {"cl": "idwt3d_haar_cl4", "cat": "idwt3d_haar_cl4", "ncdhw": "idwt3d_haar_nc4"}[layout]
     return {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(kname, batch), "algorithmic_bytes_per_launch": alg,
             "avg_launch_us": round(us, 2), "launches_timed": reps,
             "shape": f"channel-last bands 8 x ({batch}, 64^3, 48) -> ({batch}, 48, 128^3) "
-                     f"{'channel-last' if layout == 'cl' else 'NCDHW'} into a 96-channel buffer"}
+                     f"{'NCDHW' if layout == 'ncdhw' else 'channel-last'} into a 96-channel "
+                     f"buffer" + (" + the 48-channel skip into its other half" if layout == "cat" else "")}
 
 
 def build_encoder(img, device):
@@ -732,6 +738,7 @@ def main():
         if args.op_timers and not full:
             out["rooflines"]["idwt3d_haar"] = idwt_roofline(args.batch, dev, "cl")
             out["rooflines"]["idwt3d_haar_ncdhw"] = idwt_roofline(args.batch, dev, "ncdhw")
+            out["rooflines"]["idwt3d_haar_cat"] = idwt_roofline(args.batch, dev, "cat")
         if "window_attention" in out["rooflines"]:
             vf, src = pmc_valu("attn_tbl_kernel", args.batch)
             if vf is not None:

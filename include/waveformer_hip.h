@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 12
+#define WF_ABI_VERSION 13
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
@@ -123,6 +123,17 @@ int wf_idwt3d_haar_cl(const float* ll, int64_t ll_bstride, int64_t ll_cstride,
                       int64_t ll_pstride, const float* const* det, const int64_t* det_s,
                       int levels, float* out, int64_t out_bstride, int64_t ldo, int64_t B,
                       int64_t C, int64_t d, int64_t h, int64_t w, void* stream);
+
+/* wf_idwt3d_haar_cl fused with the concatenation that follows it (ABI 13; idwt_upsample.py:
+ * 160-163, torch.cat((out, skip), 1)): also writes the C skip channels into channels [C, 2C)
+ * of the same rows, skip element (b, c, pos) at skip[b*skip_bstride + pos*skip_ld + c]
+ * (channel-last; skip_ld, skip_bstride multiples of 4, 16-byte aligned; ldo >= 2C).  Whole
+ * 2C-channel rows leave the kernel instead of two half-row passes.                        */
+int wf_idwt3d_haar_cl_cat(const float* ll, int64_t ll_bstride, int64_t ll_cstride,
+                          int64_t ll_pstride, const float* const* det, const int64_t* det_s,
+                          int levels, const float* skip, int64_t skip_bstride, int64_t skip_ld,
+                          float* out, int64_t out_bstride, int64_t ldo, int64_t B, int64_t C,
+                          int64_t d, int64_t h, int64_t w, void* stream);
 
 /* ---- channel-last data movement of the decoder (ABI 12) ---------------------------- */
 /* dst[p*ldd + c] = src[p*lds + c] for P positions x C channels (C, lds, ldd multiples of 4,

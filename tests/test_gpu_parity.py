@@ -131,6 +131,30 @@ def test_idwt_vector_paths_match_scalar(levels, C_, base):
     assert torch.all(nc[:, C_:] == 3.0) and torch.all(cl[:, C_:] == 3.0)
 
 
+@pytest.mark.parametrize("levels,C_,base", [(1, 48, (4, 4, 8)), (2, 12, (2, 1, 2))])
+def test_idwt_fused_concat(levels, C_, base):
+    """wf_idwt3d_haar_cl_cat (ABI 13): the IDWT into channels [0, C) and the skip into [C, 2C)
+    of the decoder's channel-last concat buffer in one kernel -- bit-identical to the IDWT
+    followed by the copy (idwt_upsample.py:160-163), the skip copied exactly."""
+    from waveformer_amd import ops
+    B = 2
+    full = tuple(b * 2 ** levels for b in base)
+    co = R.wavedec3(seeded_randn((B, C_) + full, 13), "db1", levels)
+    ll = cuda(co[0]).contiguous(memory_format=torch.channels_last_3d)
+    dets = [{k: cuda(v).permute(0, 2, 3, 4, 1).contiguous().permute(0, 4, 1, 2, 3)
+             for k, v in d.items()} for d in co[1:]]
+    skip = cuda(seeded_randn((B, C_) + full, 14)).contiguous(memory_format=torch.channels_last_3d)
+    want = torch.full((B, 2 * C_) + full, 5.0, device=DEV).contiguous(
+        memory_format=torch.channels_last_3d)
+    ops.idwt3d_haar(ll, dets, out=want)
+    ops.copy_cl(skip, want[:, C_:])
+    got = torch.full((B, 2 * C_) + full, 5.0, device=DEV).contiguous(
+        memory_format=torch.channels_last_3d)
+    ops.idwt3d_haar(ll, dets, out=got, skip=skip)
+    assert torch.equal(got, want)
+    assert torch.equal(got[:, C_:], skip)
+
+
 def test_encoder_hf_feed_idwt_roundtrip():
     """DWT bands of the forward kernel, re-synthesised by the IDWT kernel, give back the input
     (Haar is orthonormal): the property that holds at full 128^3 sizes."""

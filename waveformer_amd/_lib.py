@@ -36,6 +36,8 @@ SIGNATURES = {
     "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar_cl": (_I, [_P, _I64, _I64, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64,
                                _I64, _I64, _I64, _P]),
+    "wf_idwt3d_haar_cl_cat": (_I, [_P, _I64, _I64, _I64, _P, _P, _I, _P, _I64, _I64, _P, _I64,
+                                   _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_copy_cl": (_I, [_P, _I64, _P, _I64, _I64, _I64, _P]),
     "wf_subvoxel_scatter_cl": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_convtranspose2_cl": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
@@ -118,7 +120,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 _lock = threading.Lock()
 _lib = None
 _err = None

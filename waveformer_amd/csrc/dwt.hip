@@ -114,6 +114,8 @@ struct IdwtArgs {
   int64_t out_bstride;
   int64_t ldo;   // channel-last output (CL kernel): floats between positions, channels contiguous
   int levels, B, C, d, h, w, CB;
+  const float* skip;             // cl4 kernel: concat skip rows (channel-last) or NULL
+  int64_t skip_bstride, skip_ld;
 };
 
 __device__ __forceinline__ float idwt_coef(const IdwtArgs& a, int l, int k, int b, int c,
@@ -275,6 +277,23 @@ __global__ __launch_bounds__(256) void idwt3d_haar_cl4_kernel(IdwtArgs a, int64_
   }
   const int Wo = 2 * w1, Ho = 2 * h1;
   float* ob = a.out + b * a.out_bstride + c;
+  if (a.skip) {  // torch.cat((out, skip), 1): the same 4 channels of the skip, C further
+    const float* sb = a.skip + b * a.skip_bstride + c;
+    f32x4 sk[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int zo = 2 * z1 + (n >> 2), yo = 2 * y1 + ((n >> 1) & 1), xo = 2 * x1 + (n & 1);
+      sk[n] = *reinterpret_cast<const f32x4*>(sb + (((int64_t)zo * Ho + yo) * Wo + xo) * a.skip_ld);
+    }
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int zo = 2 * z1 + (n >> 2), yo = 2 * y1 + ((n >> 1) & 1), xo = 2 * x1 + (n & 1);
+      float* o = ob + (((int64_t)zo * Ho + yo) * Wo + xo) * a.ldo;
+      *reinterpret_cast<f32x4*>(o) = v[n] * kHaar3;
+      *reinterpret_cast<f32x4*>(o + a.C) = sk[n];
+    }
+    return;
+  }
 #pragma unroll
   for (int n = 0; n < 8; ++n) {
     const int zo = 2 * z1 + (n >> 2), yo = 2 * y1 + ((n >> 1) & 1), xo = 2 * x1 + (n & 1);
@@ -422,7 +441,8 @@ extern "C" int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float*
 static int idwt_launch(const float* ll, int64_t ll_bstride, int64_t ll_cs, int64_t ll_ps,
                        const float* const* det, const int64_t* det_s, int levels, float* out,
                        int64_t out_bstride, int64_t ldo, int64_t B, int64_t C, int64_t d,
-                       int64_t h, int64_t w, void* stream) {
+                       int64_t h, int64_t w, void* stream, const float* skip = nullptr,
+                       int64_t skip_bstride = 0, int64_t skip_ld = 0) {
   WF_REQUIRE(levels >= 1 && levels <= kMaxLevels, "levels must be in [1, 4]");
   WF_REQUIRE(B >= 1 && C >= 1 && d >= 1 && h >= 1 && w >= 1, "empty tensor");
   WF_REQUIRE_PTR(ll);
@@ -461,6 +481,15 @@ static int idwt_launch(const float* ll, int64_t ll_bstride, int64_t ll_cs, int64
     for (int k = 0; k < 7 && vec; ++k) vec = al16(det[l * 7 + k]);
   }
   vec = vec && al16(out) && out_bstride % 4 == 0;
+  if (skip) {
+    WF_REQUIRE(vec && cl && ll_cs == 1 && ll_ps % 4 == 0 && ll_bstride % 4 == 0 && al16(ll) &&
+                   ldo % 4 == 0 && ldo >= 2 * C && al16(skip) && skip_ld % 4 == 0 &&
+                   skip_ld >= C && skip_bstride % 4 == 0,
+               "fused concat: channel-last LL / details / skip / output, 16-B aligned, C % 4 == 0");
+    a.skip = skip;
+    a.skip_bstride = skip_bstride;
+    a.skip_ld = skip_ld;
+  }
   if (vec && cl && ll_cs == 1 && ll_ps % 4 == 0 && ll_bstride % 4 == 0 && al16(ll) && ldo % 4 == 0) {
     const int64_t total = B * d1 * h1 * w1 * (C / 4);
     hipLaunchKernelGGL(idwt3d_haar_cl4_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
@@ -512,4 +541,16 @@ extern "C" int wf_idwt3d_haar_cl(const float* ll, int64_t ll_bstride, int64_t ll
   WF_REQUIRE(ll_cstride >= 1 && ll_pstride >= 1, "LL strides must be positive");
   return idwt_launch(ll, ll_bstride, ll_cstride, ll_pstride, det, det_s, levels, out,
                      out_bstride, ldo, B, C, d, h, w, stream);
+}
+
+extern "C" int wf_idwt3d_haar_cl_cat(const float* ll, int64_t ll_bstride, int64_t ll_cstride,
+                                     int64_t ll_pstride, const float* const* det,
+                                     const int64_t* det_s, int levels, const float* skip,
+                                     int64_t skip_bstride, int64_t skip_ld, float* out,
+                                     int64_t out_bstride, int64_t ldo, int64_t B, int64_t C,
+                                     int64_t d, int64_t h, int64_t w, void* stream) {
+  WF_REQUIRE_PTR(skip);
+  WF_REQUIRE(ldo >= 2 * C, "fused concat: ldo must be >= 2C");
+  return idwt_launch(ll, ll_bstride, ll_cstride, ll_pstride, det, det_s, levels, out,
+                     out_bstride, ldo, B, C, d, h, w, stream, skip, skip_bstride, skip_ld);
 }

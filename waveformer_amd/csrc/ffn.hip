@@ -633,11 +633,15 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
     d.eps1 = eps1;
     return launch_ffn_fused(d, precision, s);
   }
-  // stages 3 / 4 at inference: the pwconv epilogue writes LN1 partials, a finalize pass makes
-  // the per-row {mean, rstd}, and the dwconv applies LN1 + GELU while staging its planes --
-  // no separate LayerNorm + GELU pass over h1 (WF_FFN_LN1_PASS=1: the round-3 pass, A/B).
-  // Training (keep) stores h1 = GELU(LN1(.)) for the backward: the pass stays.
-  static const bool ln1_pass = getenv("WF_FFN_LN1_FUSE") == nullptr;  // (pending GPU A/B)
+  // stages 3 / 4 at inference, WF_FFN_LN1_FUSE=1: the pwconv epilogue writes LN1 partials, a
+  // finalize pass makes the per-row {mean, rstd}, and the dwconv applies LN1 + GELU while
+  // staging its planes (no separate LayerNorm + GELU pass over h1).  Training (keep) stores
+  // h1 = GELU(LN1(.)) for the backward: the pass stays.
+  // opt-in (WF_FFN_LN1_FUSE=1): the LN1 + GELU in the staging measured slower than the
+  // separate pass -- the depthwise conv 64 -> 130 us (stage 3) and 36 -> 82 us (stage 4)
+  // against 44 / 21 us for ln_act_fwd (round 4): the halo-redundant GELU on the staging
+  // lanes costs more than the h1 round trip through HBM at these small shapes
+  static const bool ln1_pass = getenv("WF_FFN_LN1_FUSE") == nullptr;
   const int64_t stq = ((M * (hidden / DW_STAT_GROUP) * 2 * 4) + 255) & ~(int64_t)255;
   float* pw_pst = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 2 * one + stq);
   float* ln1_st = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 2 * one + 2 * stq);

@@ -34,7 +34,12 @@ struct KcCfg {
   static constexpr int WPT = (WITEMS + NTHR - 1) / NTHR;  // per thread
 };
 
-template <int NT, int P, int MAP, int EPI, bool ABF16>
+// KR > 0 (K == 32 KR, LN_COMPUTE, one row tile per wave; PatchMerging 1 -> 2 at K = 384):
+// the lane's whole A row share (KR k-octets, 8 KR floats) is loaded ONCE into registers before
+// the k loop, the LayerNorm moments come from those registers and the (fully unrolled) k loop
+// reads them again -- the round-3 statistics pass and the k loop each streamed the rows, and
+// with 128-row workgroups the second read missed L2 (PMC 2.2x the input bytes)
+template <int NT, int P, int MAP, int EPI, bool ABF16, int KR = 0>
 __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
   typedef KcCfg<NT> C;
   constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
@@ -94,6 +99,31 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
       mean[rt] = g.a_stats[2 * arow[rt]];
       rstd[rt] = g.a_stats[2 * arow[rt] + 1];
     }
+  }
+  float areg[KR > 0 ? KR : 1][8];
+  if constexpr (KR > 0) {
+    static_assert(C::RT == 1, "register-resident A: one row tile per wave");
+    const RowMapper<MAP> rm(g, arow[0]);
+#pragma unroll
+    for (int ks = 0; ks < KR; ++ks) load8f<ABF16>(g.a_src, rm.offset(g, ks * KC_BK + 8 * g4), areg[ks]);
+    // the same shifted one-pass moments as below, in the same order (octet g4 + 4 ks)
+    const float sh = __shfl(areg[0][0], l15, 64);
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KR; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = areg[ks][j] - sh;
+        s += d;
+        q += d * d;
+      }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float ms = s / (float)K;
+    mean[0] = sh + ms;
+    rstd[0] = rsqrtf(fmaxf(q / (float)K - ms * ms, 0.f) + g.a_eps);
   } else if (g.a_ln == LN_COMPUTE) {
     // one pass: sums of x - s and (x - s)^2 with s = the row's first element (keeps the
     // variance free of cancellation when |mean| >> std); the 4 lanes of a row split the k range
@@ -153,6 +183,7 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
 
   float an[RT][8];
   auto afetch = [&](int ks) {
+    if constexpr (KR > 0) return;
     const int k = min(ks * KC_BK + 8 * g4, K - 8);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -176,15 +207,14 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
   afetch(0);
   __syncthreads();
   int buf = 0;
-#pragma unroll 1
-  for (int ks = 0; ks < nks; ++ks) {
+  auto kbody = [&](int ks, const float (&vin)[RT][8]) {
     const int k = ks * KC_BK + 8 * g4;
     const bool kv = k < K;
     float v[RT][8];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[rt][j] = an[rt][j];
+      for (int j = 0; j < 8; ++j) v[rt][j] = vin[rt][j];
     wfetch(min(ks + 1, nks - 1));  // next step's weight slice (last step: unused re-read)
     afetch(min(ks + 1, nks - 1));
     bf16x8 ah[RT], al[RT];
@@ -239,6 +269,25 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
     wcommit(buf ^ 1);
     __syncthreads();
     buf ^= 1;
+  };
+  if constexpr (KR > 0) {
+#pragma unroll
+    for (int ks = 0; ks < KR; ++ks) {
+      float vin[RT][8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vin[0][j] = areg[ks][j];
+      kbody(ks, vin);
+    }
+  } else {
+#pragma unroll 1
+    for (int ks = 0; ks < nks; ++ks) {
+      float vin[RT][8];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vin[rt][j] = an[rt][j];
+      kbody(ks, vin);
+    }
   }
 
   // ---- epilogue: acc[rt][t][i] = out[row rbase + 16 rt + l15][channel c0 + 16 t + 4 g4 + i]
@@ -341,7 +390,16 @@ static void go_kc(const GemmArgs& g, hipStream_t s) {
   typedef KcCfg<NT> C;
   const bool split = g.prec == PREC_SPLIT;
   void (*kern)(GemmArgs);
-  if (g.a_bf16)  // bf16 activations only exist in PREC_BF16
+  // PatchMerging 1 -> 2 (K = 8 x 48): A rows register-resident, opt-in WF_KC_AREG=1 -- one
+  // read of A, but 170 VGPRs (one 8-wave workgroup per CU instead of two) and it measured
+  // 207-210 us against 204 us for the statistics pass + streaming k loop (round 4)
+  static const bool no_areg = getenv("WF_KC_AREG") == nullptr || getenv("WF_KC_AREG")[0] == '0';
+  constexpr bool areg_ok = MAP == MAP_MERGE && EPI == EPI_STORE && NT <= 8;
+  if (areg_ok && !no_areg && g.K == 12 * KC_BK && g.a_ln == LN_COMPUTE && !g.a_bf16)
+    kern = split ? gemm_kc_kernel<NT, PREC_SPLIT, MAP, EPI, false, areg_ok ? 12 : 0>
+                 : (g.prec == PREC_FP16 ? gemm_kc_kernel<NT, PREC_FP16, MAP, EPI, false, areg_ok ? 12 : 0>
+                                        : gemm_kc_kernel<NT, PREC_BF16, MAP, EPI, false, areg_ok ? 12 : 0>);
+  else if (g.a_bf16)  // bf16 activations only exist in PREC_BF16
     kern = gemm_kc_kernel<NT, PREC_BF16, MAP, EPI, true>;
   else if (split)
     kern = gemm_kc_kernel<NT, PREC_SPLIT, MAP, EPI, false>;

@@ -20,7 +20,7 @@
 
 namespace wf {
 
-// NTH = 768 (LN + GELU epilogue with fp32 output, WF_GEMM_ROWS_12W=1): 12 waves per
+// NTH = 768 (LN + GELU epilogue with fp32 output; WF_GEMM_ROWS_12W=0 for the 8-wave one): 12 waves per
 // workgroup, three per SIMD -- the epilogue's LayerNorm / GELU VALU work needs three waves to
 // reach the SIMD's issue rate (tools/ubench_valu.hip); the output restaging then goes through
 // LDS 8 rows at a time so 12 waves' staging buffers fit next to the weight chunk
@@ -406,7 +406,8 @@ template <int NT, int MAP, int EPI>
 static void go_rows(const GemmArgs& g, dim3 grid, size_t lds, hipStream_t s) {
   void (*kern)(GemmArgs);
   if constexpr (EPI == EPI_LN_GELU && MAP == MAP_IDENTITY) {
-    static const bool w12 = getenv("WF_GEMM_ROWS_12W") != nullptr;
+    // default since round 4 (446 vs 452-453 us per stage-1 launch at B = 8); WF_GEMM_ROWS_12W=0
+    static const bool w12 = getenv("WF_GEMM_ROWS_12W") == nullptr || getenv("WF_GEMM_ROWS_12W")[0] != '0';
     if (w12 && !g.a_bf16 && g.prec != PREC_BF16) {
       kern = g.prec == PREC_SPLIT ? gemm_rows_kernel<NT, PREC_SPLIT, MAP, EPI, false, 768>
                                   : gemm_rows_kernel<NT, PREC_FP16, MAP, EPI, false, 768>;

@@ -114,6 +114,9 @@ class UnetrIDWTBlock(nn.Module):
         # the concatenation is converted again (round 2 built it NCDHW: two full-resolution
         # layout copies per decoder level)
         buf = ops.empty_cl(B, C + skip.shape[1], *size, inp.device)
-        ops.idwt3d_haar(inp, hf_coeffs, out=buf)   # channels [0, C)
-        ops.copy_cl(skip, buf[:, C:])               # torch.cat((out, skip), 1)
+        if skip.shape[1] == C:  # IDWT into [0, C) and torch.cat((out, skip), 1) in one pass
+            ops.idwt3d_haar(inp, hf_coeffs, out=buf, skip=skip)
+        else:
+            ops.idwt3d_haar(inp, hf_coeffs, out=buf)   # channels [0, C)
+            ops.copy_cl(skip, buf[:, C:])               # torch.cat((out, skip), 1)
         return self.conv_block(buf)

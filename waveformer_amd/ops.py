@@ -354,13 +354,16 @@ def bands_to_coeffs(bands: torch.Tensor) -> Tuple[torch.Tensor, Dict[str, torch.
 # a11: Haar synthesis
 # ------------------------------------------------------------------------------------------
 def idwt3d_haar(ll: torch.Tensor, details: Sequence[Dict[str, torch.Tensor]],
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None,
+                skip: Optional[torch.Tensor] = None) -> torch.Tensor:
     """ptwt.waverec3((ll,) + tuple(details), 'db1') for NCDHW-shaped tensors of any strides
     inside each (B, C, ...) batch with contiguous spatial (y, x) rows or channel-last layout.
 
     `details` is coarse -> fine.  If `out` is given (B, >=C, 2^L d, 2^L h, 2^L w) with a
     contiguous (C, D, H, W) block per batch, the result is written into its first C channels
-    (this is how the decoder fuses torch.cat((out, skip), 1), idwt_upsample.py:163)."""
+    (this is how the decoder fuses torch.cat((out, skip), 1), idwt_upsample.py:163).  With
+    `skip` (B, C, ...) as well, channels [C, 2C) of `out` receive it -- in the same kernel
+    (wf_idwt3d_haar_cl_cat) when everything is channel-last, else by a copy."""
     if ll.device.type != "cuda":
         raise RuntimeError("idwt3d_haar: GPU tensors only")
     if ll.dtype != torch.float32:
@@ -412,13 +415,25 @@ def idwt3d_haar(ll: torch.Tensor, details: Sequence[Dict[str, torch.Tensor]],
     sarr = (ctypes.c_int64 * len(strides))(*strides)
     if ll_ld is not None and ldo is None:
         ll, ll_ld = ll.contiguous(), None  # the NCDHW-output entry reads an NCDHW LL
-    if ldo is not None:
+    if skip is not None and (out is None or out.shape[1] < 2 * C or tuple(skip.shape) != (B, C, Do, Ho, Wo)):
+        raise ValueError("idwt3d_haar: skip must be (B, C, ...) of the output and out >= 2C channels")
+    skip_ld = cl_ld(skip) if skip is not None else None
+    fused = (skip is not None and ldo is not None and ll_ld is not None and skip_ld is not None
+             and C % 4 == 0 and skip.device == out.device and skip.dtype == torch.float32
+             and skip.stride(0) % 4 == 0 and skip.data_ptr() % 16 == 0)
+    if fused:
+        _lib.call("wf_idwt3d_haar_cl_cat", ll.data_ptr(), ll.stride(0), 1, ll_ld, arr, sarr, L,
+                  skip.data_ptr(), skip.stride(0), skip_ld, out.data_ptr(), out.stride(0), ldo,
+                  B, C, d, h, w, _stream())
+    elif ldo is not None:
         ll_cs, ll_ps = (1, ll_ld) if ll_ld is not None else (d * h * w, 1)
         _lib.call("wf_idwt3d_haar_cl", ll.data_ptr(), ll.stride(0), ll_cs, ll_ps, arr, sarr, L,
                   out.data_ptr(), out.stride(0), ldo, B, C, d, h, w, _stream())
     else:
         _lib.call("wf_idwt3d_haar", ll.data_ptr(), ll.stride(0), arr, sarr, L, out.data_ptr(),
                   out.stride(0), B, C, d, h, w, _stream())
+    if skip is not None and not fused:
+        copy_cl(skip, out[:, C:2 * C])
     del keep
     return out
 
