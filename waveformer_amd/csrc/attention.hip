@@ -225,8 +225,8 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const void* __restrict__
     }
   }
   // full column sums: the 4 lane groups hold disjoint key subsets
-  lrun += __shfl_xor(lrun, 16, 64);
-  lrun += __shfl_xor(lrun, 32, 64);
+  lrun = xsum16(lrun);
+  lrun = xsum32(lrun);
   // training: the row log-sum-exp (log2 domain) that the backward recomputes P from
   if (lse && qv && lane < 16) lse[(bw * heads + h) * N + q] = mrun + __log2f(lrun);
   if (qv) {
@@ -419,8 +419,8 @@ __global__ __launch_bounds__(256, 2) void attn_win_kernel(const void* __restrict
       }
     }
   }
-  lrun += __shfl_xor(lrun, 16, 64);
-  lrun += __shfl_xor(lrun, 32, 64);
+  lrun = xsum16(lrun);
+  lrun = xsum32(lrun);
   if (lse && qv && lane < 16) lse[(bw * heads + h) * N + q] = mrun + __log2f(lrun);
   if (qv) {
     const float inv = 1.f / lrun;
@@ -492,6 +492,9 @@ __device__ __forceinline__ int kswz(int row) {  // 16-B chunk XOR of a K row (se
 // pipe, is the tighter resource, so the default keeps the sums on the MFMA.
 #ifndef WF_ATTN_MFMA_SUM
 #define WF_ATTN_MFMA_SUM 1
+#endif
+#ifndef WF_ATTN_BPERMUTE  // 1: the round-3 __shfl_xor (ds_bpermute) max exchange, for A/B
+#define WF_ATTN_BPERMUTE 0
 #endif
 template <int P>
 __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict__ qkv,
@@ -587,8 +590,22 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) tmax = fmaxf(tmax, s[kt][i]);
+#if WF_ATTN_BPERMUTE
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+#else
+      // the 4 key groups of a query column (lanes l15 + 16 g4): xor 16 / xor 32 exchanges on
+      // v_permlane16_swap / v_permlane32_swap (VALU) instead of two ds_bpermute round trips
+      // on every tile's max -> exp chain
+      {
+        const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(tmax),
+                                                          __float_as_uint(tmax), false, false);
+        tmax = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+        const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax),
+                                                          __float_as_uint(tmax), false, false);
+        tmax = fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+      }
+#endif
       const float mnew = tmax;
       const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
       mrun = mnew;
@@ -647,8 +664,8 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
 #if WF_ATTN_MFMA_SUM
     const float inv = 1.f / l4[0];
 #else
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
+    lsum = xsum16(lsum);
+    lsum = xsum32(lsum);
     const float inv = 1.f / lsum;
 #endif
     const int64_t off = (row0 + q) * C + h * HD + 4 * g4;

@@ -212,7 +212,7 @@ __global__ __launch_bounds__(ff::NTH, 1) void ffn_fused_kernel(DwFcArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) s += (acc[j].x + acc[j].y) + (acc[j].z + acc[j].w);
     s += swz_xor16(s);
-    s += __shfl_xor(s, 32, 64);
+    s = xsum32(s);
     const float gm = s * (1.f / CG_CH);
     float q = 0.f;
 #pragma unroll
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(ff::NTH, 1) void ffn_fused_kernel(DwFcArgs a) {
       q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
     }
     q += swz_xor16(q);
-    q += __shfl_xor(q, 32, 64);
+    q = xsum32(q);
     const int lhp = 16 * ((ltid >> 6) & 3) + ll15;
     if (lg4 == 0 && lhp < PP) *reinterpret_cast<f32x2*>(pst + (lcg * 64 + lhp) * 2) = f32x2{gm, q};
   };

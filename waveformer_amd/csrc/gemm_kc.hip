@@ -117,10 +117,10 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
         s += d;
         q += d * d;
       }
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    q += __shfl_xor(q, 16, 64);
-    q += __shfl_xor(q, 32, 64);
+    s = xsum16(s);
+    s = xsum32(s);
+    q = xsum16(q);
+    q = xsum32(q);
     const float ms = s / (float)K;
     mean[0] = sh + ms;
     rstd[0] = rsqrtf(fmaxf(q / (float)K - ms * ms, 0.f) + g.a_eps);
@@ -144,10 +144,10 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
           q += d * d;
         }
       }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+      s = xsum16(s);
+      s = xsum32(s);
+      q = xsum16(q);
+      q = xsum32(q);
       const float ms = s / (float)K;
       mean[rt] = sh + ms;
       rstd[rt] = rsqrtf(fmaxf(q / (float)K - ms * ms, 0.f) + g.a_eps);
@@ -160,16 +160,16 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
       const float* ps = g.a_stats + (int64_t)arow[rt] * np * 2;
       float s = 0.f;
       for (int c = g4; c < np; c += 4) s += ps[2 * c];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
+      s = xsum16(s);
+      s = xsum32(s);
       const float mu = s / (float)np;
       float q = 0.f;
       for (int c = g4; c < np; c += 4) {
         const float d = ps[2 * c] - mu;
         q += ps[2 * c + 1] + ng * d * d;
       }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+      q = xsum16(q);
+      q = xsum32(q);
       mean[rt] = mu;
       rstd[rt] = rsqrtf(q / (float)K + g.a_eps);
     }
@@ -306,8 +306,8 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
       float s = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t) s += (acc[rt][t].x + acc[rt][t].y) + (acc[rt][t].z + acc[rt][t].w);
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
+      s = xsum16(s);
+      s = xsum32(s);
       rm_ = s / (float)N;
       float q = 0.f;
 #pragma unroll
@@ -315,8 +315,8 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
         const f32x4 d = acc[rt][t] - rm_;
         q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
       }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+      q = xsum16(q);
+      q = xsum32(q);
       rs_ = rsqrtf(q / (float)N + g.e_eps);
     } else if (EPI == EPI_RESID) {
       if (g.r_stats) {
@@ -331,8 +331,8 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
         float sm = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; ++t) sm += (acc[rt][t].x + acc[rt][t].y) + (acc[rt][t].z + acc[rt][t].w);
-        sm += __shfl_xor(sm, 16, 64);
-        sm += __shfl_xor(sm, 32, 64);
+        sm = xsum16(sm);
+        sm = xsum32(sm);
         const float mu = sm * (1.f / NC);
         float q = 0.f;
 #pragma unroll
@@ -340,8 +340,8 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
           const f32x4 d = acc[rt][t] - mu;
           q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
         }
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
+        q = xsum16(q);
+        q = xsum32(q);
         if (rv && g4 == 0)
           *reinterpret_cast<float2*>(g.o_pstats + ((int64_t)row * gridDim.y + blockIdx.y) * 2) =
               float2{mu, q};

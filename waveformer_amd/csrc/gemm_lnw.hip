@@ -142,8 +142,8 @@ __global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
     float s = 0.f;
 #pragma unroll
     for (int t = 0; t < LW_NTW; ++t) s += (acc[rt][t].x + acc[rt][t].y) + (acc[rt][t].z + acc[rt][t].w);
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    s = xsum16(s);
+    s = xsum32(s);
     if (g4 == 0) red[wid][rt * 16 + l15] = s;
   }
   __syncthreads();
@@ -161,8 +161,8 @@ __global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
       const f32x4 d = acc[rt][t] - mean[rt];
       q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
     }
-    q += __shfl_xor(q, 16, 64);
-    q += __shfl_xor(q, 32, 64);
+    q = xsum16(q);
+    q = xsum32(q);
     if (g4 == 0) red[wid][rt * 16 + l15] = q;
   }
   __syncthreads();

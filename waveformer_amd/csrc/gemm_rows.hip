@@ -138,8 +138,8 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += v[j];
       }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
+      s = xsum16(s);
+      s = xsum32(s);
       mean = s / (float)K;
       float q = 0.f;
       for (int ch = g4; ch < K / 8; ch += 4) {
@@ -151,16 +151,16 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
           q += d * d;
         }
       }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+      q = xsum16(q);
+      q = xsum32(q);
       rstd = rsqrtf(q / (float)K + g.a_eps);
     } else if (a_ln == LN_PARTIAL) {  // combine the producer's per-group {mean, M2}
       const int np = g.a_np;
       const float* ps = g.a_stats + (int64_t)arow_c * np * 2;
       float s = 0.f;
       for (int c = g4; c < np; c += 4) s += ps[2 * c];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
+      s = xsum16(s);
+      s = xsum32(s);
       mean = s / (float)np;
       const float ng = (float)(K / np);
       float q = 0.f;
@@ -168,8 +168,8 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
         const float d = ps[2 * c] - mean;
         q += ps[2 * c + 1] + ng * d * d;
       }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+      q = xsum16(q);
+      q = xsum32(q);
       rstd = rsqrtf(q / (float)K + g.a_eps);
     }
 
@@ -279,8 +279,8 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) s2 += lo2(acc[t]) + hi2(acc[t]);
       float s = s2.x + s2.y;
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
+      s = xsum16(s);
+      s = xsum32(s);
       rm_ = s / (float)N;
       f32x2 q2 = {0.f, 0.f};
 #pragma unroll
@@ -290,8 +290,8 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
         q2 = d1 * d1 + q2;
       }
       float q = q2.x + q2.y;
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+      q = xsum16(q);
+      q = xsum32(q);
       rs_ = rsqrtf(q / (float)N + g.e_eps);
     } else if (EPI == EPI_RESID) {
       if (g.r_stats) {

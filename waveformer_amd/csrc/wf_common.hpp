@@ -145,6 +145,19 @@ __device__ __forceinline__ float group_max(float v) {
   return v;
 }
 
+// v + v[lane ^ 16] and v + v[lane ^ 32] on the VALU lane-swap instructions (round 4): the
+// same bits as v + __shfl_xor(v, 16 / 32) (the two addends of a pair are the same values in
+// either order), without __shfl_xor's ds_bpermute round trip through the LDS unit on the
+// reductions' dependency chains
+__device__ __forceinline__ float xsum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), true, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), true, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace wf

@@ -53,9 +53,11 @@ def attn_workspace_bytes(B, C, D1, H1, W1):
 
 def ffn_workspace_bytes(B, C, hidden, D, H, W):
     """wf_ccf_ffn_workspace_bytes(..., WF_PREC_BF16X3): h1 and h2 fp32 + the dwconv's
-    (mean, M2) per 32 channels of every position."""
+    (mean, M2) per 32 channels of every position + the same-size area of the pwconv's LN1
+    partials + their per-row (mean, rstd) (ffn.hip, WF_FFN_LN1_FUSE)."""
     M = B * D * H * W
-    return 2 * _round256(M * hidden * 4) + _round256(M * (hidden // 32) * 2 * 4)
+    return (2 * _round256(M * hidden * 4) + 2 * _round256(M * (hidden // 32) * 2 * 4)
+            + _round256(M * 2 * 4))
 
 
 # ------------------------------------------------------------------------------------------
