@@ -1558,8 +1558,13 @@ static int go_dwfc_ws(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks
   static const bool ws = getenv("WF_FFN_DWFC_WS") != nullptr;
   // WF_FFN_DWFC_TB=1: three VALU waves per SIMD, one barrier per plane (ffn_dwfc_tb.hip;
   // round 4, under tuning)
-  static const bool tb = getenv("WF_FFN_DWFC_TB") != nullptr;
-  if (!ws && tb && prec != PREC_BF16) return launch_ffn_dwfc_tb(a, prec, s);
+  // default (round 4, fp32 h1): ffn_dwfc_tb4 -- three VALU waves per SIMD on 4 x 8 tiles,
+  // LDS-DMA staging (977-989 vs 1027-1043 us for ffn_dwfc_sb at B = 8, profiles/r4_ffn_tb/);
+  // WF_FFN_DWFC_SB=1 keeps the round-3 kernel, WF_FFN_DWFC_TB=1 the 3 x 8 single-barrier one
+  static const char* tbv = getenv("WF_FFN_DWFC_TB");
+  static const bool sbv = getenv("WF_FFN_DWFC_SB") != nullptr;
+  if (!ws && !sbv && prec != PREC_BF16)
+    return (tbv && tbv[0] == '1') ? launch_ffn_dwfc_tb(a, prec, s) : launch_ffn_dwfc_tb4(a, prec, s);
   void (*kern)(DwFcArgs) =
       ws ? (prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>
             : prec == PREC_FP16 ? ffn_dwfc_ws_kernel<PREC_FP16, float>

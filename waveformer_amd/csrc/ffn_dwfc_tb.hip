@@ -439,6 +439,375 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
   TB_PROBE_DUMP
 }
 
+// ---------------------------------------------------------------------------------------
+// 4 x 8 variant (WF_FFN_DWFC_TB=4): the same three VALU waves per SIMD on the tile of
+// ffn_dwfc_sb (no 3-row waste: 64 rows / 4), which leaves room for only two h2 tiles, so two
+// barriers per plane as in ffn_dwfc_sb:
+//   phase 1: D slots 0, 1: LN2 of h2 tile (p-2), 16 lanes x 12 channels per position, 4
+//            positions per wave (8 per SIMD); D slot 2: scatter rows [0, TB4_S2) of plane p
+//            E: LDS-DMA of plane p+1 into the buffer plane p-1 left; residual rows of p-2
+//   phase 2: D slots 0, 1: scatter rows [0, 6); slot 2: rows [TB4_S2, 6); all D: h2 tile p-1
+//            E: fc of tile (p-2) + epilogue + store; wait for the DMA
+// LDS: 2 x 46 KB planes + 2 x 25 KB h2 tiles + 18 KB fc lo fragments + vectors = 162,880 B.
+// ---------------------------------------------------------------------------------------
+#ifndef TB4_S2
+#define TB4_S2 4
+#endif
+namespace tb4 {
+constexpr int C = 48, HID = 192, TY = 4, TX = 8;
+constexpr int PY = TY + 2, PX = TX + 2, PP = PY * PX;  // 6 x 10
+constexpr int NPOS = TY * TX;                          // 32
+constexpr int HS = HID + 4;
+constexpr int PLANE_F = PP * HID;
+constexpr int H2F = NPOS * HS;
+constexpr int NV = HID / 4;
+constexpr int NPC = (PP * NV + 63) / 64;               // 45 LDS-DMA pieces
+constexpr int NPCE = (NPC + 3) / 4;
+constexpr int KS = HID / 32;
+constexpr int FWL_BYTES = (C / 16) * KS * 64 * 16;
+constexpr size_t LDS_BYTES = (size_t)(2 * PLANE_F + 2 * H2F + 2 * HID + 3 * C) * 4 + FWL_BYTES;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+}  // namespace tb4
+
+template <int P>
+__global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
+  using namespace tb4;
+  constexpr bool SPLIT = P == PREC_SPLIT;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* planes = lds;                     // [2][PP][HID]
+  float* h2b = lds + 2 * PLANE_F;          // [2][NPOS][HS]
+  float* lnw = h2b + 2 * H2F;              // [HID] (halved: GELU from x / 2)
+  float* lnb = lnw + HID;
+  float* fcb = lnb + HID;
+  float* n2w = fcb + C;
+  float* n2b = n2w + C;
+  bf16x8* fwlo = reinterpret_cast<bf16x8*>(n2b + C);
+  __shared__ int simd_cnt[4];
+
+  const int tid = threadIdx.x;
+  const int wid = tid >> 6, lane = tid & 63;
+  const int D = a.D, H = a.H, W = a.W;
+  const int ntx = (W + TX - 1) / TX, nty = (H + TY - 1) / TY, nzs = (D + a.ZS - 1) / a.ZS;
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int xt = t % ntx;
+  t /= ntx;
+  const int yt = t % nty;
+  t /= nty;
+  const int zt = t % nzs;
+  const int b = t / nzs;
+  const int x0 = xt * TX, y0 = yt * TY, z0 = zt * a.ZS, z1 = min(z0 + a.ZS, D);
+  const int64_t plane_sz = (int64_t)H * W;
+
+  if (tid < 4) simd_cnt[tid] = 0;
+  for (int i = tid; i < HID; i += 1024) {
+    lnw[i] = 0.5f * a.ln2_w[i];
+    lnb[i] = 0.5f * a.ln2_b[i];
+  }
+  for (int i = tid; i < C; i += 1024) {
+    fcb[i] = a.fc_b ? a.fc_b[i] : 0.f;
+    n2w[i] = a.stats ? a.n2_w[i] : 1.f;
+    n2b[i] = a.stats ? a.n2_b[i] : 0.f;
+  }
+  if (SPLIT) {
+    for (int i = tid; i < (C / 16) * KS * 64; i += 1024) {
+      const int l = i & 63, ks = (i >> 6) % KS, ct = (i >> 6) / KS;
+      fwlo[i] = *reinterpret_cast<const bf16x8*>(a.fc + (size_t)C * HID +
+                                                 (size_t)(ct * 16 + (l & 15)) * HID + ks * 32 + 8 * (l >> 4));
+    }
+  }
+  for (int i = tid; i < HID * 27; i += 1024) planes[i] = a.dw_w[i];
+  for (int i = tid; i < HID; i += 1024) planes[HID * 27 + i] = a.dw_b[i];
+  __syncthreads();
+  const int simd = tb_simd_id();
+  int slot = 0;
+  if (lane == 0) slot = atomicAdd(&simd_cnt[simd], 1);
+  slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0, 64));
+  __syncthreads();
+  const bool even = simd_cnt[0] == 4 && simd_cnt[1] == 4 && simd_cnt[2] == 4 && simd_cnt[3] == 4;
+  int role = even ? (slot < 3 ? 3 * simd + slot : 12 + simd) : wid;
+  role = __builtin_amdgcn_readfirstlane(role);
+
+  if (role < 12) {
+    // ================================ D waves ===========================================
+    const int cp = role / 3, kslot = role % 3, c = kslot * 64 + lane;
+    float w[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) w[k] = planes[c * 27 + k];
+    const float bias = planes[HID * 27 + c];
+    float acc[3][TY][2];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int o = 0; o < TY; ++o) acc[s][o][0] = acc[s][o][1] = 0.f;
+    // LN2 (slots 0, 1): positions 8 cp + 4 kslot + (lane >> 4), channels 12 (lane & 15) ..
+    const int lpos = 8 * cp + 4 * kslot + (lane >> 4), lg = lane & 15;
+    __syncthreads();  // (prologue) weights read out of the plane buffer
+    __syncthreads();  // (prologue) plane z0-1 staged
+
+    auto ln2_rows = [&](float* h2t) {
+      constexpr int LNC = HID / 16;
+      float* row = h2t + lpos * HS;
+      float v[LNC];
+#pragma unroll
+      for (int j = 0; j < LNC / 4; ++j) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(row + lg * LNC + 4 * j);
+        v[4 * j] = u.x;
+        v[4 * j + 1] = u.y;
+        v[4 * j + 2] = u.z;
+        v[4 * j + 3] = u.w;
+      }
+      float s4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s4[j] = (v[j] + v[j + 4]) + v[j + 8];
+      const float mean = group_sum<16>((s4[0] + s4[1]) + (s4[2] + s4[3])) * (1.f / HID);
+      float q4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d0 = v[j] - mean, d1 = v[j + 4] - mean, d2 = v[j + 8] - mean;
+        q4[j] = d2 * d2 + (d1 * d1 + d0 * d0);
+      }
+      const float rstd = __builtin_amdgcn_rsqf(
+          group_sum<16>((q4[0] + q4[1]) + (q4[2] + q4[3])) * (1.f / HID) + a.eps2);
+      const float nmr = -mean * rstd;
+      uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
+#pragma unroll
+      for (int j = 0; j < LNC / 4; ++j) {
+        const int cc = lg * LNC + 4 * j;
+        const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + cc);
+        const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + cc);
+        const f32x4 y = gelu_half4((f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]} *
+                                    rstd + nmr) * lw4 + lb4);
+        bf16x4 hi4, lo4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint16_t hb = op_cvt<P>(y[k]);
+          hi4[k] = (short)hb;
+          lo4[k] = op_lo<P>(y[k], hb);
+        }
+        *reinterpret_cast<bf16x4*>(rowh + cc) = hi4;
+        if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + cc) = lo4;
+      }
+    };
+    auto rows = [&](const float (&vin)[PY][4], auto SAc, auto SBc, auto SCc, auto LOc, auto HIc) {
+      constexpr int SA = decltype(SAc)::value, SB = decltype(SBc)::value,
+                    SC = decltype(SCc)::value, LO = decltype(LOc)::value, HI = decltype(HIc)::value;
+#pragma unroll
+      for (int r = LO; r < HI; ++r) {
+        const float* v = vin[r];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int o = r - ky;
+          if (o < 0 || o >= TY) continue;
+          const float* w0 = w + ky * 3;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (ky == 0)
+              acc[SC][o][j] = w0[2] * v[j + 2] + (w0[1] * v[j + 1] + w0[0] * v[j]);
+            else
+              acc[SC][o][j] = w0[2] * v[j + 2] + (w0[1] * v[j + 1] + (w0[0] * v[j] + acc[SC][o][j]));
+            acc[SB][o][j] = w0[11] * v[j + 2] + (w0[10] * v[j + 1] + (w0[9] * v[j] + acc[SB][o][j]));
+            acc[SA][o][j] = w0[20] * v[j + 2] + (w0[19] * v[j + 1] + (w0[18] * v[j] + acc[SA][o][j]));
+          }
+        }
+      }
+    };
+    typedef std::integral_constant<int, 0> I0;
+    typedef std::integral_constant<int, TB4_S2> IS;
+    typedef std::integral_constant<int, PY> IP;
+    auto step = [&](int p, auto Rc) {
+      constexpr int R = decltype(Rc)::value;
+      typedef std::integral_constant<int, R> SA;
+      typedef std::integral_constant<int, (R + 1) % 3> SB;
+      typedef std::integral_constant<int, (R + 2) % 3> SC;
+      const bool live = p <= z1 && !(a.dbg & 1);
+      const bool ln = p - 2 >= z0 && p - 2 < z1 && !(a.dbg & 2);
+      float vin[PY][4];
+      if (live) {
+        const float* q0 = planes + ((p - z0 + 1) & 1) * PLANE_F + 2 * cp * HID + c;
+#pragma unroll
+        for (int r = 0; r < PY; ++r)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) vin[r][k] = q0[(r * PX + k) * HID];
+      }
+      // ---- phase 1
+      if (kslot < 2) {
+        if (ln) ln2_rows(h2b + ((p - 2 - z0) & 1) * H2F);
+      } else if (live) {
+        rows(vin, SA(), SB(), SC(), I0(), IS());
+      }
+      __syncthreads();  // 1 -> 2: LN2'd tile (p-2) visible to the fc
+      // ---- phase 2
+      if (live) {
+        if (kslot < 2) rows(vin, SA(), SB(), SC(), I0(), IP());
+        else rows(vin, SA(), SB(), SC(), IS(), IP());
+        if (p - 1 >= z0) {
+          float* h2t = h2b + ((p - 1 - z0) & 1) * H2F;
+#pragma unroll
+          for (int o = 0; o < TY; ++o)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              h2t[(o * TX + 2 * cp + j) * HS + c] = acc[R][o][j] + bias;
+        }
+      }
+      __syncthreads();  // 2 -> next 1
+    };
+    for (int p = z0 - 1; p <= z1 + 1; p += 3) {
+      step(p, std::integral_constant<int, 0>());
+      if (p + 1 <= z1 + 1) step(p + 1, std::integral_constant<int, 1>());
+      if (p + 2 <= z1 + 1) step(p + 2, std::integral_constant<int, 2>());
+    }
+    return;
+  }
+
+  // ================================== E waves ============================================
+  __builtin_amdgcn_s_setprio(WF_TB_EPRIO);
+  const int e = role - 12;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const bool has_fc = e < C / 16;
+  const int ct = has_fc ? e : 0;
+  const float bs = a.bscale ? a.bscale[b] : 1.f;
+  bf16x8 fwh[KS];
+  {
+    const uint16_t* wr = a.fc + (size_t)(ct * 16 + l15) * HID + 8 * g4;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) fwh[ks] = *reinterpret_cast<const bf16x8*>(wr + ks * 32);
+  }
+  const bf16x8* fwl = fwlo + ct * KS * 64 + lane;
+  const float* src = reinterpret_cast<const float*>(a.h1) + (int64_t)b * D * H * W * HID;
+  const int64_t plane_elems = (int64_t)H * W * HID;
+  uint32_t off[NPCE];
+#pragma unroll
+  for (int k = 0; k < NPCE; ++k) {
+    const int i = min((4 * k + e) * 64 + lane, PP * NV - 1);
+    const int pos = i / NV, v = i - pos * NV;
+    const int yy = y0 - 1 + pos / PX, xx = x0 - 1 + pos % PX;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    off[k] = ok ? (uint32_t)(((yy * W + xx) * HID + 4 * v) * 4) : 0x80000000u;
+  }
+  auto stage = [&](int p, float* dst) {
+    const bool pz = p >= 0 && p < D;
+    const float* base = src + (int64_t)min(max(p, 0), D - 1) * plane_elems;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base), 0, pz ? (int)(plane_elems * 4) : 0, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < NPCE; ++k) {
+      const int j = 4 * k + e;
+      if (j * 64 < PP * NV && (j * 64 + lane < PP * NV))
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(dst + j * 256), 16, off[k], 0, 0, 0);
+    }
+  };
+  const int col = ct * 16 + 4 * g4;
+  const float* sbase = a.stats ? a.stats : a.x;
+  auto gpos_of = [&](int zo, int rt, bool clamp) {
+    const int lp = rt * 16 + l15;
+    int yo = y0 + lp / TX, xo = x0 + lp % TX;
+    if (clamp) {
+      yo = min(yo, H - 1);
+      xo = min(xo, W - 1);
+    }
+    return (int64_t)b * D * plane_sz + (int64_t)zo * plane_sz + (int64_t)yo * W + xo;
+  };
+  auto row_ok = [&](int rt) {
+    const int lp = rt * 16 + l15;
+    return y0 + lp / TX < H && x0 + lp % TX < W;
+  };
+  f32x4 xr[2];
+  f32x2 es[2];
+  auto load_resid = [&](int zo, int rt) {
+    const int64_t g = gpos_of(zo, rt, true);
+    xr[rt] = *reinterpret_cast<const f32x4*>(a.x + g * C + col);
+    es[rt] = *reinterpret_cast<const f32x2*>(sbase + 2 * g);
+  };
+  auto fc_store = [&](const float* h2t, int zo, int rt) {
+    const int lp = rt * 16 + l15;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)lp * (2 * HS);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = ks * 32 + 8 * g4;
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bh + k);
+      if (SPLIT) {
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
+        acc = mma32<P>(fwh[ks], bl, acc);
+        acc = mma32<P>(fwl[ks * 64], bh, acc);
+      }
+      acc = mma32<P>(fwh[ks], bh, acc);
+    }
+    f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+    const f32x4 xv = xr[rt];
+    if (a.stats) {
+      const f32x4 lw = *reinterpret_cast<const f32x4*>(n2w + col);
+      const f32x4 lb = *reinterpret_cast<const f32x4*>(n2b + col);
+      const float em = es[rt].x, er = es[rt].y;
+      const f32x4 n2 = (xv - em) * er * lw + lb;
+      v = xv + (n2 + v) * bs;
+    } else {
+      v = xv + v * bs;
+    }
+    if (row_ok(rt)) *reinterpret_cast<f32x4*>(a.out + gpos_of(zo, rt, false) * C + col) = v;
+  };
+
+  __syncthreads();  // (prologue) weights read out of the plane buffer
+  stage(z0 - 1, planes);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // (prologue) plane z0-1 staged
+  for (int p = z0 - 1; p <= z1 + 1; ++p) {
+    const int zo = p - 2;
+    const bool epi = has_fc && zo >= z0 && zo < z1;
+    // ---- phase 1: plane p+1 into the buffer plane p-1 left; residual rows of zo
+    if (p + 1 <= z1 && !(a.dbg & 8)) stage(p + 1, planes + ((p + 2 - z0) & 1) * PLANE_F);
+    if (epi) {
+      load_resid(zo, 0);
+      load_resid(zo, 1);
+    }
+    __syncthreads();  // 1 -> 2
+    // ---- phase 2: fc of tile zo + epilogue; the staged plane must land before the barrier
+    if (epi && !(a.dbg & 4)) {
+      const float* h2t = h2b + ((zo - z0) & 1) * H2F;
+      fc_store(h2t, zo, 0);
+      fc_store(h2t, zo, 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // 2 -> next 1
+  }
+}
+
+int launch_ffn_dwfc_tb4(const DwFcArgs& a, int prec, hipStream_t s) {
+  using namespace tb4;
+  DwFcArgs g = a;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int64_t base = (int64_t)g.B * cdiv(g.H, TY) * cdiv(g.W, TX);
+  int best_zs = g.D;
+  int64_t best = -1;
+  for (int nz = 1; nz <= 8 && nz <= g.D; ++nz) {
+    const int zs = (int)cdiv(g.D, nz);
+    const int64_t cost = cdiv(base * cdiv(g.D, zs), cus) * (zs + 3);
+    if (best < 0 || cost < best) {
+      best = cost;
+      best_zs = zs;
+    }
+  }
+  g.ZS = best_zs;
+  static const int dbg = getenv("WF_FFN_DBG") ? atoi(getenv("WF_FFN_DBG")) : 0;
+  g.dbg = dbg;
+  const int64_t blocks = base * cdiv(g.D, g.ZS);
+  if (prec != PREC_SPLIT && prec != PREC_FP16) return fail(WF_E_SHAPE, "ffn_dwfc_tb4: fp32 h1 only");
+  void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_dwfc_tb4_kernel<PREC_SPLIT>
+                                              : ffn_dwfc_tb4_kernel<PREC_FP16>;
+  set_max_lds(reinterpret_cast<const void*>(kern), (int)LDS_BYTES);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), LDS_BYTES, s, g);
+  return check_launch("ffn_dwfc_tb4");
+}
+
 int launch_ffn_dwfc_tb(const DwFcArgs& a, int prec, hipStream_t s) {
   using namespace tb;
   DwFcArgs g = a;

@@ -164,6 +164,8 @@ struct DwFcArgs {
 int launch_ffn_dwfc(const DwFcArgs& a, int prec, hipStream_t s);
 // stage-1 shape, three VALU waves per SIMD and one barrier per plane (ffn_dwfc_tb.hip)
 int launch_ffn_dwfc_tb(const DwFcArgs& a, int prec, hipStream_t s);
+// the same on 4 x 8 tiles with two barriers per plane (ffn_dwfc_tb.hip, WF_FFN_DWFC_TB=4)
+int launch_ffn_dwfc_tb4(const DwFcArgs& a, int prec, hipStream_t s);
 // h1 plane staging: fp32 (SPLIT / FP16 workspaces) or bf16 (BF16) rows widened to fp32
 template <typename T>
 struct H1Load;

@@ -407,6 +407,11 @@ def ccf_ffn(xh: Tensor, stats: Optional[Tensor], n2w: Optional[Tensor], n2b: Opt
     out = torch.empty_like(xh)
     wsb = _lib.query("wf_ccf_ffn_workspace_bytes", B, C, hid, D, H, W, SPLIT)
     work = torch.empty(wsb, dtype=torch.uint8, device=xh.device)
+    # the training path writes h1, h2 and the LN2 partials; the inference-only LN1 areas after
+    # them are zeroed so the returned workspace is a deterministic function of the inputs
+    M = B * D * H * W
+    used = 2 * _round256(M * hid * 4) + _round256(M * (hid // 32) * 2 * 4)
+    work[used:].zero_()
     _lib.call("wf_ccf_ffn_stage", _FFN_KEEP, xh.data_ptr(), _p(stats), _p(n2w), _p(n2b),
               pw.data_ptr(), _p(pwb), l1w.data_ptr(), l1b.data_ptr(), float(eps1),
               dww.data_ptr(), dwb.data_ptr(), l2w.data_ptr(), l2b.data_ptr(), float(eps2),
