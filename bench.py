@@ -47,7 +47,9 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_fused_kernel" if os.environ.get("WF_FFN_FUSED")
               else "ffn_dwfc_kernel" if os.environ.get("WF_FFN_DWFC_CLASSIC")
               else "ffn_dwfc_ws_kernel" if os.environ.get("WF_FFN_DWFC_WS")
-              else "ffn_dwfc_sb_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
+              else "ffn_dwfc_sb_kernel" if os.environ.get("WF_FFN_DWFC_SB")
+              else "ffn_dwfc_tb_kernel" if os.environ.get("WF_FFN_DWFC_TB", "4") == "1"
+              else "ffn_dwfc_tb4_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
               "window_attention": "attn_tbl_kernel",
               "msfuse": "msfuse", "proj_out": "proj_out"}
 

@@ -87,8 +87,12 @@ def test_ddp_two_ranks_match_single_process(tmp_path):
                     continue
                 e = r[mode] / r["norm"]
                 worst[mode] = max(worst.get(mode, 0.0), e)
-                if mode in BARS and not e <= BARS[mode]:
-                    bad.append((step, mode, k, e))
+                # a tensor whose own single-process run-to-run noise is already a large part
+                # of the bar (stage-4 biases summed over a handful of positions) is held to 4x
+                # that noise instead
+                bar = max(BARS[mode], 4 * r["noise"] / r["norm"]) if mode in BARS else None
+                if mode in BARS and not e <= bar:
+                    bad.append((step, mode, k, e, r["noise"] / r["norm"]))
     print("DDP vs single-process, worst rel-L2 per reference:", worst)
     assert not bad, bad[:8]
     # DDP adds nothing beyond the run-to-run noise of the single-process computation

@@ -453,6 +453,9 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb_kernel(DwFcArgs a) {
 #ifndef TB4_S2
 #define TB4_S2 4
 #endif
+#ifndef WF_TB4_EPIPE  // 0: the first version's E-wave memory pipeline, for A/B
+#define WF_TB4_EPIPE 1
+#endif
 namespace tb4 {
 constexpr int C = 48, HID = 192, TY = 4, TX = 8;
 constexpr int PY = TY + 2, PX = TX + 2, PP = PY * PX;  // 6 x 10
@@ -473,15 +476,18 @@ template <int P>
 __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
   using namespace tb4;
   constexpr bool SPLIT = P == PREC_SPLIT;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* planes = lds;                     // [2][PP][HID]
-  float* h2b = lds + 2 * PLANE_F;          // [2][NPOS][HS]
-  float* lnw = h2b + 2 * H2F;              // [HID] (halved: GELU from x / 2)
+  // separate static LDS objects (not one dynamic array carved by offsets): the compiler's
+  // wait insertion can then tell the planes the LDS-DMA writes from the h2 tiles and fc
+  // fragments the E waves read, instead of waiting for every DMA before any LDS read
+  __shared__ __attribute__((aligned(16))) float planes[2 * PLANE_F];  // [2][PP][HID]
+  __shared__ __attribute__((aligned(16))) float h2b[2 * H2F];         // [2][NPOS][HS]
+  __shared__ __attribute__((aligned(16))) float vecs[2 * HID + 3 * C];
+  __shared__ bf16x8 fwlo[FWL_BYTES / 16];
+  float* lnw = vecs;                       // [HID] (halved: GELU from x / 2)
   float* lnb = lnw + HID;
   float* fcb = lnb + HID;
   float* n2w = fcb + C;
   float* n2b = n2w + C;
-  bf16x8* fwlo = reinterpret_cast<bf16x8*>(n2b + C);
   __shared__ int simd_cnt[4];
 
   const int tid = threadIdx.x;
@@ -677,15 +683,20 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
   const bf16x8* fwl = fwlo + ct * KS * 64 + lane;
   const float* src = reinterpret_cast<const float*>(a.h1) + (int64_t)b * D * H * W * HID;
   const int64_t plane_elems = (int64_t)H * W * HID;
-  uint32_t off[NPCE];
-#pragma unroll
-  for (int k = 0; k < NPCE; ++k) {
+  // the DMA pieces' source offsets (k-th piece of this E wave); recomputed per plane on the
+  // EPIPE path -- the E waves have VALU to spare and the registers went to the residual sets
+  auto piece_off = [&](int k) {
     const int i = min((4 * k + e) * 64 + lane, PP * NV - 1);
     const int pos = i / NV, v = i - pos * NV;
     const int yy = y0 - 1 + pos / PX, xx = x0 - 1 + pos % PX;
     const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-    off[k] = ok ? (uint32_t)(((yy * W + xx) * HID + 4 * v) * 4) : 0x80000000u;
-  }
+    return ok ? (uint32_t)(((yy * W + xx) * HID + 4 * v) * 4) : 0x80000000u;
+  };
+#if !WF_TB4_EPIPE
+  uint32_t off[NPCE];
+#pragma unroll
+  for (int k = 0; k < NPCE; ++k) off[k] = piece_off(k);
+#endif
   auto stage = [&](int p, float* dst) {
     const bool pz = p >= 0 && p < D;
     const float* base = src + (int64_t)min(max(p, 0), D - 1) * plane_elems;
@@ -694,9 +705,14 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
 #pragma unroll
     for (int k = 0; k < NPCE; ++k) {
       const int j = 4 * k + e;
+#if WF_TB4_EPIPE
+      const uint32_t o = piece_off(k);
+#else
+      const uint32_t o = off[k];
+#endif
       if (j * 64 < PP * NV && (j * 64 + lane < PP * NV))
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(dst + j * 256), 16, off[k], 0, 0, 0);
+            rs, (__attribute__((address_space(3))) void*)(dst + j * 256), 16, o, 0, 0, 0);
     }
   };
   const int col = ct * 16 + 4 * g4;
@@ -714,6 +730,104 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
     const int lp = rt * 16 + l15;
     return y0 + lp / TX < H && x0 + lp % TX < W;
   };
+#if WF_TB4_EPIPE
+  // The E waves' memory pipeline (vmcnt retires in issue order and counts stores too):
+  //   * the residual rows of output plane zo + 1 are loaded in iteration p (ahead of the plane
+  //     DMA), into the register set of zo + 1's parity, and used by the fc one iteration later
+  //     -- the fc never waits for a load younger than the DMA, i.e. never for the DMA itself;
+  //   * the output rows go out as range-checked buffer stores (rows outside the volume get an
+  //     out-of-range offset and are dropped), exactly two per fc wave, so the end-of-phase wait
+  //     for the DMA is vmcnt(2): it no longer waits for the stores to reach memory.
+  // The first version (WF_TB4_EPIPE=0) loaded the residual in the same iteration, behind the
+  // DMA, so the fc waited for both, and drained vmcnt(0) over its stores: two memory round
+  // trips per plane on the E wave's path to the barrier.
+  // residual / statistics rows through 32-bit buffer offsets (64-bit pointer pairs for the two
+  // register sets spilled: the host keeps the tensors under 2 GiB)
+  f32x4 xr[2][2];
+  f32x2 es[2][2];
+  const int64_t npos = (int64_t)a.B * D * plane_sz;
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.x), 0, (int)(npos * C * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(sbase), 0, (int)(npos * 2 * 4), 0x00020000);
+  auto load_resid = [&](int zo, f32x4 (&xv)[2], f32x2 (&ev)[2]) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int g = (int)gpos_of(zo, rt, true);
+      xv[rt] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrsrc, (g * C + col) * 4, 0, 0));
+      ev[rt] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(srsrc, g * 8, 0, 0));
+    }
+  };
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      a.out, 0, (int)(npos * C * 4), 0x00020000);
+  auto fc_store = [&](const float* h2t, int zo, int rt, const f32x4& xv, const f32x2& ev) {
+    const int lp = rt * 16 + l15;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint16_t* Bh = reinterpret_cast<const uint16_t*>(h2t) + (size_t)lp * (2 * HS);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = ks * 32 + 8 * g4;
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Bh + k);
+      if (SPLIT) {
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Bh + HID + k);
+        acc = mma32<P>(fwh[ks], bl, acc);
+        acc = mma32<P>(fwl[ks * 64], bh, acc);
+      }
+      acc = mma32<P>(fwh[ks], bh, acc);
+    }
+    f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+    if (a.stats) {
+      const f32x4 lw = *reinterpret_cast<const f32x4*>(n2w + col);
+      const f32x4 lb = *reinterpret_cast<const f32x4*>(n2b + col);
+      const f32x4 n2 = (xv - ev.x) * ev.y * lw + lb;
+      v = xv + (n2 + v) * bs;
+    } else {
+      v = xv + v * bs;
+    }
+    const int voff = row_ok(rt) ? (int)((gpos_of(zo, rt, false) * C + col) * 4) : (int)0x80000000;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), orsrc, voff, 0, 0);
+  };
+
+  __syncthreads();  // (prologue) weights read out of the plane buffer
+  stage(z0 - 1, planes);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // (prologue) plane z0-1 staged
+  // iteration p: zo = p - 2; register set of output plane z: (z - z0) & 1, a compile-time S
+  // for the fc (zo) and S ^ 1 for the prefetch (zo + 1) with the loop unrolled by two
+  auto iter = [&](int p, auto Sc) {
+    constexpr int S = decltype(Sc)::value;
+    const int zo = p - 2;
+    const bool epi = has_fc && zo >= z0 && zo < z1;
+    // ---- phase 1: residual rows of zo + 1, then plane p + 1 into the buffer p - 1 left
+    if (has_fc && zo + 1 >= z0 && zo + 1 < z1) load_resid(zo + 1, xr[S ^ 1], es[S ^ 1]);
+    if (p + 1 <= z1 && !(a.dbg & 8)) stage(p + 1, planes + ((p + 2 - z0) & 1) * PLANE_F);
+    // 1 -> 2 as a bare s_barrier: __syncthreads()' workgroup release fence makes the compiler
+    // drain vmcnt(0) first -- the LDS-DMA writes LDS, so the fence waited for the plane just
+    // issued and put a full memory round trip in front of every plane's phase 2.  This wave
+    // wrote no LDS in phase 1; the DMA is waited for at the end of phase 2.
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 2: fc of tile zo + epilogue; the staged plane must land before the barrier,
+    // the two stores may still be in flight
+    if (epi && !(a.dbg & 4)) {
+      const float* h2t = h2b + ((zo - z0) & 1) * H2F;
+      fc_store(h2t, zo, 0, xr[S][0], es[S][0]);
+      fc_store(h2t, zo, 1, xr[S][1], es[S][1]);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // bare as well (its fence would drain the stores): the DMA has landed (waited above) and
+    // the LDS reads of the fc are complete before the barrier (lgkmcnt)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // 2 -> next 1
+  };
+  // (zo - z0) & 1 at p = z0 - 1 + i is (i + 1) & 1: even i -> S = 1
+  for (int p = z0 - 1; p <= z1 + 1; p += 2) {
+    iter(p, std::integral_constant<int, 1>());
+    if (p + 1 <= z1 + 1) iter(p + 1, std::integral_constant<int, 0>());
+  }
+}
+#else
   f32x4 xr[2];
   f32x2 es[2];
   auto load_resid = [&](int zo, int rt) {
@@ -774,6 +888,7 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
     __syncthreads();  // 2 -> next 1
   }
 }
+#endif
 
 int launch_ffn_dwfc_tb4(const DwFcArgs& a, int prec, hipStream_t s) {
   using namespace tb4;
@@ -801,10 +916,11 @@ int launch_ffn_dwfc_tb4(const DwFcArgs& a, int prec, hipStream_t s) {
   g.dbg = dbg;
   const int64_t blocks = base * cdiv(g.D, g.ZS);
   if (prec != PREC_SPLIT && prec != PREC_FP16) return fail(WF_E_SHAPE, "ffn_dwfc_tb4: fp32 h1 only");
+  if ((int64_t)g.B * g.D * g.H * g.W * C * 4 >= ((int64_t)1 << 31))
+    return fail(WF_E_SHAPE, "ffn_dwfc_tb4: output beyond the 2 GiB buffer-store range");
   void (*kern)(DwFcArgs) = prec == PREC_SPLIT ? ffn_dwfc_tb4_kernel<PREC_SPLIT>
                                               : ffn_dwfc_tb4_kernel<PREC_FP16>;
-  set_max_lds(reinterpret_cast<const void*>(kern), (int)LDS_BYTES);
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), LDS_BYTES, s, g);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, s, g);  // static LDS
   return check_launch("ffn_dwfc_tb4");
 }
 

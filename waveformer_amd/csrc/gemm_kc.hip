@@ -53,25 +53,26 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
   const int l15 = lane & 15, g4 = lane >> 4;
   const int rbase = blockIdx.x * C::ROWS + wid * (16 * RT);
 
-  // ---- weight staging: piece i -> (column i / 4, k-octet i % 4) of the step's slice
-  bf16x8 wst[NPL][C::WPT];
-  auto wfetch = [&](int ks) {
+  // ---- weight staging: piece i -> (column i / 4, k-octet i % 4) of the step's slice.  Two
+  // register sets: step ks + 2's slice is fetched while step ks runs, and step ks + 1's (fetched
+  // a whole step earlier) is written to the other LDS buffer behind its MFMAs -- the round-3
+  // loop fetched one step ahead and waited out a full L2 round trip in every step's commit
+  typedef bf16x8 WRegs[NPL][C::WPT];
+  WRegs wst[2];
+  auto wfetch = [&](int ks, WRegs& dst) {
 #pragma unroll
     for (int j = 0; j < C::WPT; ++j) {
       const int i = min(j * C::NTHR + tid, C::WITEMS - 1);
+      // no zero-select on the loaded slice (a select is a use: it would wait for the load
+      // where it is placed): pieces past K re-read the last octet, finite weights that only
+      // meet the zeroed A octets (kv below), i.e. exact zero products
       const int n = c0 + (i >> 2), k = ks * KC_BK + 8 * (i & 3);
-      const bool ok = n < N && k < K;
       const int64_t off = (int64_t)min(n, N - 1) * K + min(k, K - 8);
-      const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-      const bf16x8 h = *reinterpret_cast<const bf16x8*>(g.w + off);
-      wst[0][j] = ok ? h : z;
-      if (SPLIT) {
-        const bf16x8 l = *reinterpret_cast<const bf16x8*>(g.w + (int64_t)N * K + off);
-        wst[NPL - 1][j] = ok ? l : z;
-      }
+      dst[0][j] = *reinterpret_cast<const bf16x8*>(g.w + off);
+      if (SPLIT) dst[NPL - 1][j] = *reinterpret_cast<const bf16x8*>(g.w + (int64_t)N * K + off);
     }
   };
-  auto wcommit = [&](int buf) {
+  auto wcommit = [&](int buf, const WRegs& src) {
 #pragma unroll
     for (int j = 0; j < C::WPT; ++j) {
       const int i = j * C::NTHR + tid;
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
 #pragma unroll
         for (int pl = 0; pl < NPL; ++pl)
           *reinterpret_cast<bf16x8*>(Wl + ((size_t)(buf * NPL + pl) * NC + (i >> 2)) * KC_KP +
-                                     8 * (i & 3)) = wst[pl][j];
+                                     8 * (i & 3)) = src[pl][j];
       }
     }
   };
@@ -134,14 +135,22 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
       load8f<ABF16>(g.a_src, rm.offset(g, 0), v0);
       const float sh = v0[0];
       float s = 0.f, q = 0.f;
-      for (int ch = g4; ch < K / 8; ch += 4) {
-        float v[8];
-        load8f<ABF16>(g.a_src, rm.offset(g, ch * 8), v);
+      // four octets per batch, loads first: the round-3 loop waited out one load latency per
+      // octet (12 in a row at K = 384); same summation order, the clamped tail octets add 0
+      const int noct = K / 8;
+      for (int cb = g4; cb < noct; cb += 16) {
+        float v[4][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = v[j] - sh;
-          s += d;
-          q += d * d;
+        for (int u = 0; u < 4; ++u) load8f<ABF16>(g.a_src, rm.offset(g, min(cb + 4 * u, noct - 1) * 8), v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float mk = cb + 4 * u < noct ? 1.f : 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = (v[u][j] - sh) * mk;
+            s += d;
+            q += d * d;
+          }
         }
       }
       s = xsum16(s);
@@ -181,14 +190,15 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0, 0, 0, 0};
 
-  float an[RT][8];
-  auto afetch = [&](int ks) {
+  typedef float ARegs[RT][8];
+  ARegs an[2];
+  auto afetch = [&](int ks, ARegs& dst) {
     if constexpr (KR > 0) return;
     const int k = min(ks * KC_BK + 8 * g4, K - 8);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const RowMapper<MAP> rm(g, arow[rt]);
-      load8f<ABF16>(g.a_src, rm.offset(g, k), an[rt]);
+      load8f<ABF16>(g.a_src, rm.offset(g, k), dst[rt]);
     }
   };
 
@@ -202,12 +212,17 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
       lnb[i] = i < K ? g.a_ln_b[i] : 0.f;
     }
   }
-  wfetch(0);
-  wcommit(0);
-  afetch(0);
+  wfetch(0, wst[0]);
+  afetch(0, an[0]);
+  wfetch(min(1, nks - 1), wst[1]);
+  afetch(min(1, nks - 1), an[1]);
+  wcommit(0, wst[0]);
   __syncthreads();
-  int buf = 0;
-  auto kbody = [&](int ks, const float (&vin)[RT][8]) {
+  // step ks runs on LDS buffer / register set S = ks & 1 (a compile-time slot: the k loop is
+  // unrolled by two)
+  auto kbody = [&](int ks, auto slot, const ARegs& vin) {
+    constexpr int S = decltype(slot)::value;
+    const int buf = S;
     const int k = ks * KC_BK + 8 * g4;
     const bool kv = k < K;
     float v[RT][8];
@@ -215,8 +230,7 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[rt][j] = vin[rt][j];
-    wfetch(min(ks + 1, nks - 1));  // next step's weight slice (last step: unused re-read)
-    afetch(min(ks + 1, nks - 1));
+    wfetch(min(ks + 2, nks - 1), wst[S]);  // two steps ahead (tail steps: unused re-reads)
     bf16x8 ah[RT], al[RT];
     {
       float wv[8], bv[8];
@@ -248,6 +262,9 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
         }
       }
     }
+    // the A set of this slot is consumed (split) before its next load is issued, so the load
+    // can reuse its registers: no loop-carried copies (and load waits) at the barrier
+    afetch(min(ks + 2, nks - 1), an[S]);
     const uint16_t* Wb = Wl + (size_t)buf * NPL * NC * KC_KP;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -266,27 +283,32 @@ __global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
         acc[rt][t] = mma32<P>(bh, ah[rt], acc[rt][t]);
       if (t % 4 == 3) __builtin_amdgcn_sched_barrier(0);
     }
-    wcommit(buf ^ 1);
+    wcommit(buf ^ 1, wst[S ^ 1]);  // step ks + 1's slice, fetched during step ks - 1
     __syncthreads();
-    buf ^= 1;
   };
+  typedef std::integral_constant<int, 0> Slot0;
+  typedef std::integral_constant<int, 1> Slot1;
   if constexpr (KR > 0) {
 #pragma unroll
-    for (int ks = 0; ks < KR; ++ks) {
-      float vin[RT][8];
+    for (int ks = 0; ks < KR; ks += 2) {
+      ARegs vin;
 #pragma unroll
       for (int j = 0; j < 8; ++j) vin[0][j] = areg[ks][j];
-      kbody(ks, vin);
+      kbody(ks, Slot0{}, vin);
+      if (ks + 1 < KR) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vin[0][j] = areg[ks + 1][j];
+        kbody(ks + 1, Slot1{}, vin);
+      }
     }
   } else {
+    // both halves unconditional (a conditional second half makes the loop-carried register
+    // sets phis, and their copies wait for the prefetches at every barrier): an odd step
+    // count runs one extra step with A and the weight slice zeroed (k >= K), adding exact zeros
 #pragma unroll 1
-    for (int ks = 0; ks < nks; ++ks) {
-      float vin[RT][8];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) vin[rt][j] = an[rt][j];
-      kbody(ks, vin);
+    for (int ks = 0; ks < nks; ks += 2) {
+      kbody(ks, Slot0{}, an[0]);
+      kbody(ks + 1, Slot1{}, an[1]);
     }
   }
 
