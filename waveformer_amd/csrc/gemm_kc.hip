@@ -20,7 +20,7 @@
 namespace wf {
 
 constexpr int KC_BK = 32;       // k per step (one 16x16x32 MFMA)
-constexpr int KC_KP = KC_BK + 8;  // LDS row stride in bf16 (16 B pad: conflict-free b128 reads)
+constexpr int KC_KP = KC_BK + WF_LDS_KPAD;  // LDS row stride in bf16 (gemm_common.hpp)
 
 template <int NT>
 struct KcCfg {

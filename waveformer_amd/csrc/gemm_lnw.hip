@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
   constexpr bool SPLIT = P == PREC_SPLIT;
   constexpr int NPL = SPLIT ? 2 : 1;
   constexpr int K32 = KS * 32;
-  constexpr int AS = K32 + 8;                 // LDS row stride (bf16): conflict-free b128 reads
+  constexpr int AS = K32 + WF_LDS_KPAD;       // LDS row stride (bf16, gemm_common.hpp)
   constexpr int ROWS = LW_RT * 16;
   __shared__ __attribute__((aligned(16))) uint16_t As[NPL * ROWS * AS];
   __shared__ float red[4][ROWS];

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
   const int a_ln = EPI == EPI_LN_GELU ? (g.a_ln == LN_GIVEN ? LN_GIVEN : LN_NONE) : g.a_ln;
   const int a_gelu = EPI == EPI_LN_GELU ? 0 : g.a_gelu;
   const int K32 = (K + 31) & ~31;
-  const int KP = K32 + 8;
+  const int KP = K32 + WF_LDS_KPAD;
   constexpr int NCOL = NT * 16;
   const int c0 = blockIdx.y * NCOL;  // first column of this chunk
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -402,20 +402,23 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
   }
 }
 
+// the 12-wave LN + GELU variant (fp32 output, identity rows): default since round 4 (446 vs
+// 452-453 us per stage-1 launch at B = 8); WF_GEMM_ROWS_12W=0 for the 8-wave one
+static bool rows_w12(const GemmArgs& g) {
+  static const bool w12 = getenv("WF_GEMM_ROWS_12W") == nullptr || getenv("WF_GEMM_ROWS_12W")[0] != '0';
+  return w12 && g.epi == EPI_LN_GELU && g.a_map == MAP_IDENTITY && !g.a_bf16 && g.prec != PREC_BF16;
+}
+
 template <int NT, int MAP, int EPI>
 static void go_rows(const GemmArgs& g, dim3 grid, size_t lds, hipStream_t s) {
   void (*kern)(GemmArgs);
   if constexpr (EPI == EPI_LN_GELU && MAP == MAP_IDENTITY) {
-    // default since round 4 (446 vs 452-453 us per stage-1 launch at B = 8); WF_GEMM_ROWS_12W=0
-    static const bool w12 = getenv("WF_GEMM_ROWS_12W") == nullptr || getenv("WF_GEMM_ROWS_12W")[0] != '0';
-    if (w12 && !g.a_bf16 && g.prec != PREC_BF16) {
+    if (rows_w12(g)) {  // lds already holds the 12 x 8-row output staging (host below)
       kern = g.prec == PREC_SPLIT ? gemm_rows_kernel<NT, PREC_SPLIT, MAP, EPI, false, 768>
                                   : gemm_rows_kernel<NT, PREC_FP16, MAP, EPI, false, 768>;
-      // the 16-row staging of 8 waves (the host's lds) -> 8 rows of 12 waves
-      const size_t lds12 = lds - (size_t)8 * 16 * (NT * 16 + 4) * 4 + (size_t)12 * 8 * (NT * 16 + 4) * 4;
-      set_max_lds(reinterpret_cast<const void*>(kern), (int)lds12);
+      set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
       const unsigned gx = (unsigned)std::min<int64_t>(cdiv((g.M + 15) / 16, 12), 256);
-      hipLaunchKernelGGL(kern, dim3(gx, grid.y), dim3(768), lds12, s, g);
+      hipLaunchKernelGGL(kern, dim3(gx, grid.y), dim3(768), lds, s, g);
       return;
     }
   }
@@ -462,7 +465,7 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
     return 0;
   const bool split = g.prec == PREC_SPLIT;
   const int K32 = (g.K + 31) & ~31;
-  const size_t per_col = (size_t)(split ? 2 : 1) * (K32 + 8) * 2;
+  const size_t per_col = (size_t)(split ? 2 : 1) * (K32 + WF_LDS_KPAD) * 2;
   const int tiles = g.N / 16;
   static const int cand[] = {12, 9, 8, 6, 4, 3, 2, 1};
   // the transposed conv's N = 8 Cout is wide: one workgroup per CU holding half the columns
@@ -479,8 +482,8 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
   }
   if (nt == 0) return 0;
   size_t lds = (size_t)nt * 16 * per_col + (size_t)(2 * K32 + 3 * nt * 16) * 4;
-  if (g.epi == EPI_LN_GELU && g.prec != PREC_BF16 && !g.a_bf16)  // output staging
-    lds += (size_t)8 * 16 * (nt * 16 + 4) * 4;
+  if (g.epi == EPI_LN_GELU && g.prec != PREC_BF16 && !g.a_bf16)  // output staging per wave
+    lds += (size_t)(rows_w12(g) ? 12 * 8 : 8 * 16) * (nt * 16 + 4) * 4;
   if (lds > 160 * 1024) return 0;
   const int chunks = tiles / nt;
   if (single_chunk_only && chunks > 1) return 0;
