@@ -15,6 +15,8 @@
 // LayerNorm of A: LN_GIVEN (stats passed in), LN_COMPUTE (one shifted sum / sum-of-squares
 // pass over the row before the k loop) or LN_PARTIAL (per-group {mean, M2} of the producer
 // combined by Chan's formula).
+#include <algorithm>
+
 #include "gemm_common.hpp"
 
 namespace wf {
@@ -446,7 +448,8 @@ static void dispatch_kc(int nt, const GemmArgs& g, hipStream_t s) {
     case 6: go_kc<6, MAP, EPI>(g, s); break;
     case 4: go_kc<4, MAP, EPI>(g, s); break;
     case 3: go_kc<3, MAP, EPI>(g, s); break;
-    default: go_kc<2, MAP, EPI>(g, s); break;
+    case 2: go_kc<2, MAP, EPI>(g, s); break;
+    default: go_kc<1, MAP, EPI>(g, s); break;
   }
 }
 
@@ -457,7 +460,9 @@ int gemm_kc_pick_nt(const GemmArgs& g) {
                      (g.a_map == MAP_IDENTITY) || (g.a_map == MAP_MERGE && g.epi == EPI_STORE);
   if (!known) return 0;
   const int tiles = g.N / 16;
-  static const int cand[] = {24, 12, 8, 6, 4, 3, 2};
+  static const int cand[] = {24, 12, 8, 6, 4, 3, 2, 1};
+  // narrowest chunk the small-M search may go down to (WF_KC_MINNT, A/B; round 1-4: 3)
+  static const int minnt = getenv("WF_KC_MINNT") ? std::max(1, atoi(getenv("WF_KC_MINNT"))) : 3;
   // widest column chunk that divides N (fewest re-reads of A); then, for small M, narrower
   // chunks until the grid has ~2 workgroups per CU (the K loop is a serial chain per workgroup)
   auto blocks = [&](int c) { return cdiv(g.M, 128) * (tiles / c); };
@@ -469,7 +474,7 @@ int gemm_kc_pick_nt(const GemmArgs& g) {
   for (int c : cand) {
     if (tiles % c != 0 || c > ntmax) continue;
     if (g.epi == EPI_LN_GELU && c != tiles) continue;  // LayerNorm needs the full row
-    if (nt == 0 || (g.epi != EPI_LN_GELU && blocks(nt) < 512 && c >= 3)) nt = c;
+    if (nt == 0 || (g.epi != EPI_LN_GELU && blocks(nt) < 512 && c >= minnt)) nt = c;
     if (blocks(nt) >= 512) break;
   }
   return nt;

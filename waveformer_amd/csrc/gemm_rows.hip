@@ -131,24 +131,37 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
     const RowMapper<MAP> rmn(g, arow_n);
     float mean = gmean, rstd = grstd;
     if (a_ln == LN_COMPUTE) {  // lanes l15, l15+16, l15+32, l15+48 share the row
+      // two passes, each issuing its loads four octets at a time (a load per iteration waited
+      // out one latency per octet); same summation order, clamped tail octets add 0
+      const int noct = K / 8;
       float s = 0.f;
-      for (int ch = g4; ch < K / 8; ch += 4) {
-        float v[8];
-        load8f<ABF16>(g.a_src, rm.offset(g, ch * 8), v);
+      for (int cb = g4; cb < noct; cb += 16) {
+        float v[4][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += v[j];
+        for (int u = 0; u < 4; ++u) load8f<ABF16>(g.a_src, rm.offset(g, min(cb + 4 * u, noct - 1) * 8), v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float mk = cb + 4 * u < noct ? 1.f : 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s += v[u][j] * mk;
+        }
       }
       s = xsum16(s);
       s = xsum32(s);
       mean = s / (float)K;
       float q = 0.f;
-      for (int ch = g4; ch < K / 8; ch += 4) {
-        float v[8];
-        load8f<ABF16>(g.a_src, rm.offset(g, ch * 8), v);
+      for (int cb = g4; cb < noct; cb += 16) {
+        float v[4][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = v[j] - mean;
-          q += d * d;
+        for (int u = 0; u < 4; ++u) load8f<ABF16>(g.a_src, rm.offset(g, min(cb + 4 * u, noct - 1) * 8), v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float mk = cb + 4 * u < noct ? 1.f : 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = (v[u][j] - mean) * mk;
+            q += d * d;
+          }
         }
       }
       q = xsum16(q);
@@ -470,7 +483,12 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
   static const int cand[] = {12, 9, 8, 6, 4, 3, 2, 1};
   // the transposed conv's N = 8 Cout is wide: one workgroup per CU holding half the columns
   // reads A twice instead of six times at 64 KB
-  const size_t wbudget = g.epi == EPI_SUBVOXEL ? 136 * 1024 : 64 * 1024;
+  // WF_ROWS_WIDE=1 (A/B): PatchMerging's whole 8C -> 2C weight (150 KB at 1 -> 2) resident in
+  // one workgroup per CU, persistent over row tiles, no barrier in the k loop (gemm_kc streams
+  // the weight through LDS a k-step at a time)
+  static const bool wide = getenv("WF_ROWS_WIDE") && getenv("WF_ROWS_WIDE")[0] == '1';
+  const size_t wbudget = g.epi == EPI_SUBVOXEL ? 136 * 1024
+                         : (wide && g.a_map == MAP_MERGE) ? 152 * 1024 : 64 * 1024;
   int nt = 0;
   for (int c : cand) {
     if (tiles % c != 0) continue;
@@ -489,7 +507,8 @@ int try_launch_gemm_rows(const GemmArgs& g, hipStream_t s, bool single_chunk_onl
   if (single_chunk_only && chunks > 1) return 0;
   const int64_t ntiles = (g.M + 15) / 16;
   int64_t gx = cdiv(ntiles, 8);
-  const int64_t cap = (512 + chunks - 1) / chunks;  // ~2 workgroups of 8 waves per CU
+  // ~2 workgroups of 8 waves per CU; one per CU when the weight chunk fills the LDS
+  const int64_t cap = lds > 80 * 1024 ? 256 : (512 + chunks - 1) / chunks;
   if (gx > cap) gx = cap;
   if (gx < 1) gx = 1;
   dim3 grid((unsigned)gx, (unsigned)chunks);
