@@ -9,6 +9,7 @@ PosCNN, PatchEmbed) are kept as plain PyTorch modules so the reference import su
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -357,6 +358,31 @@ class WaveletTransform3D(nn.Module):
         return cur.permute(0, 4, 1, 2, 3), list(reversed(yh))
 
 
+# Inference: the attention passes of a multi-scale Block's wavelet levels are independent
+# until the fuse, so the coarser levels (their DWTs and attention chains, small grids that
+# leave most CUs idle) run on a side stream beside the finest level's attention -- forked from
+# and joined back into the current stream, so they are captured as parallel branches of the
+# bench's HIP graph.  Opt-in (WF_MS_STREAMS=1): at B = 8 the finest level's attention
+# (1536 workgroups, two per CU) leaves no CU slots for the side branch until its tail, and the
+# bench measured no gain beyond noise (1117.6 / 1113.4 vs 1118.5 / 1108.4 volumes/s).
+_MS_STREAMS = os.environ.get("WF_MS_STREAMS", "0") == "1"
+_SIDE = {}
+
+
+def _side_stream(dev: torch.device):
+    """The per-device side stream, created outside graph capture (None while capturing before
+    one exists: the caller then stays on one stream)."""
+    s = _SIDE.get(dev.index)
+    if s is None and not torch.cuda.is_current_stream_capturing():
+        s = _SIDE[dev.index] = torch.cuda.Stream(dev)
+    return s
+
+
+def _concurrent_levels(x: torch.Tensor) -> bool:
+    return (_MS_STREAMS and x.is_cuda and not torch.is_grad_enabled()
+            and not torch.compiler.is_compiling())
+
+
 class Block(nn.Module):
     """Transformer block with multi-scale DWT attention (wave_helper.py:357-569)."""
 
@@ -442,8 +468,26 @@ class Block(nn.Module):
         hfs = None
         if self.level > 0:
             self.dwt_downsamples._check()
-            bands = self._levels(x, ln1, self.attn_computation_level)
-            srcs = [self.attn.forward_raster(b[0]) for b in bands]
+            n = self.attn_computation_level
+            side = _side_stream(x.device) if n > 1 and _concurrent_levels(x) else None
+            if side is None:
+                bands = self._levels(x, ln1, n)
+                srcs = [self.attn.forward_raster(b[0]) for b in bands]
+            else:
+                # level 1 on this stream; levels 2..n (DWT chain + attention) on the side stream
+                main = torch.cuda.current_stream(x.device)
+                bands = self._levels(x, ln1, 1)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    cur, rest = bands[0][0], []
+                    for _ in range(n - 1):
+                        b = _OPS.dwt3d(cur, None, None, 0.0)
+                        rest.append(b)
+                        cur = b[0]
+                    rest_srcs = [self.attn.forward_raster(b[0]) for b in rest]
+                srcs = [self.attn.forward_raster(bands[0][0])] + rest_srcs
+                main.wait_stream(side)
+                bands = bands + rest
             hfs = [ops.bands_to_coeffs(b)[1] for b in bands]
         else:
             srcs = [self.attn.forward_raster(x, ln1)]

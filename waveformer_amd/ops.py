@@ -267,14 +267,29 @@ class weight_scope:
 
 
 def per_forward(key: tuple, make):
-    """make() once per weight_scope (once per call outside any scope)."""
+    """make() once per weight_scope (once per call outside any scope).  The value's producing
+    stream is remembered with an event: a Block runs its coarser wavelet levels on a side
+    stream (network_models/wave_helper.py), and a consumer on another stream must wait for the
+    kernel that made the cached operand (an fp16-policy forward splits the attention weights
+    on whichever stream first asks for them)."""
     sc = _cur_scope()
     if sc is None:
         return make()
-    v = sc.cache.get(key)
-    if v is None:
+    hit = sc.cache.get(key)
+    if hit is None:
         v = make()
-        sc.cache[key] = v
+        ev = st = None
+        if isinstance(v, torch.Tensor) and v.is_cuda:
+            st = torch.cuda.current_stream(v.device)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        sc.cache[key] = (v, ev, st)
+        return v
+    v, ev, st = hit
+    if ev is not None:
+        cur = torch.cuda.current_stream(v.device)
+        if cur != st:
+            cur.wait_event(ev)
     return v
 
 
