@@ -24,13 +24,13 @@ namespace wf {
 constexpr int KC_BK = 32;       // k per step (one 16x16x32 MFMA)
 constexpr int KC_KP = KC_BK + WF_LDS_KPAD;  // LDS row stride in bf16 (gemm_common.hpp)
 
-template <int NT>
+template <int NT, int WV = 8>
 struct KcCfg {
   // one 16-row tile per wave and 8 waves per workgroup (128 rows): the accumulators stay
   // at NT * 4 VGPRs, so NT <= 8 fits four waves per SIMD to hide the A stream and the
   // per-step barrier (4 waves x 2 tiles: 168-188 VGPRs, two waves per SIMD, ~2x slower)
   static constexpr int RT = 1;
-  static constexpr int WAVES = 8, NTHR = 64 * WAVES, ROWS = 16 * RT * WAVES;
+  static constexpr int WAVES = WV, NTHR = 64 * WAVES, ROWS = 16 * RT * WAVES;
   static constexpr int NC = NT * 16;
   static constexpr int WITEMS = NC * (KC_BK / 8);  // 16-byte pieces per plane per k step
   static constexpr int WPT = (WITEMS + NTHR - 1) / NTHR;  // per thread
@@ -41,9 +41,12 @@ struct KcCfg {
 // the k loop, the LayerNorm moments come from those registers and the (fully unrolled) k loop
 // reads them again -- the round-3 statistics pass and the k loop each streamed the rows, and
 // with 128-row workgroups the second read missed L2 (PMC 2.2x the input bytes)
-template <int NT, int P, int MAP, int EPI, bool ABF16, int KR = 0>
-__global__ __launch_bounds__(512) void gemm_kc_kernel(GemmArgs g) {
-  typedef KcCfg<NT> C;
+// WV = 16 (PatchMerging 1 -> 2, 2048 workgroups of 8 waves): 256-row workgroups, so the weight
+// chunk is staged through LDS once per 256 rows instead of per 128 -- at 128 rows the staged
+// weight bytes (147 KB per workgroup, 302 MB per launch) were 60 % of the A bytes
+template <int NT, int P, int MAP, int EPI, bool ABF16, int KR = 0, int WV = 8>
+__global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
+  typedef KcCfg<NT, WV> C;
   constexpr bool SPLIT = P == PREC_SPLIT;  // P: Prec (operand kind)
   constexpr int RT = C::RT, NC = C::NC, NPL = SPLIT ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) uint16_t Wl[];  // [2][NPL][NC][KC_KP]
@@ -419,7 +422,8 @@ static void go_kc(const GemmArgs& g, hipStream_t s) {
   // 207-210 us against 204 us for the statistics pass + streaming k loop (round 4)
   static const bool no_areg = getenv("WF_KC_AREG") == nullptr || getenv("WF_KC_AREG")[0] == '0';
   constexpr bool areg_ok = MAP == MAP_MERGE && EPI == EPI_STORE && NT <= 8;
-  if (areg_ok && !no_areg && g.K == 12 * KC_BK && g.a_ln == LN_COMPUTE && !g.a_bf16)
+  const bool areg = areg_ok && !no_areg && g.K == 12 * KC_BK && g.a_ln == LN_COMPUTE && !g.a_bf16;
+  if (areg)
     kern = split ? gemm_kc_kernel<NT, PREC_SPLIT, MAP, EPI, false, areg_ok ? 12 : 0>
                  : (g.prec == PREC_FP16 ? gemm_kc_kernel<NT, PREC_FP16, MAP, EPI, false, areg_ok ? 12 : 0>
                                         : gemm_kc_kernel<NT, PREC_BF16, MAP, EPI, false, areg_ok ? 12 : 0>);
@@ -431,12 +435,26 @@ static void go_kc(const GemmArgs& g, hipStream_t s) {
     kern = gemm_kc_kernel<NT, PREC_FP16, MAP, EPI, false>;
   else
     kern = gemm_kc_kernel<NT, PREC_BF16, MAP, EPI, false>;
+  // 16-wave workgroups for large grids: PatchMerging (default, WF_KC_WV16=2), every large
+  // gemm_kc grid (=1, A/B) or none (=0)
+  static const int wv16 = getenv("WF_KC_WV16") ? atoi(getenv("WF_KC_WV16")) : 2;
+  int rows = C::ROWS, nthr = C::NTHR;
+  if constexpr (NT <= 8 && EPI != EPI_LN_GELU) {
+    const bool want = wv16 == 1 || (wv16 == 2 && MAP == MAP_MERGE);
+    if (want && !areg && !g.a_bf16 && cdiv(g.M, C::ROWS) * (g.N / C::NC) >= 1024 &&
+        (split || g.prec == PREC_FP16)) {
+      kern = split ? gemm_kc_kernel<NT, PREC_SPLIT, MAP, EPI, false, 0, 16>
+                   : gemm_kc_kernel<NT, PREC_FP16, MAP, EPI, false, 0, 16>;
+      rows = KcCfg<NT, 16>::ROWS;
+      nthr = KcCfg<NT, 16>::NTHR;
+    }
+  }
   const size_t lds = (size_t)2 * (split ? 2 : 1) * C::NC * KC_KP * 2 +
                      (g.a_ln != LN_NONE ? (size_t)2 * cdiv(g.K, KC_BK) * KC_BK * 4 : 0);
   if (lds > 64 * 1024)
     set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
-  const dim3 grid((unsigned)cdiv(g.M, C::ROWS), (unsigned)(g.N / C::NC));
-  hipLaunchKernelGGL(kern, grid, dim3(C::NTHR), lds, s, g);
+  const dim3 grid((unsigned)cdiv(g.M, rows), (unsigned)(g.N / C::NC));
+  hipLaunchKernelGGL(kern, grid, dim3(nthr), lds, s, g);
 }
 
 template <int MAP, int EPI>
