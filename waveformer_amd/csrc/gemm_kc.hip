@@ -435,9 +435,10 @@ static void go_kc(const GemmArgs& g, hipStream_t s) {
     kern = gemm_kc_kernel<NT, PREC_FP16, MAP, EPI, false>;
   else
     kern = gemm_kc_kernel<NT, PREC_BF16, MAP, EPI, false>;
-  // 16-wave workgroups for large grids: PatchMerging (default, WF_KC_WV16=2), every large
-  // gemm_kc grid (=1, A/B) or none (=0)
-  static const int wv16 = getenv("WF_KC_WV16") ? atoi(getenv("WF_KC_WV16")) : 2;
+  // 16-wave workgroups for every grid of >= 1024 8-wave workgroups (default, WF_KC_WV16=1),
+  // PatchMerging only (=2) or none (=0): stage-1 merge 209.8 -> 201.9 us, stage-3 pwconv
+  // 64.2 -> 61.4, config 5 45.6-45.8 -> 46.0 volumes/s (profiles/r4_gemm/)
+  static const int wv16 = getenv("WF_KC_WV16") ? atoi(getenv("WF_KC_WV16")) : 1;
   int rows = C::ROWS, nthr = C::NTHR;
   if constexpr (NT <= 8 && EPI != EPI_LN_GELU) {
     const bool want = wv16 == 1 || (wv16 == 2 && MAP == MAP_MERGE);
