@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 13
+#define WF_ABI_VERSION 14
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
@@ -195,17 +195,25 @@ int wf_conv3d_k3_pack_f16(const float* w, uint16_t* packed, int64_t Cin, int64_t
                           void* stream);
 /* stats_acc: NULL, or a ZEROED (B, Cout, 2) fp64 buffer that receives each output channel's
  * sum and sum of squares per sample (InstanceNorm statistics fused into the epilogue; finish
- * with wf_instnorm_finalize).                                                                 */
+ * with wf_instnorm_finalize).
+ * workspace: wf_conv3d_k3_workspace_bytes(...) bytes (0 for most shapes; NULL allowed).  Small
+ * grids (the 8^3 / 16^3 decoder convs) split the input channels over several workgroups whose
+ * partial outputs land there and are summed in a fixed order (ABI 14: bitwise repeatable; was
+ * fp32 atomics).  With workspace NULL such grids run unsplit.                                 */
+int64_t wf_conv3d_k3_workspace_bytes(int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H,
+                                     int64_t W, int precision, int fp16_input);
 int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed, const float* bias,
-                     float* out, int64_t ldo, double* stats_acc, int64_t B, int64_t Cin,
-                     int64_t Cout, int64_t D, int64_t H, int64_t W, int precision, void* stream);
+                     float* out, int64_t ldo, double* stats_acc, void* workspace, int64_t B,
+                     int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W, int precision,
+                     void* stream);
 /* wf_conv3d_k3_fwd at WF_PREC_FP16 with the input already fp16 (channel-last, ldx halves per
  * position, 8-byte aligned; w packed by wf_conv3d_k3_pack_f16): the operands are those the fp32
  * path stages after rounding, so the output is bitwise the same for an input written by
  * wf_norm_act_h_cl.  Half the staging bytes, no conversion.                                 */
 int wf_conv3d_k3_fwd_xh(const uint16_t* x, int64_t ldx, const uint16_t* w_packed_f16,
-                        const float* bias, float* out, int64_t ldo, double* stats_acc, int64_t B,
-                        int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W, void* stream);
+                        const float* bias, float* out, int64_t ldo, double* stats_acc,
+                        void* workspace, int64_t B, int64_t Cin, int64_t Cout, int64_t D,
+                        int64_t H, int64_t W, void* stream);
 
 /* Weight gradient of wf_conv3d_k3_fwd (training, config 4):
  *   dw[co, ci, kz, ky, kx] (+)= sum_p dy[p, co] * x[p + (kz-1, ky-1, kx-1), ci]
@@ -490,17 +498,26 @@ int wf_window_attention_fwd_train(const float* x, const float* ln_w, const float
  * gradient of o (window-major), lse from wf_window_attention_fwd_train.
  * dqkv: (B*D1*H1*W1, 3C) in RASTER row order (the inverse of window_partition,
  * wave_helper.py:450-461), so the qkv weight gradient pairs it with the un-permuted input.
- * dbias: (heads, N, N), the bias gradient summed over all windows.  Both are zeroed here.
+ * dbias: (heads, N, N), the bias gradient summed over all windows.  Every element of both is
+ * written (no zeroing needed).  Deterministic (ABI 14): no atomics; the key-block partials of
+ * dQ and the window-group partials of dbias live in `workspace`
+ * (wf_window_attention_bwd_workspace_bytes) and are summed in index order.
  * head_dim in {16, 32, 48, 64}.                                                             */
+int64_t wf_window_attention_bwd_workspace_bytes(int64_t B, int64_t C, int64_t D1, int64_t H1,
+                                                int64_t W1, int64_t ws, int64_t heads);
 int wf_window_attention_bwd_core(const float* qkv, const float* o, const float* dout,
                                  const float* bias, const float* lse, float* dqkv, float* dbias,
-                                 int64_t B, int64_t C, int64_t D1, int64_t H1, int64_t W1,
-                                 int64_t ws, int64_t heads, float scale, void* stream);
+                                 void* workspace, int64_t B, int64_t C, int64_t D1, int64_t H1,
+                                 int64_t W1, int64_t ws, int64_t heads, float scale,
+                                 void* stream);
 
-/* dtable[index[i][j]][h] += dbias[h][i][j] (the gather at attention.py:94-97, adjoint);
- * dtable (table_rows, heads) is zeroed first.                                               */
-int wf_rel_pos_bias_bwd(const float* dbias, const int64_t* index, float* dtable, int64_t N,
-                        int64_t heads, int64_t table_rows, void* stream);
+/* dtable[r][h] = sum of dbias[h][i][j] over index[i][j] == r (the gather at
+ * attention.py:94-97, adjoint), in ascending flat order: `perm` (N*N) lists the flat positions
+ * i*N + j grouped by table row (a stable sort of the index), `offsets` (table_rows + 1) delimits
+ * the groups.  Deterministic (ABI 14); every element of dtable (table_rows, heads) is written. */
+int wf_rel_pos_bias_bwd(const float* dbias, const int64_t* perm, const int64_t* offsets,
+                        float* dtable, int64_t N, int64_t heads, int64_t table_rows,
+                        void* stream);
 
 /* out[c] = sum_r in[r][c] * (row_scale ? row_scale[r / rows_per_scale] : 1): bias gradients.
  * partials: wf_colsum_parts(R) * N floats.                                                  */

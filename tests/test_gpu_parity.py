@@ -153,6 +153,16 @@ def test_idwt_fused_concat(levels, C_, base):
     ops.idwt3d_haar(ll, dets, out=got, skip=skip)
     assert torch.equal(got, want)
     assert torch.equal(got[:, C_:], skip)
+    # under the scalar debug switch the fused entry does not apply; the op must
+    # fall back to IDWT + copy instead of raising
+    os.environ["WF_IDWT_SCALAR"] = "1"
+    try:
+        sc = torch.full((B, 2 * C_) + full, 5.0, device=DEV).contiguous(
+            memory_format=torch.channels_last_3d)
+        ops.idwt3d_haar(ll, dets, out=sc, skip=skip)
+    finally:
+        del os.environ["WF_IDWT_SCALAR"]
+    assert torch.equal(sc, want)
 
 
 def test_encoder_hf_feed_idwt_roundtrip():
@@ -266,6 +276,29 @@ def test_ccf_ffn_stage1_fused_vs_oracle(shape, block):
         assert C.rel_l2(out, ref) <= tol, prec
 
 
+def test_ccf_ffn_stage1_batch_beyond_tb4_range():
+    """the default stage-1 back half (ffn_dwfc_tb4) addresses its output through
+    32-bit buffer offsets (2 GiB).  At 64^3 x 48 that is B >= 43 (inference with a large
+    sw_batch_size): the launcher must take the unlimited SIMD-balanced kernel instead of failing.
+    Samples 0 and B-1 of a B = 44 call against the same samples run at B = 2 (tb4)."""
+    import waveformer_amd.network_models as NM
+    from oracle.weight_rule import rule_state_dict
+    from waveformer_amd import ops
+    S, B = 64, 44
+    mlp = NM.CCF_FFN(48, 192, img_size=(S,) * 3)
+    mlp.load_state_dict(rule_state_dict(mlp.state_dict()))
+    mlp = mlp.eval().to(DEV)
+    assert B * S ** 3 * 48 * 4 >= 2 ** 31
+    with torch.no_grad(), ops.precision("bf16x3"):
+        x = torch.randn((B, S, S, S, 48), device=DEV, generator=torch.Generator(DEV).manual_seed(5))
+        out = ops.ccf_ffn(x, None, None, mlp, None)
+        pair = torch.stack([x[0], x[-1]])
+        ref = ops.ccf_ffn(pair, None, None, mlp, None)
+    torch.cuda.synchronize()
+    assert C.rel_l2(out[0], ref[0]) <= 1e-6 and C.rel_l2(out[-1], ref[1]) <= 1e-6
+    del x, out
+
+
 @pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11), (3, 7, 4, 9), (1, 20, 8, 8),
                                    (1, 16, 16, 16)])
 @pytest.mark.parametrize("block", [False, True])
@@ -308,11 +341,12 @@ def test_ccf_ffn_stage2_vs_oracle(shape, block):
                                       (384, (1, 3, 5, 2))])
 @pytest.mark.parametrize("block", [False, True])
 def test_ccf_ffn_stage34_vs_oracle(C_, shape, block):
-    """C = 192 / 384, hidden = 4C (encoder stages 3 / 4): the pwconv on gemm_kc with LN1
-    partials in its epilogue, the per-row finalize, the depthwise conv applying LN1 + GELU
-    while it stages its planes (round 4: no separate LayerNorm + GELU pass over h1; ragged
-    tiles, z segments and volume edges whose zero padding must stay zero), then the fc with
-    LN2 + GELU in its loader and the Q4 residual -- same bars as stages 1 / 2."""
+    """C = 192 / 384, hidden = 4C (encoder stages 3 / 4), the default path: the pwconv on
+    gemm_kc, the LN1 + GELU pass (ln_act_fwd), the depthwise conv (ragged tiles, z segments and
+    volume edges whose zero padding must stay zero), then the fc with LN2 + GELU in its loader
+    and the Q4 residual -- same bars as stages 1 / 2.  The opt-in LN1-fused variant
+    (WF_FFN_LN1_FUSE=1, read once per process) is covered by
+    test_ccf_ffn_stage34_ln1_fuse_subprocess."""
     import waveformer_amd.network_models as NM
     from oracle.weight_rule import rule_state_dict
     from waveformer_amd import ops
@@ -339,6 +373,46 @@ def test_ccf_ffn_stage34_vs_oracle(C_, shape, block):
             stats = ops.msfuse([], xc, 1e-6)[1] if block else None
             out = ops.ccf_ffn(xc, stats, norm2 if block else None, mlp, cuda(bs))
         assert C.rel_l2(out, ref) <= tol, prec
+
+
+_LN1_FUSE_CHILD = r"""
+import sys, torch, torch.nn.functional as F
+sys.path.insert(0, '.')
+import waveformer_amd.network_models as NM
+from oracle import ref_waveformer as R
+from oracle.weight_rule import rule_state_dict, seeded_randn
+from tests import cases as C
+from waveformer_amd import ops
+worst = 0.0
+for C_, shape in ((192, (1, 5, 6, 11)), (384, (2, 4, 4, 4))):
+    mlp = NM.CCF_FFN(C_, 4 * C_, img_size=shape[1:])
+    sd = rule_state_dict(mlp.state_dict())
+    mlp.load_state_dict(sd)
+    mlp = mlp.eval().cuda()
+    x = seeded_randn(shape + (C_,), 39)
+    bs = torch.tensor([0.5, 2.0, 1.0][:shape[0]])
+    ref = x + (R.ccf_ffn(sd, "", x) - x) * bs.view(-1, 1, 1, 1, 1)
+    with torch.no_grad(), ops.precision("bf16x3"):
+        out = ops.ccf_ffn(x.cuda(), None, None, mlp, bs.cuda())
+    worst = max(worst, C.rel_l2(out, ref))
+print("LN1FUSE_WORST", worst)
+"""
+
+
+def test_ccf_ffn_stage34_ln1_fuse_subprocess():
+    """the opt-in LN1-fused stage-3/4 path (WF_FFN_LN1_FUSE=1: LN1 partials in the
+    pwconv epilogue, ln_stats_finalize, dwconv3d_kernel<float, true> applying LN1 + GELU while
+    it stages) is read once per process, so it runs in a child process with the switch set,
+    against the oracle at the bf16x3 bar."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WF_FFN_LN1_FUSE="1", PYTHONPATH=repo)
+    r = subprocess.run([sys.executable, "-c", _LN1_FUSE_CHILD], cwd=repo, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    worst = float(r.stdout.split("LN1FUSE_WORST")[1].split()[0])
+    assert worst <= 5e-5, worst
 
 
 @pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11)])

@@ -140,3 +140,25 @@ def test_index_formula_survives_device_moves():
     assert a._formula_valid()
     a.relative_position_index.fill_(0)
     assert not a._formula_valid()
+
+
+def test_index_formula_rechecked_when_written_before_a_move():
+    """an in-place write followed by a device move (or .float(), which keeps the int
+    buffer but adopts its bumped version) must not re-enable the in-kernel formula; a move of
+    an unwritten buffer, or a write that restores the formula, keeps / regains it."""
+    a = NM.Attention(48, num_heads=3, qkv_bias=True, window_size=4)
+    a.relative_position_index.fill_(0)
+    a._apply(lambda t: t.clone())  # Module.to(device)
+    assert not a._formula_valid()
+    b = NM.Attention(48, num_heads=3, qkv_bias=True, window_size=4)
+    b.relative_position_index.fill_(0)
+    b.float()  # the int buffer is returned unchanged
+    assert not b._formula_valid()
+    c = NM.Attention(48, num_heads=3, qkv_bias=True, window_size=4)
+    good = c.relative_position_index.clone()
+    c.relative_position_index.fill_(0)
+    c.relative_position_index.copy_(good)
+    c._apply(lambda t: t.clone())
+    assert c._formula_valid()
+    c._apply(lambda t: t.clone())
+    assert c._formula_valid()

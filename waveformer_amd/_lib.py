@@ -42,7 +42,9 @@ SIGNATURES = {
     "wf_subvoxel_scatter_cl": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_convtranspose2_cl": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
     "wf_moments_cl": (_I, [_P, _I64, _I64, _I64, _I64, _P, _P]),
-    "wf_conv3d_k3_fwd_xh": (_I, [_P, _I64, _P, _P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_conv3d_k3_fwd_xh": (_I, [_P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _I64,
+                                 _I64, _P]),
+    "wf_conv3d_k3_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I64, _I, _I]),
     "wf_norm_act_h_cl": (_I, [_P, _I64, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "wf_upsample_trilinear_add_cl": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
     "wf_conv1x1_head_cl": (_I, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
@@ -54,8 +56,8 @@ SIGNATURES = {
     "wf_conv3d_k3_packed_elems": (_I64, [_I64, _I64]),
     "wf_conv3d_k3_pack": (_I, [_P, _P, _I64, _I64, _P]),
     "wf_conv3d_k3_pack_f16": (_I, [_P, _P, _I64, _I64, _P]),
-    "wf_conv3d_k3_fwd": (_I, [_P, _I64, _P, _P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I64,
-                              _I64, _I, _P]),
+    "wf_conv3d_k3_fwd": (_I, [_P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64,
+                              _I64, _I64, _I, _P]),
     "wf_instnorm_finalize": (_I, [_P, _P, _I64, _I64, _I64, _F, _P]),
     "wf_instnorm_workspace_bytes": (_I64, [_I64, _I64]),
     "wf_instnorm_stats_cl": (_I, [_P, _I64, _I64, _I64, _I64, _F, _P, _P, _P]),
@@ -98,9 +100,11 @@ SIGNATURES = {
     "wf_window_attention_fwd_train": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _P,
                                            _I64, _I64, _I64, _I64, _I64, _I64, _I64, _F, _I,
                                            _P]),
-    "wf_window_attention_bwd_core": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64,
-                                          _I64, _I64, _I64, _F, _P]),
-    "wf_rel_pos_bias_bwd": (_I, [_P, _P, _P, _I64, _I64, _I64, _P]),
+    "wf_window_attention_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I64, _I64,
+                                                       _I64]),
+    "wf_window_attention_bwd_core": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64,
+                                          _I64, _I64, _I64, _I64, _F, _P]),
+    "wf_rel_pos_bias_bwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P]),
     "wf_colsum_parts": (_I64, [_I64]),
     "wf_colsum": (_I, [_P, _I64, _I64, _P, _I64, _P, _P, _P]),
     "wf_ln_act_fwd": (_I, [_P, _P, _P, _F, _I, _P, _I64, _I64, _P]),
@@ -120,7 +124,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 _lock = threading.Lock()
 _lib = None
 _err = None

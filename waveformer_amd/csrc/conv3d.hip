@@ -43,8 +43,11 @@ struct Conv3Args {
   int B, D, H, W, Cin, Cout, nch;
   int tiles_x, tiles_y;
   int64_t nblocks;
+  int64_t nblocks_pos;  // B*D*H*W: positions per split-K partial
   int ksplit;         // > 1: blockIdx.z takes chunks [z*nch/ksplit, (z+1)*nch/ksplit) and the
-                      // epilogue atomically adds into a zeroed output (small grids only)
+                      // epilogue writes its partial to part[z] (small grids only); a second
+                      // pass sums the partials in z order (deterministic, no atomics)
+  float* part;        // (ksplit, B*D*H*W, Cout) split-K partials (ksplit > 1)
   double* stats;      // (B, Cout, 2) fp64 {sum, sum of squares} accumulator or nullptr: the
                       // InstanceNorm statistics of the output, fused into the epilogue
   int zfirst;         // tile order: z fastest (1) or x fastest (0)
@@ -329,8 +332,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
         f32x4 v = acc[r][m][n];
         if (a.bias && blockIdx.z == 0) v += *reinterpret_cast<const f32x4*>(a.bias + co);
         if (a.ksplit > 1) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) atomicAdd(o + co + j, v[j]);
+          const int64_t p = ((int64_t)(b * a.D + z) * a.H + gy) * a.W + gx;
+          *reinterpret_cast<f32x4*>(a.part + ((int64_t)blockIdx.z * a.nblocks_pos + p) * a.Cout +
+                                    co) = v;
         } else {
           *reinterpret_cast<f32x4*>(o + co) = v;
         }
@@ -339,14 +343,25 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   }
 }
 
-// zero channels [0, C) of P channel-last positions (the split-K output)
-__global__ void zero_cl_kernel(float* __restrict__ out, int64_t ldo, int C, int64_t total) {
+// out[p][c] = sum_z part[z][p][c], z ascending (the split-K partials, bias in part[0])
+__global__ void splitk_sum_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                  int64_t ldo, int C, int64_t P, int ksplit) {
   const int C4 = C >> 2;
+  const int64_t total = P * C4;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = i / C4;
-    *reinterpret_cast<f32x4*>(out + p * ldo + 4 * (i - p * C4)) = f32x4{0, 0, 0, 0};
+    const int c = 4 * (int)(i - p * C4);
+    f32x4 v = *reinterpret_cast<const f32x4*>(part + p * C + c);
+    for (int z = 1; z < ksplit; ++z)
+      v += *reinterpret_cast<const f32x4*>(part + ((int64_t)z * P + p) * C + c);
+    *reinterpret_cast<f32x4*>(out + p * ldo + c) = v;
   }
+}
+
+// the split-K factor launch_conv3 picks for a grid of wgs workgroups (0 workspace: no split)
+inline int conv3_ksplit(int64_t wgs, int nch) {
+  return (wgs < 512 && nch > 1) ? (int)std::min<int64_t>(nch, cdiv(1024, wgs)) : 1;
 }
 
 template <int CO_T, int NT, int RW = 1>
@@ -363,15 +378,11 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   const size_t lds = (npl * 3 * (4 * RW + 2) * (TX + 2) * kConvCC +
                       (size_t)kConvKS * npl * CO_T * 512) * sizeof(uint16_t);
   // small grids (the 8^3 / 16^3 decoder convs): split the Cin chunks over blockIdx.z so the
-  // launch covers the 256 CUs; partial sums meet in the zeroed output through fp32 atomics
+  // launch covers the 256 CUs; the partials go to the caller's workspace and are summed in a
+  // fixed order by splitk_sum (bitwise repeatable; no split without a workspace)
   const int64_t wgs = a.nblocks * (a.Cout / (16 * CO_T));
-  a.ksplit = 1;
-  if (wgs < 512 && a.nch > 1) {
-    a.ksplit = (int)std::min<int64_t>(a.nch, cdiv(1024, wgs));
-    const int64_t total = (int64_t)a.B * a.D * a.H * a.W * (a.Cout / 4);
-    hipLaunchKernelGGL(zero_cl_kernel, dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 4096)),
-                       dim3(256), 0, stream, a.out, a.ldo, a.Cout, total);
-  }
+  a.nblocks_pos = (int64_t)a.B * a.D * a.H * a.W;
+  a.ksplit = a.part ? conv3_ksplit(wgs, a.nch) : 1;
   dim3 grid((unsigned)a.nblocks, (unsigned)(a.Cout / (16 * CO_T)), (unsigned)a.ksplit);
   const bool post_stats = a.stats && a.ksplit > 1;  // partial outputs: a separate pass below
   static const int zf = getenv("WF_CONV_ZFIRST") ? atoi(getenv("WF_CONV_ZFIRST")) : 1;
@@ -385,7 +396,16 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
   }
   int rc = check_launch("wf_conv3d_k3_fwd");
-  if (rc || !post_stats) return rc;
+  if (rc) return rc;
+  if (a.ksplit > 1) {
+    const int64_t total = a.nblocks_pos * (a.Cout / 4);
+    hipLaunchKernelGGL(splitk_sum_kernel,
+                       dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 8192)), dim3(256), 0,
+                       stream, a.part, a.out, a.ldo, a.Cout, a.nblocks_pos, a.ksplit);
+    rc = check_launch("wf_conv3d_k3_fwd (split-K sum)");
+    if (rc) return rc;
+  }
+  if (!post_stats) return 0;
   return launch_instnorm_partial(a.out, a.ldo, a.B, a.Cout, (int64_t)a.D * a.H * a.W, a.stats,
                                  stream);
 }
@@ -448,10 +468,39 @@ extern "C" int wf_conv3d_k3_pack_f16(const float* w, uint16_t* packed, int64_t C
   return conv_pack(w, packed, Cin, Cout, 1, stream);
 }
 
+namespace {
+// the tile shape conv3_fwd dispatches to: CO_T output-channel tiles, NT x tiles, RW rows
+struct Conv3Plan {
+  int co_t, nt, rw;
+};
+Conv3Plan conv3_plan(int64_t Cout, int64_t W, int precision, bool xh) {
+  const bool co3 = Cout % 48 == 0;
+  // two output rows per wave (8-row tiles: halo 10/8 rows instead of 6/4), non-split modes,
+  // W > 32.  Default for fp16 input only: with fp32 input the larger halo's prefetch registers
+  // spill (96->48 at 128^3 fp16: 1.82 vs 1.73 ms); the fp16-input variant fits (240 VGPRs) and
+  // runs 48->48 at 192^3 in 2.42 vs 2.52 ms (profiles/r3_conv/rw2_xh_ab_192.txt).
+  // WF_CONV_RW=1 / 2 forces one or the other
+  static const int rw = getenv("WF_CONV_RW") ? atoi(getenv("WF_CONV_RW")) : 0;
+  if (W > 32 && precision != PREC_SPLIT && co3 && (rw == 2 || (rw == 0 && xh))) return {3, 4, 2};
+  const int nt = W > 32 ? 4 : (W > 16 ? 2 : 1);
+  return {co3 ? 3 : 1, nt, 1};
+}
+}  // namespace
+
+extern "C" int64_t wf_conv3d_k3_workspace_bytes(int64_t B, int64_t Cin, int64_t Cout, int64_t D,
+                                                int64_t H, int64_t W, int precision,
+                                                int fp16_input) {
+  if (B < 1 || D < 1 || H < 1 || W < 1 || Cin < 4 || Cout < 16 || Cout % 16) return -1;
+  const Conv3Plan pl = conv3_plan(Cout, W, fp16_input ? PREC_FP16 : precision, fp16_input != 0);
+  const int64_t nblocks = B * D * cdiv(H, 4 * pl.rw) * cdiv(W, 16 * pl.nt);
+  const int ks = conv3_ksplit(nblocks * (Cout / (16 * pl.co_t)), (int)cdiv(Cin, kConvCC));
+  return ks > 1 ? (int64_t)ks * B * D * H * W * Cout * 4 : 0;
+}
+
 static int conv3_fwd(const float* x, const uint16_t* xh, int64_t ldx, const uint16_t* w_packed,
-                     const float* bias, float* out, int64_t ldo, double* stats_acc, int64_t B,
-                     int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W, int precision,
-                     void* stream) {
+                     const float* bias, float* out, int64_t ldo, double* stats_acc, void* work,
+                     int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W,
+                     int precision, void* stream) {
   WF_REQUIRE(B >= 1 && D >= 1 && H >= 1 && W >= 1, "empty tensor");
   WF_REQUIRE(Cin >= 4 && Cin % 4 == 0 && ldx >= Cin && ldx % 4 == 0,
              "Cin must be a positive multiple of 4 with ldx >= Cin, ldx % 4 == 0");
@@ -476,36 +525,30 @@ static int conv3_fwd(const float* x, const uint16_t* xh, int64_t ldx, const uint
   a.Cout = (int)Cout;
   a.nch = (int)cdiv(Cin, kConvCC);
   a.stats = stats_acc;
+  a.part = static_cast<float*>(work);
   hipStream_t s = (hipStream_t)stream;
-  const bool co3 = Cout % 48 == 0;
-  // two output rows per wave (8-row tiles: halo 10/8 rows instead of 6/4), non-split modes,
-  // W > 32.  Default for fp16 input only: with fp32 input the larger halo's prefetch registers
-  // spill (96->48 at 128^3 fp16: 1.82 vs 1.73 ms); the fp16-input variant fits (240 VGPRs) and
-  // runs 48->48 at 192^3 in 2.42 vs 2.52 ms (profiles/r3_conv/rw2_xh_ab_192.txt).
-  // WF_CONV_RW=1 / 2 forces one or the other
-  static const int rw = getenv("WF_CONV_RW") ? atoi(getenv("WF_CONV_RW")) : 0;
-  if (W > 32 && precision != PREC_SPLIT && co3 && (rw == 2 || (rw == 0 && xh)))
-    return launch_conv3<3, 4, 2>(a, precision, s);
-  if (W > 32) return co3 ? launch_conv3<3, 4>(a, precision, s) : launch_conv3<1, 4>(a, precision, s);
-  if (W > 16) return co3 ? launch_conv3<3, 2>(a, precision, s) : launch_conv3<1, 2>(a, precision, s);
-  return co3 ? launch_conv3<3, 1>(a, precision, s) : launch_conv3<1, 1>(a, precision, s);
+  const Conv3Plan pl = conv3_plan(Cout, W, precision, xh != nullptr);
+  if (pl.rw == 2) return launch_conv3<3, 4, 2>(a, precision, s);
+  if (pl.nt == 4) return pl.co_t == 3 ? launch_conv3<3, 4>(a, precision, s) : launch_conv3<1, 4>(a, precision, s);
+  if (pl.nt == 2) return pl.co_t == 3 ? launch_conv3<3, 2>(a, precision, s) : launch_conv3<1, 2>(a, precision, s);
+  return pl.co_t == 3 ? launch_conv3<3, 1>(a, precision, s) : launch_conv3<1, 1>(a, precision, s);
 }
 
 extern "C" int wf_conv3d_k3_fwd(const float* x, int64_t ldx, const uint16_t* w_packed,
                                 const float* bias, float* out, int64_t ldo, double* stats_acc,
-                                int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H,
-                                int64_t W, int precision, void* stream) {
+                                void* workspace, int64_t B, int64_t Cin, int64_t Cout, int64_t D,
+                                int64_t H, int64_t W, int precision, void* stream) {
   WF_REQUIRE_PTR(x);
-  return conv3_fwd(x, nullptr, ldx, w_packed, bias, out, ldo, stats_acc, B, Cin, Cout, D, H, W,
-                   precision, stream);
+  return conv3_fwd(x, nullptr, ldx, w_packed, bias, out, ldo, stats_acc, workspace, B, Cin, Cout,
+                   D, H, W, precision, stream);
 }
 
 extern "C" int wf_conv3d_k3_fwd_xh(const uint16_t* x, int64_t ldx, const uint16_t* w_packed_f16,
                                    const float* bias, float* out, int64_t ldo, double* stats_acc,
-                                   int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H,
-                                   int64_t W, void* stream) {
+                                   void* workspace, int64_t B, int64_t Cin, int64_t Cout,
+                                   int64_t D, int64_t H, int64_t W, void* stream) {
   WF_REQUIRE_PTR(x);
   WF_REQUIRE(((uintptr_t)x & 7) == 0, "x must be 8-byte aligned");
-  return conv3_fwd(nullptr, x, ldx, w_packed_f16, bias, out, ldo, stats_acc, B, Cin, Cout, D, H,
-                   W, PREC_FP16, stream);
+  return conv3_fwd(nullptr, x, ldx, w_packed_f16, bias, out, ldo, stats_acc, workspace, B, Cin,
+                   Cout, D, H, W, PREC_FP16, stream);
 }

@@ -1563,7 +1563,11 @@ static int go_dwfc_ws(const DwFcArgs& a, int prec, hipStream_t s, int min_blocks
   // WF_FFN_DWFC_SB=1 keeps the round-3 kernel, WF_FFN_DWFC_TB=1 the 3 x 8 single-barrier one
   static const char* tbv = getenv("WF_FFN_DWFC_TB");
   static const bool sbv = getenv("WF_FFN_DWFC_SB") != nullptr;
-  if (!ws && !sbv && prec != PREC_BF16)
+  // tb4 writes its output through buffer stores whose 32-bit byte offsets cover 2 GiB: larger
+  // outputs (stage 1 of a 128^3 input at B >= 43) take the SIMD-balanced kernel, which has no
+  // such limit
+  const bool tb4_fits = (int64_t)g.B * g.D * g.H * g.W * C * 4 < ((int64_t)1 << 31);
+  if (!ws && !sbv && prec != PREC_BF16 && (tb4_fits || (tbv && tbv[0] == '1')))
     return (tbv && tbv[0] == '1') ? launch_ffn_dwfc_tb(a, prec, s) : launch_ffn_dwfc_tb4(a, prec, s);
   void (*kern)(DwFcArgs) =
       ws ? (prec == PREC_SPLIT  ? ffn_dwfc_ws_kernel<PREC_SPLIT, float>

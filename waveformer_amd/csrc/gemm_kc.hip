@@ -209,10 +209,13 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
 
   // the loader's LayerNorm gamma/beta in LDS (a global load inside the k loop would queue on
   // the in-order vmcnt behind the prefetches and drain them every step)
+  // (sized for an even step count: the unrolled loop's extra step of an odd count reads
+  // lnw / lnb at k >= K, zeros here, discarded by its kv select)
+  const int nks2 = (nks + 1) & ~1;
   float* lnw = reinterpret_cast<float*>(Wl + (size_t)2 * NPL * NC * KC_KP);
-  float* lnb = lnw + nks * KC_BK;
+  float* lnb = lnw + nks2 * KC_BK;
   if (g.a_ln != LN_NONE) {
-    for (int i = tid; i < nks * KC_BK; i += C::NTHR) {
+    for (int i = tid; i < nks2 * KC_BK; i += C::NTHR) {
       lnw[i] = i < K ? g.a_ln_w[i] : 0.f;
       lnb[i] = i < K ? g.a_ln_b[i] : 0.f;
     }
@@ -309,7 +312,8 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
   } else {
     // both halves unconditional (a conditional second half makes the loop-carried register
     // sets phis, and their copies wait for the prefetches at every barrier): an odd step
-    // count runs one extra step with A and the weight slice zeroed (k >= K), adding exact zeros
+    // count runs one extra step whose A operands are zeroed (k >= K: the kv select) against a
+    // weight slice re-reading the last octet (finite), adding exact zeros
 #pragma unroll 1
     for (int ks = 0; ks < nks; ks += 2) {
       kbody(ks, Slot0{}, an[0]);
@@ -451,7 +455,8 @@ static void go_kc(const GemmArgs& g, hipStream_t s) {
     }
   }
   const size_t lds = (size_t)2 * (split ? 2 : 1) * C::NC * KC_KP * 2 +
-                     (g.a_ln != LN_NONE ? (size_t)2 * cdiv(g.K, KC_BK) * KC_BK * 4 : 0);
+                     (g.a_ln != LN_NONE ? (size_t)2 * ((cdiv(g.K, KC_BK) + 1) & ~1) * KC_BK * 4
+                                        : 0);
   if (lds > 64 * 1024)
     set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
   const dim3 grid((unsigned)cdiv(g.M, rows), (unsigned)(g.N / C::NC));

@@ -325,13 +325,17 @@ __global__ __launch_bounds__(256) void haar_analysis_ncdhw_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// window attention backward (fp32 VALU).  One workgroup = (64-key block, head, window); loops
-// over the 64-query blocks of the window:  S = scale q k^T + bias, P = exp2(S log2e - lse2),
-// dP = dO v^T, dS = P (dP - D), D = rowsum(dO o O);  dV += P^T dO, dK += scale dS^T q (kept in
-// registers), dQ += scale dS k (atomics into the raster row), dBias += dS (atomics into the
-// dense (heads, N, N) accumulator).  qkv / O / dO / lse are window-major; dqkv rows are written
-// to the raster row of the token (the inverse of window_partition), so the qkv weight gradient
-// pairs them with the un-permuted (normed) raster.
+// window attention backward (fp32 VALU), deterministic: no atomics, every sum in a fixed order.
+// One workgroup = (64-key block kb, head, window group g); it walks the windows g, g + G, ...
+// in order, and per window the 64-query blocks:  S = scale q k^T + bias,
+// P = exp2(S log2e - lse2), dP = dO v^T, dS = P (dP - D), D = rowsum(dO o O);
+// dV = P^T dO, dK = scale dS^T q (registers, written once per window to the raster row);
+// dQ (unscaled) of this key block -> dq_part[kb][window-major row] (each element written by
+// exactly one workgroup); dBias -> db_part[g][h][q][key], owned by this workgroup and summed
+// over its windows in order.  attn_dq_reduce / attn_db_reduce then add the key-block / group
+// partials in index order.  qkv / O / dO / lse are window-major; dqkv rows are RASTER rows of
+// the token (the inverse of window_partition), so the qkv weight gradient pairs them with the
+// un-permuted (normed) raster.
 // ------------------------------------------------------------------------------------------
 constexpr int kAB = 64;
 
@@ -341,23 +345,26 @@ struct AttnBwdArgs {
   const float* dout;  // (Bw*N, C) gradient of o
   const float* bias;  // (heads, N, N)
   const float* lse;   // (Bw, heads, N) log2-domain row log-sum-exp of the forward
-  float* dqkv;        // (B*D1*H1*W1, 3C) raster rows, zeroed by the caller
-  float* dbias;       // (heads, N, N), zeroed by the caller
+  float* dqkv;        // (B*D1*H1*W1, 3C) raster rows: dK / dV columns written here
+  float* dq_part;     // (nkb, Bw*N, C) window-major, unscaled
+  float* db_part;     // (G, heads, N, N)
+  int64_t Bw;
   int N, heads, C, ws, nD, nH, nW;  // windows per axis
+  int G;
   float scale, scale_log2;
 };
 
-__device__ __forceinline__ int64_t raster_row(const AttnBwdArgs& a, int64_t bw, int t) {
-  const int ws = a.ws;
+__device__ __forceinline__ int64_t raster_row_of(int64_t bw, int t, int ws, int nD, int nH,
+                                                 int nW) {
   int64_t r = bw;
-  const int ww = (int)(r % a.nW);
-  r /= a.nW;
-  const int wh = (int)(r % a.nH);
-  r /= a.nH;
-  const int wd = (int)(r % a.nD);
-  const int64_t b = r / a.nD;
+  const int ww = (int)(r % nW);
+  r /= nW;
+  const int wh = (int)(r % nH);
+  r /= nH;
+  const int wd = (int)(r % nD);
+  const int64_t b = r / nD;
   const int tx = t % ws, ty = (t / ws) % ws, tz = t / (ws * ws);
-  const int64_t D1 = (int64_t)a.nD * ws, H1 = (int64_t)a.nH * ws, W1 = (int64_t)a.nW * ws;
+  const int64_t D1 = (int64_t)nD * ws, H1 = (int64_t)nH * ws, W1 = (int64_t)nW * ws;
   return ((b * D1 + wd * ws + tz) * H1 + wh * ws + ty) * W1 + ww * ws + tx;
 }
 
@@ -369,153 +376,203 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnBwdArgs a) {
   __shared__ float Ps[kAB][kAB + 1], dSs[kAB][kAB + 1];
   __shared__ float Ls[kAB], Dq[kAB];
   const int tid = threadIdx.x;
-  const int kb = blockIdx.x, h = blockIdx.y;
-  const int64_t bw = blockIdx.z;
+  const int kb = blockIdx.x, h = blockIdx.y, g = blockIdx.z;
   const int N = a.N, C = a.C, ld = 3 * C;
-  const int64_t row0 = bw * N;
   const int k0 = kb * kAB;
-
-  // this block's keys / values
-  for (int i = tid; i < kAB * HD; i += 256) {
-    const int r = i / HD, dd = i % HD;
-    const int key = k0 + r;
-    float kv = 0.f, vv = 0.f;
-    if (key < N) {
-      const float* p = a.qkv + (row0 + key) * ld + h * HD + dd;
-      kv = p[C];
-      vv = p[2 * C];
-    }
-    Ks[r][dd] = kv;
-    Vs[r][dd] = vv;
-  }
   // phase-2 ownership: key/query row pr = tid / 4, head-dim chunk d0
   const int pr = tid >> 2, d0 = (tid & 3) * DPT;
-  float dk[DPT], dv[DPT];
-#pragma unroll
-  for (int e = 0; e < DPT; ++e) dk[e] = dv[e] = 0.f;
   // S-tile ownership: queries ti*4 .. +3, keys tj*4 .. +3
   const int ti = tid >> 4, tj = tid & 15;
+  float* dq_base = a.dq_part + (int64_t)kb * a.Bw * N * C;
 
-  for (int q0 = 0; q0 < N; q0 += kAB) {
-    __syncthreads();  // previous iteration done with Qs / dOs / Ps / dSs
+  for (int64_t bw = g; bw < a.Bw; bw += a.G) {
+    const bool first = bw == g;
+    const int64_t row0 = bw * N;
+    __syncthreads();  // the previous window is done with Ks / Vs
+    // this block's keys / values
     for (int i = tid; i < kAB * HD; i += 256) {
       const int r = i / HD, dd = i % HD;
-      const int q = q0 + r;
-      float qv = 0.f, gv = 0.f;
-      if (q < N) {
-        qv = a.qkv[(row0 + q) * ld + h * HD + dd];
-        gv = a.dout[(row0 + q) * C + h * HD + dd];
+      const int key = k0 + r;
+      float kv = 0.f, vv = 0.f;
+      if (key < N) {
+        const float* p = a.qkv + (row0 + key) * ld + h * HD + dd;
+        kv = p[C];
+        vv = p[2 * C];
       }
-      Qs[r][dd] = qv;
-      dOs[r][dd] = gv;
+      Ks[r][dd] = kv;
+      Vs[r][dd] = vv;
     }
-    {  // D = rowsum(dO o O): 4 lanes per query
-      const int q = q0 + pr;
-      float s = 0.f;
-      if (q < N) {
-        const float* op = a.o + (row0 + q) * C + h * HD + d0;
-        const float* gp = a.dout + (row0 + q) * C + h * HD + d0;
+    float dk[DPT], dv[DPT];
 #pragma unroll
-        for (int e = 0; e < DPT; ++e) s += op[e] * gp[e];
+    for (int e = 0; e < DPT; ++e) dk[e] = dv[e] = 0.f;
+
+    for (int q0 = 0; q0 < N; q0 += kAB) {
+      __syncthreads();  // previous iteration done with Qs / dOs / Ps / dSs
+      for (int i = tid; i < kAB * HD; i += 256) {
+        const int r = i / HD, dd = i % HD;
+        const int q = q0 + r;
+        float qv = 0.f, gv = 0.f;
+        if (q < N) {
+          qv = a.qkv[(row0 + q) * ld + h * HD + dd];
+          gv = a.dout[(row0 + q) * C + h * HD + dd];
+        }
+        Qs[r][dd] = qv;
+        dOs[r][dd] = gv;
       }
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      if ((tid & 3) == 0) {
-        Dq[pr] = s;
-        Ls[pr] = q < N ? a.lse[(bw * a.heads + h) * N + q] : 0.f;
+      {  // D = rowsum(dO o O): 4 lanes per query
+        const int q = q0 + pr;
+        float s = 0.f;
+        if (q < N) {
+          const float* op = a.o + (row0 + q) * C + h * HD + d0;
+          const float* gp = a.dout + (row0 + q) * C + h * HD + d0;
+#pragma unroll
+          for (int e = 0; e < DPT; ++e) s += op[e] * gp[e];
+        }
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        if ((tid & 3) == 0) {
+          Dq[pr] = s;
+          Ls[pr] = q < N ? a.lse[(bw * a.heads + h) * N + q] : 0.f;
+        }
       }
-    }
-    __syncthreads();
-    // S, dP microtiles
-    float s[4][4], dp[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s[i][j] = dp[i][j] = 0.f;
-#pragma unroll
-    for (int dd = 0; dd < HD; ++dd) {
-      float qv[4], gv[4], kv[4], vv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        qv[i] = Qs[ti * 4 + i][dd];
-        gv[i] = dOs[ti * 4 + i][dd];
-        kv[i] = Ks[tj * 4 + i][dd];
-        vv[i] = Vs[tj * 4 + i][dd];
-      }
+      __syncthreads();
+      // S, dP microtiles
+      float s[4][4], dp[4][4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
+        for (int j = 0; j < 4; ++j) s[i][j] = dp[i][j] = 0.f;
+#pragma unroll
+      for (int dd = 0; dd < HD; ++dd) {
+        float qv[4], gv[4], kv[4], vv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          qv[i] = Qs[ti * 4 + i][dd];
+          gv[i] = dOs[ti * 4 + i][dd];
+          kv[i] = Ks[tj * 4 + i][dd];
+          vv[i] = Vs[tj * 4 + i][dd];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            s[i][j] = fmaf(qv[i], kv[j], s[i][j]);
+            dp[i][j] = fmaf(gv[i], vv[j], dp[i][j]);
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ql = ti * 4 + i, q = q0 + ql;
+        const bool qok = q < N;
+        const float* brow = a.bias + ((int64_t)h * N + (qok ? q : 0)) * N;
+        float* dbrow = a.db_part + (((int64_t)g * a.heads + h) * N + (qok ? q : 0)) * N;
+#pragma unroll
         for (int j = 0; j < 4; ++j) {
-          s[i][j] = fmaf(qv[i], kv[j], s[i][j]);
-          dp[i][j] = fmaf(gv[i], vv[j], dp[i][j]);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ql = ti * 4 + i, q = q0 + ql;
-      const bool qok = q < N;
-      const float* brow = a.bias + ((int64_t)h * N + (qok ? q : 0)) * N;
-      float* dbrow = a.dbias + ((int64_t)h * N + (qok ? q : 0)) * N;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int kl = tj * 4 + j, key = k0 + kl;
-        const bool ok = qok && key < N;
-        float p = 0.f, ds = 0.f;
-        if (ok) {
-          p = exp2f(s[i][j] * a.scale_log2 + brow[key] * 1.4426950408889634f - Ls[ql]);
-          ds = p * (dp[i][j] - Dq[ql]);
-          atomicAdd(dbrow + key, ds);
-        }
-        Ps[ql][kl] = p;
-        dSs[ql][kl] = ds;
-      }
-    }
-    __syncthreads();
-    // dV, dK for key pr; dQ for query pr
-    {
-      const int kl = pr;
-      for (int ql = 0; ql < kAB; ++ql) {
-        const float p = Ps[ql][kl], ds = dSs[ql][kl];
-#pragma unroll
-        for (int e = 0; e < DPT; ++e) {
-          dv[e] = fmaf(p, dOs[ql][d0 + e], dv[e]);
-          dk[e] = fmaf(ds, Qs[ql][d0 + e], dk[e]);
+          const int kl = tj * 4 + j, key = k0 + kl;
+          const bool ok = qok && key < N;
+          float p = 0.f, ds = 0.f;
+          if (ok) {
+            p = exp2f(s[i][j] * a.scale_log2 + brow[key] * 1.4426950408889634f - Ls[ql]);
+            ds = p * (dp[i][j] - Dq[ql]);
+            // this thread owns db_part[g][h][q][key]: the windows of group g add in order
+            dbrow[key] = first ? ds : dbrow[key] + ds;
+          }
+          Ps[ql][kl] = p;
+          dSs[ql][kl] = ds;
         }
       }
-      const int ql = pr, q = q0 + ql;
-      if (q < N) {
-        float dq[DPT];
+      __syncthreads();
+      // dV, dK for key pr; this key block's dQ for query pr
+      {
+        const int kl = pr;
+        for (int ql = 0; ql < kAB; ++ql) {
+          const float p = Ps[ql][kl], ds = dSs[ql][kl];
 #pragma unroll
-        for (int e = 0; e < DPT; ++e) dq[e] = 0.f;
-        for (int k = 0; k < kAB; ++k) {
-          const float ds = dSs[ql][k];
-#pragma unroll
-          for (int e = 0; e < DPT; ++e) dq[e] = fmaf(ds, Ks[k][d0 + e], dq[e]);
+          for (int e = 0; e < DPT; ++e) {
+            dv[e] = fmaf(p, dOs[ql][d0 + e], dv[e]);
+            dk[e] = fmaf(ds, Qs[ql][d0 + e], dk[e]);
+          }
         }
-        float* dst = a.dqkv + raster_row(a, bw, q) * ld + h * HD + d0;
+        const int ql = pr, q = q0 + ql;
+        if (q < N) {
+          float dq[DPT];
 #pragma unroll
-        for (int e = 0; e < DPT; ++e) atomicAdd(dst + e, dq[e] * a.scale);
+          for (int e = 0; e < DPT; ++e) dq[e] = 0.f;
+          for (int k = 0; k < kAB; ++k) {
+            const float ds = dSs[ql][k];
+#pragma unroll
+            for (int e = 0; e < DPT; ++e) dq[e] = fmaf(ds, Ks[k][d0 + e], dq[e]);
+          }
+          float* dst = dq_base + (row0 + q) * C + h * HD + d0;
+#pragma unroll
+          for (int e = 0; e < DPT; ++e) dst[e] = dq[e];
+        }
       }
     }
-  }
-  const int key = k0 + pr;
-  if (key < N) {
-    float* dst = a.dqkv + raster_row(a, bw, key) * ld + h * HD + d0;
+    const int key = k0 + pr;
+    if (key < N) {
+      float* dst = a.dqkv + raster_row_of(bw, key, a.ws, a.nD, a.nH, a.nW) * ld + h * HD + d0;
 #pragma unroll
-    for (int e = 0; e < DPT; ++e) {
-      dst[C + e] = dk[e] * a.scale;
-      dst[2 * C + e] = dv[e];
+      for (int e = 0; e < DPT; ++e) {
+        dst[C + e] = dk[e] * a.scale;
+        dst[2 * C + e] = dv[e];
+      }
     }
   }
 }
 
-__global__ void rel_pos_bias_bwd_kernel(const float* __restrict__ dbias,
-                                        const int64_t* __restrict__ index,
-                                        float* __restrict__ dtable, int64_t NN, int heads) {
+// dQ of window-major row wr = scale * sum_kb dq_part[kb][wr] (kb ascending) -> the q columns of
+// the token's raster row; one thread per (row, 4 channels)
+__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(const float* __restrict__ part,
+                                                             float* __restrict__ dqkv,
+                                                             int64_t rows, int C, int nkb,
+                                                             float scale, int ws, int nD, int nH,
+                                                             int nW) {
+  const int C4 = C >> 2;
+  const int64_t total = rows * C4;
+  const int N = ws * ws * ws;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t wr = i / C4;
+    const int c = 4 * (int)(i - wr * C4);
+    f32x4 s = *reinterpret_cast<const f32x4*>(part + wr * C + c);
+    for (int k = 1; k < nkb; ++k)
+      s += *reinterpret_cast<const f32x4*>(part + ((int64_t)k * rows + wr) * C + c);
+    const int64_t bw = wr / N;
+    const int t = (int)(wr - bw * N);
+    *reinterpret_cast<f32x4*>(dqkv + raster_row_of(bw, t, ws, nD, nH, nW) * 3 * C + c) =
+        s * scale;
+  }
+}
+
+// dbias[e] = sum_g db_part[g][e] (g ascending), e over heads * N * N
+__global__ __launch_bounds__(256) void attn_db_reduce_kernel(const float* __restrict__ part,
+                                                             float* __restrict__ dbias,
+                                                             int64_t n, int G) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = part[i];
+    for (int g = 1; g < G; ++g) s += part[(int64_t)g * n + i];
+    dbias[i] = s;
+  }
+}
+
+// dtable[r][h] = sum over the (i, j) with index[i][j] == r, in ascending flat order, of
+// dbias[h][i][j] -- the adjoint of the gather at attention.py:94-97 without atomics: `perm`
+// lists the flat positions grouped by table row (a stable sort of the index), `offsets` (T + 1)
+// delimits each row's group
+__global__ __launch_bounds__(256) void rel_pos_bias_bwd_kernel(const float* __restrict__ dbias,
+                                                               const int64_t* __restrict__ perm,
+                                                               const int64_t* __restrict__ offsets,
+                                                               float* __restrict__ dtable,
+                                                               int64_t NN, int heads, int64_t T) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= NN) return;
-  const int64_t r = index[i];
-  for (int h = 0; h < heads; ++h) atomicAdd(dtable + r * heads + h, dbias[h * NN + i]);
+  if (i >= T * heads) return;
+  const int64_t r = i / heads;
+  const int h = (int)(i - r * heads);
+  float s = 0.f;
+  for (int64_t k = offsets[r]; k < offsets[r + 1]; ++k) s += dbias[(int64_t)h * NN + perm[k]];
+  dtable[i] = s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -913,14 +970,38 @@ extern "C" int wf_haar_analysis_ncdhw(const float* in, int64_t in_bstride, int64
   return check_launch("wf_haar_analysis_ncdhw");
 }
 
+namespace {
+// window groups of the attention backward: enough (key block, head, group) workgroups to
+// cover the CUs, each group walking ceil(Bw / G) windows
+int64_t attn_bwd_groups(int64_t Bw, int64_t N, int64_t heads) {
+  const int64_t nkb = cdiv(N, kAB);
+  int64_t G = cdiv(1024, nkb * heads);
+  G = std::min<int64_t>(std::max<int64_t>(G, 1), Bw);
+  return cdiv(Bw, cdiv(Bw, G));  // balance: every group gets the same window count (+-1)
+}
+inline int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
+}  // namespace
+
+extern "C" int64_t wf_window_attention_bwd_workspace_bytes(int64_t B, int64_t C, int64_t D1,
+                                                           int64_t H1, int64_t W1, int64_t ws,
+                                                           int64_t heads) {
+  if (ws < 1 || heads < 1 || D1 % ws || H1 % ws || W1 % ws) return -1;
+  const int64_t N = ws * ws * ws;
+  const int64_t Bw = B * (D1 / ws) * (H1 / ws) * (W1 / ws);
+  const int64_t rows = B * D1 * H1 * W1;
+  const int64_t G = attn_bwd_groups(Bw, N, heads);
+  return align256(cdiv(N, kAB) * rows * C * 4) + align256(G * heads * N * N * 4);
+}
+
 extern "C" int wf_window_attention_bwd_core(const float* qkv, const float* o, const float* dout,
                                             const float* bias, const float* lse, float* dqkv,
-                                            float* dbias, int64_t B, int64_t C, int64_t D1,
-                                            int64_t H1, int64_t W1, int64_t ws, int64_t heads,
-                                            float scale, void* stream) {
+                                            float* dbias, void* workspace, int64_t B, int64_t C,
+                                            int64_t D1, int64_t H1, int64_t W1, int64_t ws,
+                                            int64_t heads, float scale, void* stream) {
   WF_REQUIRE(ws >= 1 && D1 % ws == 0 && H1 % ws == 0 && W1 % ws == 0,
              "the raster must tile into ws^3 windows");
-  WF_REQUIRE(heads >= 1 && C % heads == 0, "dim must be divisible by num_heads");
+  WF_REQUIRE(heads >= 1 && C % heads == 0 && C % 4 == 0,
+             "dim must be divisible by num_heads and by 4");
   WF_REQUIRE_PTR(qkv);
   WF_REQUIRE_PTR(o);
   WF_REQUIRE_PTR(dout);
@@ -928,13 +1009,17 @@ extern "C" int wf_window_attention_bwd_core(const float* qkv, const float* o, co
   WF_REQUIRE_PTR(lse);
   WF_REQUIRE_PTR(dqkv);
   WF_REQUIRE_PTR(dbias);
+  WF_REQUIRE_PTR(workspace);
   const int64_t N = ws * ws * ws;
   const int64_t Bw = B * (D1 / ws) * (H1 / ws) * (W1 / ws);
-  WF_REQUIRE(Bw <= 65535, "more than 65535 windows per call");
-  hipStream_t s = (hipStream_t)stream;
   const int64_t rows = B * D1 * H1 * W1;
-  WF_HIP(hipMemsetAsync(dqkv, 0, rows * 3 * C * sizeof(float), s));
-  WF_HIP(hipMemsetAsync(dbias, 0, heads * N * N * sizeof(float), s));
+  const int64_t nkb = cdiv(N, kAB);
+  const int64_t G = attn_bwd_groups(Bw, N, heads);
+  WF_REQUIRE(G <= 65535 && nkb <= 65535, "too many windows per call");
+  const int hd = (int)(C / heads);
+  WF_REQUIRE(hd == 16 || hd == 32 || hd == 48 || hd == 64,
+             "attention backward: head_dim must be 16, 32, 48 or 64");
+  hipStream_t s = (hipStream_t)stream;
   AttnBwdArgs a;
   a.qkv = qkv;
   a.o = o;
@@ -942,7 +1027,10 @@ extern "C" int wf_window_attention_bwd_core(const float* qkv, const float* o, co
   a.bias = bias;
   a.lse = lse;
   a.dqkv = dqkv;
-  a.dbias = dbias;
+  a.dq_part = static_cast<float*>(workspace);
+  a.db_part = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                       align256(nkb * rows * C * 4));
+  a.Bw = Bw;
   a.N = (int)N;
   a.heads = (int)heads;
   a.C = (int)C;
@@ -950,30 +1038,42 @@ extern "C" int wf_window_attention_bwd_core(const float* qkv, const float* o, co
   a.nD = (int)(D1 / ws);
   a.nH = (int)(H1 / ws);
   a.nW = (int)(W1 / ws);
+  a.G = (int)G;
   a.scale = scale;
   a.scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid((unsigned)cdiv(N, kAB), (unsigned)heads, (unsigned)Bw);
-  const int hd = (int)(C / heads);
+  dim3 grid((unsigned)nkb, (unsigned)heads, (unsigned)G);
   switch (hd) {
     case 16: hipLaunchKernelGGL(attn_bwd_kernel<16>, grid, dim3(256), 0, s, a); break;
     case 32: hipLaunchKernelGGL(attn_bwd_kernel<32>, grid, dim3(256), 0, s, a); break;
     case 48: hipLaunchKernelGGL(attn_bwd_kernel<48>, grid, dim3(256), 0, s, a); break;
-    case 64: hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, s, a); break;
-    default: return fail(WF_E_SHAPE, "attention backward: head_dim must be 16, 32, 48 or 64");
+    default: hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, s, a); break;
   }
-  return check_launch("wf_window_attention_bwd_core");
+  int rc = check_launch("wf_window_attention_bwd_core");
+  if (rc) return rc;
+  const int64_t tq = rows * (C / 4);
+  hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(tq, 256), 8192)),
+                     dim3(256), 0, s, a.dq_part, dqkv, rows, (int)C, (int)nkb, scale, (int)ws,
+                     a.nD, a.nH, a.nW);
+  rc = check_launch("wf_window_attention_bwd_core (dQ reduce)");
+  if (rc) return rc;
+  const int64_t nb = heads * N * N;
+  hipLaunchKernelGGL(attn_db_reduce_kernel, dim3((unsigned)std::min<int64_t>(cdiv(nb, 256), 8192)),
+                     dim3(256), 0, s, a.db_part, dbias, nb, (int)G);
+  return check_launch("wf_window_attention_bwd_core (dBias reduce)");
 }
 
-extern "C" int wf_rel_pos_bias_bwd(const float* dbias, const int64_t* index, float* dtable,
-                                   int64_t N, int64_t heads, int64_t table_rows, void* stream) {
+extern "C" int wf_rel_pos_bias_bwd(const float* dbias, const int64_t* perm,
+                                   const int64_t* offsets, float* dtable, int64_t N, int64_t heads,
+                                   int64_t table_rows, void* stream) {
   WF_REQUIRE_PTR(dbias);
-  WF_REQUIRE_PTR(index);
+  WF_REQUIRE_PTR(perm);
+  WF_REQUIRE_PTR(offsets);
   WF_REQUIRE_PTR(dtable);
-  hipStream_t s = (hipStream_t)stream;
-  WF_HIP(hipMemsetAsync(dtable, 0, table_rows * heads * sizeof(float), s));
-  const int64_t NN = N * N;
-  hipLaunchKernelGGL(rel_pos_bias_bwd_kernel, dim3((unsigned)cdiv(NN, 256)), dim3(256), 0, s,
-                     dbias, index, dtable, NN, (int)heads);
+  WF_REQUIRE(heads >= 1 && table_rows >= 1, "empty table");
+  const int64_t n = table_rows * heads;
+  hipLaunchKernelGGL(rel_pos_bias_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     (hipStream_t)stream, dbias, perm, offsets, dtable, N * N, (int)heads,
+                     table_rows);
   return check_launch("wf_rel_pos_bias_bwd");
 }
 

@@ -243,6 +243,17 @@ def _attn_setup(ctx, inputs, output):
     ctx.save_for_backward(x, ln_w, ln_b, wqkv, bqkv, table, index, wproj, bproj, work, lse)
 
 
+def _index_groups(index: Tensor, rows: int) -> Tuple[Tensor, Tensor]:
+    """The relative-position index (attention.py:40-56) grouped by table row for the
+    deterministic bias-table gather (wf_rel_pos_bias_bwd): `perm` = the flat positions in a
+    stable sort by row, `offsets` (rows + 1) the group boundaries."""
+    flat = index.reshape(-1)
+    vals, perm = torch.sort(flat, stable=True)
+    offsets = torch.searchsorted(vals, torch.arange(rows + 1, device=index.device,
+                                                    dtype=vals.dtype))
+    return perm.contiguous(), offsets.to(torch.int64).contiguous()
+
+
 @torch.library.custom_op("waveformer::window_attn_backward", mutates_args=(),
                          device_types="cuda")
 def window_attn_backward(gout: Tensor, x: Tensor, ln_w: Optional[Tensor],
@@ -273,12 +284,15 @@ def window_attn_backward(gout: Tensor, x: Tensor, ln_w: Optional[Tensor],
     do = g.mm(wproj)
     dqkv = torch.empty((rows, 3 * C), dtype=torch.float32, device=x.device)
     dbias = torch.empty((heads, N, N), dtype=torch.float32, device=x.device)
+    bws = torch.empty(_lib.query("wf_window_attention_bwd_workspace_bytes", B, C, D1, H1, W1, ws,
+                                 heads), dtype=torch.uint8, device=x.device)
     _lib.call("wf_window_attention_bwd_core", qkv.data_ptr(), o.data_ptr(), do.data_ptr(),
-              bias.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), dbias.data_ptr(), B, C, D1,
-              H1, W1, ws, heads, float(scale), _s())
+              bias.data_ptr(), lse.data_ptr(), dqkv.data_ptr(), dbias.data_ptr(),
+              bws.data_ptr(), B, C, D1, H1, W1, ws, heads, float(scale), _s())
     dtable = torch.empty(tuple(table.shape), dtype=torch.float32, device=x.device)
-    _lib.call("wf_rel_pos_bias_bwd", dbias.data_ptr(), index.data_ptr(), dtable.data_ptr(), N,
-              heads, table.shape[0], _s())
+    perm, offsets = _index_groups(index, table.shape[0])
+    _lib.call("wf_rel_pos_bias_bwd", dbias.data_ptr(), perm.data_ptr(), offsets.data_ptr(),
+              dtable.data_ptr(), N, heads, table.shape[0], _s())
     # qkv = xin Wqkv^T + bqkv with xin = norm1?(x) in raster order (dqkv is raster-ordered)
     x2 = x.view(rows, C)
     xin = ln_fwd(x2, ln_w, ln_b, eps, False) if ln_w is not None else x2

@@ -66,8 +66,15 @@ class Attention(nn.Module):
 
     def _apply(self, fn, *args, **kwargs):
         # .to() / .cuda() / .half() replace the buffer by a copy of the same contents (at a
-        # fresh version counter): the formula check still holds for the new tensor
+        # fresh version counter): the formula check still holds for the new tensor -- unless
+        # the buffer was written in place since that check (its version moved on), in which
+        # case the moved contents are checked again (a host sync, outside any forward)
+        stale = self._index_formula and \
+            self.relative_position_index._version != self._index_version
         ret = super()._apply(fn, *args, **kwargs)
+        if stale:
+            self._index_formula = ops.index_is_formula(self.relative_position_index,
+                                                       self.window_size)
         self._index_version = self.relative_position_index._version
         return ret
 

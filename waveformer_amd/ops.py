@@ -435,7 +435,10 @@ def idwt3d_haar(ll: torch.Tensor, details: Sequence[Dict[str, torch.Tensor]],
     skip_ld = cl_ld(skip) if skip is not None else None
     fused = (skip is not None and ldo is not None and ll_ld is not None and skip_ld is not None
              and C % 4 == 0 and skip.device == out.device and skip.dtype == torch.float32
-             and skip.stride(0) % 4 == 0 and skip.data_ptr() % 16 == 0)
+             and skip.stride(0) % 4 == 0 and skip.data_ptr() % 16 == 0
+             # the debug switch WF_IDWT_SCALAR (read per call by the library) selects the scalar
+             # kernel, which has no fused concat: IDWT + copy then
+             and "WF_IDWT_SCALAR" not in os.environ)
     if fused:
         _lib.call("wf_idwt3d_haar_cl_cat", ll.data_ptr(), ll.stride(0), 1, ll_ld, arr, sarr, L,
                   skip.data_ptr(), skip.stride(0), skip_ld, out.data_ptr(), out.stride(0), ldo,
@@ -767,6 +770,12 @@ def conv3d_k3_packed(weight: torch.Tensor, prec: Optional[int] = None) -> torch.
     return per_forward(("conv3", weight.data_ptr(), tuple(weight.shape), f16), make)
 
 
+def _conv3_workspace(B, Cin, Cout, D, H, W, prec, xh, device) -> Optional[torch.Tensor]:
+    """The split-K partial buffer of a small-grid conv3d_k3 (None when the grid is not split)."""
+    n = _lib.query("wf_conv3d_k3_workspace_bytes", B, Cin, Cout, D, H, W, prec, int(xh))
+    return torch.empty(n, dtype=torch.uint8, device=device) if n > 0 else None
+
+
 def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
               out: Optional[torch.Tensor] = None, norm_eps: Optional[float] = None):
     """Conv3d(k=3, stride 1, padding 1) of an NCDHW-shaped fp32 tensor on the MFMA implicit-GEMM
@@ -793,8 +802,9 @@ def conv3d_k3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor
     if norm_eps is not None:
         acc = torch.zeros((B, Cout, 2), dtype=torch.float64, device=x.device)
     prec = _prec()
+    work = _conv3_workspace(B, Cin, Cout, D, H, W, prec, False, x.device)
     _lib.call("wf_conv3d_k3_fwd", x.data_ptr(), cl_ld(x), conv3d_k3_packed(weight, prec).data_ptr(),
-              _ptr(bias), out.data_ptr(), ldo, _ptr(acc), B, Cin, Cout, D, H, W, prec,
+              _ptr(bias), out.data_ptr(), ldo, _ptr(acc), _ptr(work), B, Cin, Cout, D, H, W, prec,
               _stream())
     if acc is None:
         return out
@@ -824,8 +834,10 @@ def _conv3d_k3_xh(x, weight, bias, out, norm_eps):
     acc = None
     if norm_eps is not None:
         acc = torch.zeros((B, Cout, 2), dtype=torch.float64, device=x.device)
+    work = _conv3_workspace(B, Cin, Cout, D, H, W, FP16, True, x.device)
     _lib.call("wf_conv3d_k3_fwd_xh", x.data_ptr(), ld, conv3d_k3_packed(weight, FP16).data_ptr(),
-              _ptr(bias), out.data_ptr(), ldo, _ptr(acc), B, Cin, Cout, D, H, W, _stream())
+              _ptr(bias), out.data_ptr(), ldo, _ptr(acc), _ptr(work), B, Cin, Cout, D, H, W,
+              _stream())
     if acc is None:
         return out
     stats = torch.empty((B, 2, Cout), dtype=torch.float32, device=x.device)
