@@ -181,12 +181,18 @@ class OpTimer:
             if not self.active:
                 return self.orig(*a, **kw)
             out = self.orig(*a, **kw)
+            # MFMA operand precision of this launch (the fp16 policy keeps attention and the
+            # skip-feature convolutions at bf16x3): 3 issued MFMAs per product for bf16x3
+            prec = kw.get("prec") if name == "window_attention" else None
+            if prec is None:
+                prec = self.ops.prec_id()
+            issue = 3 if prec == self.ops.PRECISIONS["bf16x3"] else 1
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(self.REPS):
                 self.orig(*a, **kw)
             e.record()
-            self.rec.append((self.WORK[name](a, kw, out), s, e))
+            self.rec.append((self.WORK[name](a, kw, out), s, e, issue))
             return out
 
         setattr(ops, name, wrapped)
@@ -197,17 +203,18 @@ class OpTimer:
         torch.cuda.synchronize()
         if not self.rec:
             return None
-        big = max(b for b, _, _ in self.rec)
-        sel = [(b, s.elapsed_time(e) / self.REPS) for b, s, e in self.rec if b == big]
-        avg_ms = sum(t for _, t in sel) / len(sel)
+        big = max(r[0] for r in self.rec)
+        sel = [(b, s.elapsed_time(e) / self.REPS, i) for b, s, e, i in self.rec if b == big]
+        avg_ms = sum(t for _, t, _ in sel) / len(sel)
         return {"work_per_launch": big, "avg_ms": avg_ms, "launches": len(sel),
-                "rate": big / (avg_ms * 1e-3)}
+                "rate": big / (avg_ms * 1e-3), "issue": max(i for _, _, i in sel)}
 
 
-def pmc_traffic(kernel_substr, batch):
+def pmc_traffic(kernel_substr, batch, grid=None):
     """HBM bytes per launch from the newest profiles/*pmc*.json written by tools/pmc_traffic.py
     whose PMC passes ran at this per-GPU batch (summaries without the field were taken at 4);
-    None when no summary matches."""
+    None when no summary matches.  With `grid` (the timed launch's size in work-items) the
+    entry of that launch shape; None when the summary has no per-shape record of it."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True)
     for f in files:
         try:
@@ -218,7 +225,9 @@ def pmc_traffic(kernel_substr, batch):
             continue
         for k, v in d["kernels"].items():
             if kernel_substr in k:
-                return v.get("hbm_bytes_per_launch_largest")
+                if grid is None:
+                    return v.get("hbm_bytes_per_launch_largest")
+                return v.get("by_grid", {}).get(str(grid), {}).get("hbm_bytes_per_launch")
         return None
     return None
 
@@ -283,10 +292,15 @@ def idwt_roofline(batch, dev, layout="cl"):
         alg *= 2  # + the skip: 4 B read + 4 B written per element
     ach = alg / (us * 1e-6) / 1e9
     del bands, ll, det, out, skip
-    kname = {"cl": "idwt3d_haar_cl4", "cat": "idwt3d_haar_cl4", "ncdhw": "idwt3d_haar_nc4"}[layout]
+    # the plain and the fused-concat launches are separate instantiations (<false> / <true>),
+    # so the counter summary tells them apart; the cl4 grid is one thread per finest
+    # 4-channel group
+    kname = {"cl": "idwt3d_haar_cl4_kernel<false>", "cat": "idwt3d_haar_cl4_kernel<true>",
+             "ncdhw": "idwt3d_haar_nc4"}[layout]
+    grid = (-(-batch * 128 ** 3 * 12 // 256)) * 256 if layout != "ncdhw" else None
     return {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(kname, batch), "algorithmic_bytes_per_launch": alg,
+            "traffic": pmc_traffic(kname, batch, grid), "algorithmic_bytes_per_launch": alg,
             "avg_launch_us": round(us, 2), "launches_timed": reps,
             "shape": f"channel-last bands 8 x ({batch}, 64^3, 48) -> ({batch}, 48, 128^3) "
                      f"{'NCDHW' if layout == 'ncdhw' else 'channel-last'} into a 96-channel "
@@ -427,7 +441,7 @@ def main_sliding(args, world, rank, dev):
         rl = {}
         if rc:  # the dominant kernel of this workload (a third of the step)
             ach = rc["rate"] / 1e12
-            issue = 3 if args.precision == "bf16x3" else 1
+            issue = rc["issue"]
             rl["conv3d_k3"] = {
                 "bound": "mfma", "kernel": "conv3d_k3", "achieved": round(ach, 1),
                 "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -712,7 +726,7 @@ def main():
                 # MFMA-bound: algorithmic FLOPs vs the dense bf16 / fp16 peak (the same 2.5
                 # PFLOP/s on gfx950); bf16x3 issues three MFMAs per product
                 ach = r["rate"] / 1e12
-                issue = 3 if args.precision == "bf16x3" else 1
+                issue = r["issue"]  # of the timed launches (fp16 mode: attention at bf16x3)
                 return {"bound": "mfma", "kernel": name, "achieved": round(ach, 2),
                         "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
@@ -742,9 +756,18 @@ def main():
             out["rooflines"]["idwt3d_haar_ncdhw"] = idwt_roofline(args.batch, dev, "ncdhw")
             out["rooflines"]["idwt3d_haar_cat"] = idwt_roofline(args.batch, dev, "cat")
         if "window_attention" in out["rooflines"]:
+            wa = out["rooflines"]["window_attention"]
+            # the core's MFMA issue per useful flop at head_dim 16 (attention.hip attn_tbl):
+            # QK^T packs hd = 16 into K = 32 (2x) and bf16x3 adds the lo pass (4x); PV issues
+            # vl*P + vh*P_lo + vh*P (3x) plus the MFMA row sums (ones*P_lo, ones*P: +2x):
+            # 147,456 issued for 32,768 useful flops per 16 queries x 32 keys = 4.5x (bf16x3);
+            # 2.0x with plain 16-bit operands.  A saturated pipe reaches 1 / that of the peak
+            # in useful flops -- the ceiling beside north_star's 60 % target
+            ipu = 4.5 if wa.get("mfma_issue_frac", 0) > wa.get("frac", 0) * 2 else 2.0
+            wa["core_mfma_issued_per_useful"] = ipu
+            wa["core_useful_frac_ceiling"] = round(1.0 / ipu, 4)
             vf, src = pmc_valu("attn_tbl_kernel", args.batch)
             if vf is not None:
-                wa = out["rooflines"]["window_attention"]
                 wa["core_valu_issue_frac"] = vf["valu_issue_frac"]
                 if "mfma_busy_frac" in vf:  # SQ_VALU_MFMA_BUSY_CYCLES: the pipe, not the spec
                     wa["core_mfma_busy_frac"] = vf["mfma_busy_frac"]

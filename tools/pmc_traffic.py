@@ -11,7 +11,9 @@ listed in WIDE16 -- their bulk reads are 16 B per lane (f32x4 / b128 loads, chec
 source) -- and every other kernel's FETCH_SIZE is reported raw with rule "raw-uncalibrated"
 (the old scalar IDWT read its bands 4 B per lane and the blanket x2
 inflated its traffic to 1.44x).  Each kernel's entry records the rule it got.
-For each kernel the largest launch (max fetch) is reported."""
+For each kernel the largest launch (max fetch) is reported, and under "by_grid" the largest
+launch of each launch shape (grid size in work-items): bench.py keys its traffic by the shape
+of the launch it times when it knows it."""
 import collections
 import csv
 import glob
@@ -20,16 +22,21 @@ import sys
 
 
 def load(root, counter):
+    """{kernel name: [(grid size in work-items, counter value summed over the dispatch's
+    XCD / instance rows), ...]}, one entry per dispatch."""
     out = collections.defaultdict(list)
+    grid = {}
     for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"].split("(")[0]
-            out[(name, r.get("Dispatch_Id", ""))].append(float(r["Counter_Value"]))
+            key = (name, r.get("Dispatch_Id", ""))
+            out[key].append(float(r["Counter_Value"]))
+            grid[key] = int(float(r.get("Grid_Size", 0) or 0))
     per = collections.defaultdict(list)
-    for (name, _), v in out.items():
-        per[name].append(sum(v))  # sum over XCD/instance rows of one dispatch
+    for key, v in out.items():
+        per[key[0]].append((grid[key], sum(v)))
     return per
 
 
@@ -53,16 +60,25 @@ def main():
     for name, fv in fetch.items():
         if "rocclr" in name or "at::native" in name:
             continue
-        wv = write.get(name, [0.0])
-        f_kb, w_kb = max(fv), max(wv)
+        wv = write.get(name, [(0, 0.0)])
         rule = rule_of(name)
+        k = 2 if rule == "x2-fetch-16B" else 1
+        f_kb, w_kb = max(v for _, v in fv), max(v for _, v in wv)
+        # per launch shape (grid size in work-items): the largest launch of each, so a bench
+        # roofline can take the entry of ITS launch rather than the kernel name's largest
+        shapes = {}
+        for g in sorted({g for g, _ in fv}):
+            fg = max(v for gg, v in fv if gg == g)
+            wg = max((v for gg, v in wv if gg == g), default=0.0)
+            shapes[str(g)] = {"launches": sum(1 for gg, _ in fv if gg == g),
+                              "hbm_bytes_per_launch": int(k * fg * 1024 + wg * 1024)}
         kernels[name] = {
             "launches": len(fv),
             "fetch_size_kb_largest": f_kb,
             "write_size_kb_largest": w_kb,
             "rule": rule,
-            "hbm_bytes_per_launch_largest": int((2 if rule == "x2-fetch-16B" else 1) * f_kb * 1024
-                                                + w_kb * 1024),
+            "hbm_bytes_per_launch_largest": int(k * f_kb * 1024 + w_kb * 1024),
+            "by_grid": shapes,
         }
     json.dump({"source": [fetch_root, write_root], "per_gpu_batch": batch,
                "correction": "bytes = k * FETCH_SIZE[KB] * 1024 + WRITE_SIZE[KB] * 1024, k = 2 for "

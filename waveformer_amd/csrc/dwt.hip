@@ -223,6 +223,9 @@ __global__ __launch_bounds__(256) void idwt3d_haar_kernel(IdwtArgs a) {
 // levels (L > 1) are re-read by the 8^l descendants of a coefficient; they are 1/8 of the
 // level below and hit L2.
 // ---------------------------------------------------------------------------------------
+// CAT: the fused torch.cat with the skip (wf_idwt3d_haar_cl_cat) -- a separate instantiation
+// so counter passes and kernel traces tell the two launch kinds apart
+template <bool CAT>
 __global__ __launch_bounds__(256) void idwt3d_haar_cl4_kernel(IdwtArgs a, int64_t total) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= total) return;
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(256) void idwt3d_haar_cl4_kernel(IdwtArgs a, int64_
   }
   const int Wo = 2 * w1, Ho = 2 * h1;
   float* ob = a.out + b * a.out_bstride + c;
-  if (a.skip) {  // torch.cat((out, skip), 1): the same 4 channels of the skip, C further
+  if (CAT) {  // torch.cat((out, skip), 1): the same 4 channels of the skip, C further
     const float* sb = a.skip + b * a.skip_bstride + c;
     f32x4 sk[8];
 #pragma unroll
@@ -492,8 +495,12 @@ static int idwt_launch(const float* ll, int64_t ll_bstride, int64_t ll_cs, int64
   }
   if (vec && cl && ll_cs == 1 && ll_ps % 4 == 0 && ll_bstride % 4 == 0 && al16(ll) && ldo % 4 == 0) {
     const int64_t total = B * d1 * h1 * w1 * (C / 4);
-    hipLaunchKernelGGL(idwt3d_haar_cl4_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
-                       (hipStream_t)stream, a, total);
+    if (skip)
+      hipLaunchKernelGGL(idwt3d_haar_cl4_kernel<true>, dim3((unsigned)cdiv(total, 256)),
+                         dim3(256), 0, (hipStream_t)stream, a, total);
+    else
+      hipLaunchKernelGGL(idwt3d_haar_cl4_kernel<false>, dim3((unsigned)cdiv(total, 256)),
+                         dim3(256), 0, (hipStream_t)stream, a, total);
     return check_launch("wf_idwt3d_haar_cl");
   }
   if (vec && !cl && ll_ps == 1 && (2 * w1) % 4 == 0) {

@@ -4,7 +4,9 @@ Mirrors network_models/idwt_upsample.py (HFRefinementRes :12-50, UnetrIDWTBlock 
 same constructor and state_dict keys.  HFRefinementRes runs as one fused HIP call per level
 at inference (ops.hf_refine; PyTorch modules under autograd).  The wavelet synthesis (ptwt.waverec3, :160) and the
 concatenation with the skip (:163) run as one wf_idwt3d_haar launch that writes straight into
-the first half of the concatenated buffer; the surrounding convolutions are PyTorch/MIOpen.
+the first half of the concatenated buffer (with the skip in the same kernel,
+wf_idwt3d_haar_cl_cat); the surrounding convolutions run on the HIP conv3d_k3 kernel and the
+fused InstanceNorm + LeakyReLU passes (blocks.py).
 """
 from __future__ import annotations
 

@@ -3,8 +3,10 @@
 Mirrors network_models/network_backbone.py (ProjectionHead :35-63, ChannelCalibration :66-128,
 Waveformer :131-407, create_waveformer :410-431): same constructor signatures and the same 232
 state_dict keys at the default configuration, so reference checkpoints load with strict=True.
-The encoder and the IDWT synthesis run on the waveformer_amd HIP kernels; the MONAI-style
-decoder convolutions, ChannelCalibration and ProjectionUpsample are PyTorch (MIOpen) modules.
+The encoder and the IDWT synthesis run on the waveformer_amd HIP kernels; so do the MONAI-style
+decoder blocks, ChannelCalibration and ProjectionUpsample (3^3 convolutions on conv3d_k3,
+InstanceNorm + LeakyReLU fused, 1x1 / transposed convolutions on the in-house MFMA GEMMs;
+blocks.py) -- no MIOpen convolution on any path.
 """
 from __future__ import annotations
 

@@ -68,7 +68,9 @@ class DropPath(nn.Module):
 class ProjectionUpsample(nn.Module):
     """Decoder upsampler (wave_helper.py:33-81): trilinear x`stride` (align_corners=True, Q6) +
     depthwise 3^3 conv, GroupNorm(C, C), 1x1 conv C->2C + GELU, 1x1 projection (double conv
-    with GELU for large reductions), plus an upsampled 1x1-conv residual.  PyTorch/MIOpen."""
+    with GELU for large reductions), plus an upsampled 1x1-conv residual.  Inference: HIP
+    kernels (upsample_cl, dwconv3d, GroupNorm folded into the 1x1 GEMMs); training: the
+    autograd Functions of autograd.py."""
 
     def __init__(self, in_channels, out_channels, stride=2, residual=True, use_double_conv=False):
         super().__init__()

@@ -153,7 +153,9 @@ class WeightArena:
     Stream safety: the forward that used the arena last records an event on its stream when
     its scope closes; a refresh issued on another stream waits for that event first, so a
     forward on stream B never rewrites planes that stream A's kernels still read (graph
-    capture skips the event: a captured graph replays on its own stream, in order)."""
+    capture skips the event: a captured graph replays on its own stream, in order).  Arenas
+    are per thread (weight_scope), so this ordering is only ever between one thread's
+    successive forwards."""
 
     def __init__(self, params: Sequence[torch.Tensor], f16: bool = False):
         dev = params[0].device
@@ -203,6 +205,7 @@ class _Scope:
 
 
 _tls = threading.local()  # the open weight_scope of THIS thread (two threads: two scopes)
+_arena_lock = threading.Lock()
 
 
 def _cur_scope() -> Optional[_Scope]:
@@ -245,14 +248,19 @@ class weight_scope:
             # forward, else bf16 hi / lo (training always runs fp32-faithful bf16x3)
             train = torch.is_grad_enabled() and any(p.requires_grad for p in params)
             f16 = get_precision() == "fp16" and not train
-            arenas = getattr(self.module, "_wf_arenas", None)
-            if arenas is None:
-                arenas = {}
-                object.__setattr__(self.module, "_wf_arenas", arenas)
-            arena = arenas.get(f16)
-            if arena is None or arena.key != tuple((p.data_ptr(), p.numel()) for p in params):
-                arena = WeightArena(params, f16)
-                arenas[f16] = arena
+            # one arena per (operand format, thread): two threads running forwards of one
+            # model on their own streams never share planes or the done / done_stream pair
+            # (ADVICE r3 #3); the dict itself is guarded by a lock
+            with _arena_lock:
+                arenas = getattr(self.module, "_wf_arenas", None)
+                if arenas is None:
+                    arenas = {}
+                    object.__setattr__(self.module, "_wf_arenas", arenas)
+                akey = (f16, threading.get_ident())
+                arena = arenas.get(akey)
+                if arena is None or arena.key != tuple((p.data_ptr(), p.numel()) for p in params):
+                    arena = WeightArena(params, f16)
+                    arenas[akey] = arena
             arena.refresh()
         _tls.scope = _Scope(arena)
         self.owner = True
