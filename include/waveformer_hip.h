@@ -511,6 +511,15 @@ int wf_window_attention_bwd_core(const float* qkv, const float* o, const float* 
                                  int64_t W1, int64_t ws, int64_t heads, float scale,
                                  void* stream);
 
+/* c[n][k] (+)= sum_m a[m][n] * b[m][k] -- dW = dY^T X of the training path's Linear / 1x1
+ * conv / transposed-conv weights (ABI 14).  a (M, >= N) and b (M, >= K) fp32 row-major, lda /
+ * ldb floats apart; c (N, K), ldc apart (accumulate = 1 adds to it).  fp32-faithful bf16x3
+ * MFMAs, M dealt to many workgroups whose partials (workspace:
+ * wf_gemm_tn_workspace_bytes(M, N, K) bytes) are summed in a fixed order: deterministic.    */
+int64_t wf_gemm_tn_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int wf_gemm_tn(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
+               int accumulate, void* workspace, int64_t M, int64_t N, int64_t K, void* stream);
+
 /* dtable[r][h] = sum of dbias[h][i][j] over index[i][j] == r (the gather at
  * attention.py:94-97, adjoint), in ascending flat order: `perm` (N*N) lists the flat positions
  * i*N + j grouped by table row (a stable sort of the index), `offsets` (table_rows + 1) delimits

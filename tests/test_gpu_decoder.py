@@ -209,6 +209,61 @@ def test_conv3d_k3_autograd(cin, cout, S):
     assert C.rel_l2(bg.grad, bc.grad) <= 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,pad", [(100000, 192, 48, 0), (4097, 48, 32, 8),
+                                       (3000, 384, 96, 0), (777, 20, 70, 4), (64, 1536, 384, 0),
+                                       (33, 5, 3, 0)])
+def test_gemm_tn_vs_fp64(M, N, K, pad):
+    """wf_gemm_tn (the training path's weight gradients dW = dY^T X, ABI 14): bf16x3 MFMAs over
+    M rows dealt to many workgroups, partials summed in a fixed order -- against the fp64
+    product, rel-L2 <= 1e-5; strided rows (lda > N), ragged N / K / M; accumulate mode; two
+    calls bitwise equal (deterministic).  Bar 1e-5: the split's 2^-17 product rounding is the
+    same relative error whatever M (random-sign terms: measured 4.4e-6 at M = 10^5)."""
+    from waveformer_amd import ops
+    a = seeded_randn((M, N + pad), 40)[:, :N].cuda()
+    b = seeded_randn((M, K), 41).cuda()
+    want = a.double().t().mm(b.double())
+    got = ops.gemm_tn(a, b)
+    assert C.rel_l2(got, want) <= 1e-5
+    assert torch.equal(got, ops.gemm_tn(a, b))
+    acc = torch.ones((N, K), device="cuda")
+    ops.gemm_tn(a, b, out=acc, accumulate=True)
+    assert C.rel_l2(acc, want + 1) <= 1e-5
+
+
+@pytest.mark.parametrize("cin,cout,S,bias", [(96, 48, (6, 5, 7), True), (48, 4, (8, 8, 8), True),
+                                             (384, 192, (4, 4, 4), False)])
+def test_conv1x1_and_convtranspose2_autograd(cin, cout, S, bias):
+    """The decoder's 1x1 convs (wfa.Conv1x1Fn) and 2^3 transposed convs (wfa.ConvT2Fn) in
+    training: fp32 GEMM forward / input gradient, weight gradient on wf_gemm_tn, bias by column
+    sums -- against fp64 CPU autograd: rel-L2 <= 2e-6 for the fp32 GEMMs' output / input
+    gradient, <= 1e-5 for the bf16x3 weight gradient."""
+    from waveformer_amd import autograd as wfa
+    x = seeded_randn((2, cin) + S, 50)
+    conv = torch.nn.Conv3d(cin, cout, 1, bias=bias)
+    convt = torch.nn.ConvTranspose3d(cin, cout, 2, stride=2, bias=bias)
+    for m, seed in ((conv, 51), (convt, 52)):
+        with torch.no_grad():
+            for prm in m.parameters():
+                prm.copy_(seeded_randn(tuple(prm.shape), seed) * 0.1)
+        md = m.double()
+        xd = x.double().requires_grad_(True)
+        yd = md(xd)
+        g = seeded_randn(tuple(yd.shape), seed + 10)
+        yd.backward(g.double())
+        mc = type(m)(*([cin, cout, 1] if m is conv else [cin, cout, 2]),
+                     **({} if m is conv else {"stride": 2}), bias=bias).cuda()
+        mc.load_state_dict({k: v.float() for k, v in md.state_dict().items()})
+        xg = x.cuda().requires_grad_(True)
+        y = wfa.conv_train(mc, xg)
+        y.backward(g.cuda())
+        assert C.rel_l2(y, yd.detach()) <= 2e-6
+        assert C.rel_l2(xg.grad, xd.grad) <= 2e-6
+        assert C.rel_l2(mc.weight.grad, md.weight.grad) <= 1e-5
+        if bias:
+            assert C.rel_l2(mc.bias.grad, md.bias.grad) <= 2e-6
+        m.float()
+
+
 @pytest.mark.parametrize("C_,B,S,sig", [
     (48, 2, (12, 12, 12), True),    # decoder2 level shapes (C 48)
     (96, 1, (6, 7, 9), True),       # ragged planes / rows, z not a multiple of the 8-plane tile

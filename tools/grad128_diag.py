@@ -54,6 +54,11 @@ def main():
     ap.add_argument("--no-oracle", action="store_true")
     ap.add_argument("--runs", type=int, default=2)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--round-weights", action="store_true",
+                    help="also run the fp64 oracle with every weight rounded to a bf16 hi + lo "
+                         "pair (16 mantissa bits): the gradients' sensitivity to bf16x3 operands")
+    ap.add_argument("--round-scope", default="all", choices=["all", "encoder", "decoder"],
+                    help="which weights --round-weights rounds")
     args = ap.parse_args()
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
@@ -86,6 +91,25 @@ def main():
             if v.is_floating_point() and v.grad is not None:
                 o64[k] = v.grad.detach().cpu()
         o64 = {k: (summ(v), v.numel(), v) for k, v in o64.items()}
+    o64r = None
+    if not args.no_oracle and args.round_weights:
+        def r16(t):
+            hi = t.float().to(torch.bfloat16).float()
+            lo = (t.float() - hi).to(torch.bfloat16).float()
+            return (hi.double() + lo.double())
+        def pick(k):
+            enc = k.startswith("waveformer_encoder.")
+            return args.round_scope == "all" or (enc == (args.round_scope == "encoder"))
+        sdr = {k: ((r16(v) if pick(k) else v.double()).cuda().requires_grad_(True)
+                   if v.is_floating_point() else v.cuda()) for k, v in sd.items()}
+        xr = x0.double().clone().requires_grad_(True)
+        C.grad_loss(C.flat_outputs(case.oracle(sdr, xr))).backward()
+        torch.cuda.synchronize()
+        o64r = {"x": xr.grad.detach().cpu()}
+        for k, v in sdr.items():
+            if v.is_floating_point() and v.grad is not None:
+                o64r[k] = v.grad.detach().cpu()
+        o64r = {k: (summ(v), v.numel(), v) for k, v in o64r.items()}
     rows = []
     norms = {k: float(w[1]) ** 0.5 for k, w in want.items()}
     floor = 1e-5 * max(norms.values())
@@ -104,6 +128,8 @@ def main():
             row["P1_O64"] = err(s1, so, n)
             row["G_O64"] = err(w, so, n)
             row["P1_O64_rel_l2"] = C.rel_l2(t1, to)
+        if o64r is not None:
+            row["O64r_O64"] = err(o64r[k][0], o64[k][0], n)
         rows.append(row)
     # input-gradient strided sample
     samp_g = torch.from_numpy(fx["x__sample"])
@@ -114,8 +140,9 @@ def main():
         xs["O64_G"] = C.rel_l2(o64["x"][2].reshape(-1)[::stride][:4096].float(), samp_g)
         xs["P1_O64"] = C.rel_l2(runs[0][1]["x"][2], o64["x"][2])
     cols = [c for c in ("P1_G", "P2_G", "P1_P2", "P1_P2_rel_l2", "P1_O64", "G_O64",
-                        "P1_O64_rel_l2") if c in rows[0]]
-    rows.sort(key=lambda r: -r["P1_G"])
+                        "P1_O64_rel_l2", "O64r_O64") if c in rows[0]]
+    key = "P1_O64" if "P1_O64" in rows[0] else "P1_G"
+    rows.sort(key=lambda r: -r[key])
     print(f"{'tensor':66s} " + " ".join(f"{c:>13s}" for c in cols))
     for r in rows[:30]:
         print(f"{r['tensor'][:66]:66s} " + " ".join(f"{r[c]:13.3e}" for c in cols))

@@ -105,6 +105,8 @@ SIGNATURES = {
     "wf_window_attention_bwd_core": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64,
                                           _I64, _I64, _I64, _I64, _F, _P]),
     "wf_rel_pos_bias_bwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P]),
+    "wf_gemm_tn_workspace_bytes": (_I64, [_I64, _I64, _I64]),
+    "wf_gemm_tn": (_I, [_P, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _I64, _I64, _P]),
     "wf_colsum_parts": (_I64, [_I64]),
     "wf_colsum": (_I, [_P, _I64, _I64, _P, _I64, _P, _P, _P]),
     "wf_ln_act_fwd": (_I, [_P, _P, _P, _F, _I, _P, _I64, _I64, _P]),

@@ -13,6 +13,7 @@ workspaces the backward consumes are fp32 in that mode.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -135,7 +136,7 @@ class PatchEmbedFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             rows = torch.empty((M, Cin * 8), dtype=torch.float32, device=x.device)
             _lib.call("wf_patchify", x.data_ptr(), rows.data_ptr(), 0, B, Cin, D, H, W, _s())
-            dw = g.t().mm(rows).view_as(w)
+            dw = ops.gemm_tn(g, rows).view_as(w)
         if b is not None and ctx.needs_input_grad[2]:
             db = colsum(g)
         if ctx.needs_input_grad[0]:
@@ -288,6 +289,9 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
     return ops.to_cl(x).permute(0, 2, 3, 4, 1)
 
 
+_TORCH_CONV = os.environ.get("WF_TRAIN_TORCH_CONV") == "1"
+
+
 def conv_train(conv: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
     """A decoder Conv3d / ConvTranspose3d on the waveformer_amd paths (autograd-aware):
     3^3 dense (Conv3dK3), 3^3 depthwise (DWConv3dK3), 1^3 (F.linear over channel-last rows),
@@ -295,6 +299,10 @@ def conv_train(conv: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
     F = torch.nn.functional
     nn = torch.nn
     ok = x.is_cuda and x.dtype == torch.float32 and x.dim() == 5
+    if _TORCH_CONV and type(conv) is nn.Conv3d and conv.kernel_size == (3, 3, 3):
+        # diagnostics only (tools/grad128_diag.py): the 3^3 convs on the framework's fp32
+        # convolution, to attribute the gradient error of the bf16x3 kernels
+        return conv(x.contiguous())
     if ok and type(conv) is nn.Conv3d and conv.padding_mode == "zeros" \
             and conv.dilation == (1, 1, 1) and conv.stride == (1, 1, 1):
         Cin, Cout = conv.in_channels, conv.out_channels
@@ -304,21 +312,83 @@ def conv_train(conv: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
             if conv.groups == Cin == Cout and Cin % 4 == 0:
                 return DWConv3dK3.apply(x, conv.weight, conv.bias)
         if conv.kernel_size == (1, 1, 1) and conv.padding == (0, 0, 0) and conv.groups == 1:
-            y = F.linear(_rows(x), conv.weight.view(Cout, Cin), conv.bias)
-            return y.permute(0, 4, 1, 2, 3)
+            return Conv1x1Fn.apply(x, conv.weight, conv.bias)
     if ok and type(conv) is nn.ConvTranspose3d and conv.kernel_size == (2, 2, 2) \
             and conv.stride == (2, 2, 2) and conv.padding == (0, 0, 0) \
             and conv.output_padding == (0, 0, 0) and conv.groups == 1 \
             and conv.dilation == (1, 1, 1):
-        B, Cin, d, h, w = x.shape
-        Cout = conv.out_channels
-        wr = conv.weight.permute(0, 2, 3, 4, 1).reshape(Cin, 8 * Cout)
-        y = (_rows(x).reshape(-1, Cin) @ wr).view(B, d, h, w, 2, 2, 2, Cout)
-        y = y.permute(0, 1, 4, 2, 5, 3, 6, 7).reshape(B, 2 * d, 2 * h, 2 * w, Cout)
-        if conv.bias is not None:
-            y = y + conv.bias
-        return y.permute(0, 4, 1, 2, 3)
+        return ConvT2Fn.apply(x, conv.weight, conv.bias)
     return conv(x)
+
+
+class Conv1x1Fn(torch.autograd.Function):
+    """Conv3d(k=1) over channel-last position rows: y = x W^T + b (fp32 GEMM), dx = dy W (fp32
+    GEMM), dW = dy^T x on wf_gemm_tn (the platform BLAS put this long-K shape on a handful of
+    workgroups: 1.8-8 ms per call at 128^3), db = column sums (deterministic)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        B, Cin, D, H, W = x.shape
+        Cout = w.shape[0]
+        rows = _rows(x).reshape(-1, Cin)
+        w2 = w.view(Cout, Cin)
+        y = torch.addmm(b, rows, w2.t()) if b is not None else rows.mm(w2.t())
+        ctx.save_for_backward(rows, w)
+        ctx.has_bias, ctx.shape = b is not None, (B, D, H, W)
+        return y.view(B, D, H, W, Cout).permute(0, 4, 1, 2, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        rows, w = ctx.saved_tensors
+        B, D, H, W = ctx.shape
+        Cout, Cin = w.shape[0], w.shape[1]
+        gr = _rows(g).reshape(-1, Cout)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gr.mm(w.view(Cout, Cin)).view(B, D, H, W, Cin).permute(0, 4, 1, 2, 3)
+        if ctx.needs_input_grad[1]:
+            dw = ops.gemm_tn(gr, rows).view_as(w)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = colsum(gr)
+        return dx, dw, db
+
+
+class ConvT2Fn(torch.autograd.Function):
+    """ConvTranspose3d(k=2, s=2) (unetr_block.py:73-80) as one GEMM into the 8 sub-voxels:
+    y[2z+dz, 2y+dy, 2x+dx] = x W[:, :, dz, dy, dx] + b.  Backward: the sub-voxel gradient rows
+    (M, 8 Cout), dx = rows . Wr^T (fp32 GEMM), dW = x^T rows on wf_gemm_tn, db = column sums."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        B, Cin, d, h, ww = x.shape
+        Cout = w.shape[1]
+        rows = _rows(x).reshape(-1, Cin)
+        wr = w.permute(0, 2, 3, 4, 1).reshape(Cin, 8 * Cout)
+        y = (rows @ wr).view(B, d, h, ww, 2, 2, 2, Cout)
+        y = y.permute(0, 1, 4, 2, 5, 3, 6, 7).reshape(B, 2 * d, 2 * h, 2 * ww, Cout)
+        if b is not None:
+            y = y + b
+        ctx.save_for_backward(rows, w)
+        ctx.has_bias, ctx.shape = b is not None, (B, d, h, ww)
+        return y.permute(0, 4, 1, 2, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        rows, w = ctx.saved_tensors
+        B, d, h, ww = ctx.shape
+        Cin, Cout = w.shape[0], w.shape[1]
+        gcl = _rows(g)                                            # (B, 2d, 2h, 2w, Cout)
+        gsub = gcl.reshape(B, d, 2, h, 2, ww, 2, Cout).permute(0, 1, 3, 5, 2, 4, 6, 7)
+        gsub = gsub.reshape(-1, 8 * Cout)                         # rows (b, z, y, x) x (s, c)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wr = w.permute(0, 2, 3, 4, 1).reshape(Cin, 8 * Cout)
+            dx = gsub.mm(wr.t()).view(B, d, h, ww, Cin).permute(0, 4, 1, 2, 3)
+        if ctx.needs_input_grad[1]:
+            dw = ops.gemm_tn(rows, gsub).view(Cin, 2, 2, 2, Cout).permute(0, 4, 1, 2, 3)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = colsum(gcl.reshape(-1, Cout))
+        return dx, dw, db
 
 
 # ------------------------------------------------------------------------------------------

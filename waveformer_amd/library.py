@@ -23,6 +23,7 @@ outputs are empty and the backward raises.  Arithmetic precision is an explicit 
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -243,6 +244,17 @@ def _attn_setup(ctx, inputs, output):
     ctx.save_for_backward(x, ln_w, ln_b, wqkv, bqkv, table, index, wproj, bproj, work, lse)
 
 
+_BLAS_WGRAD = os.environ.get("WF_TRAIN_BLAS_WGRAD") == "1"
+
+
+def _wgrad(dy: Tensor, x: Tensor) -> Tensor:
+    """dW = dy^T x over the position rows: wf_gemm_tn (bf16x3 MFMAs, deterministic split over
+    the rows); WF_TRAIN_BLAS_WGRAD=1 keeps the platform BLAS's fp32 GEMM (A/B only)."""
+    if _BLAS_WGRAD:
+        return dy.t().mm(x)
+    return ops.gemm_tn(dy, x)
+
+
 def _index_groups(index: Tensor, rows: int) -> Tuple[Tensor, Tensor]:
     """The relative-position index (attention.py:40-56) grouped by table row for the
     deterministic bias-table gather (wf_rel_pos_bias_bwd): `perm` = the flat positions in a
@@ -279,7 +291,7 @@ def window_attn_backward(gout: Tensor, x: Tensor, ln_w: Optional[Tensor],
     o = work[qkv_bytes:qkv_bytes + rows * C * 4].view(torch.float32).view(rows, C)
     g = _f32(gout).view(rows, C)
     # proj: out = o Wp^T + bp (rows in window-major order == the Q1 raster order)
-    dwproj = g.t().mm(o)
+    dwproj = _wgrad(g, o)
     dbproj = colsum(g) if bproj is not None else E()
     do = g.mm(wproj)
     dqkv = torch.empty((rows, 3 * C), dtype=torch.float32, device=x.device)
@@ -296,7 +308,7 @@ def window_attn_backward(gout: Tensor, x: Tensor, ln_w: Optional[Tensor],
     # qkv = xin Wqkv^T + bqkv with xin = norm1?(x) in raster order (dqkv is raster-ordered)
     x2 = x.view(rows, C)
     xin = ln_fwd(x2, ln_w, ln_b, eps, False) if ln_w is not None else x2
-    dwqkv = dqkv.t().mm(xin)
+    dwqkv = _wgrad(dqkv, xin)
     dbqkv = colsum(dqkv) if bqkv is not None else E()
     dxin = dqkv.mm(wqkv)
     dlnw, dlnb = E(), E()
@@ -479,7 +491,7 @@ def ccf_ffn_backward(gout: Tensor, xh: Tensor, n2w: Optional[Tensor], n2b: Optio
     df = _scale_rows(g.view(B, -1), s_mlp).view(M, C) if block else g
     # fc: f = u2 Wfc^T + bfc, u2 = GELU(LN2(h2))
     u2 = ln_fwd(h2, l2w, l2b, eps2, True)
-    dfcw = df.t().mm(u2)
+    dfcw = _wgrad(df, u2)
     dfcb = colsum(df) if fcb is not None else E()
     du2 = df.mm(fcw)
     del u2
@@ -503,7 +515,7 @@ def ccf_ffn_backward(gout: Tensor, xh: Tensor, n2w: Optional[Tensor], n2b: Optio
     h1 = torch.addmm(pwb, n2, wpw.t()) if pwb is not None else n2.mm(wpw.t())
     dh1, dl1w, dl1b = ln_bwd(h1, l1w, l1b, eps1, True, du1)
     del h1, du1
-    dpww = dh1.t().mm(n2).view_as(pww)
+    dpww = _wgrad(dh1, n2).view_as(pww)
     dpwb = colsum(dh1) if pwb is not None else E()
     dn2 = dh1.mm(wpw)
     dn2w, dn2b = E(), E()
@@ -581,7 +593,7 @@ def patch_merging_backward(gout: Tensor, x: Tensor, nw: Tensor, nb: Tensor, red:
               _s())
     z = ln_fwd(merged, nw, nb, eps, False)
     g = _f32(gout).view(M, 2 * C)
-    dred = g.t().mm(z)
+    dred = _wgrad(g, z)
     del z
     dz = g.mm(red)
     dm, dnw, dnb = ln_bwd(merged, nw, nb, eps, False, dz)

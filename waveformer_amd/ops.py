@@ -977,6 +977,29 @@ def conv3d_k3_wgrad(x: torch.Tensor, dy: torch.Tensor, wshape) -> torch.Tensor:
     return dw
 
 
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+            accumulate: bool = False) -> torch.Tensor:
+    """a^T b for row matrices a (M, N), b (M, K) (unit column stride, any row stride): the
+    weight gradient dW = dY^T X of a Linear over M positions (wf_gemm_tn: bf16x3 MFMAs,
+    deterministic split over M).  Returns (N, K) fp32, or adds into / writes `out`."""
+    if a.dim() != 2 or b.dim() != 2 or a.shape[0] != b.shape[0]:
+        raise ValueError(f"gemm_tn: a {tuple(a.shape)} and b {tuple(b.shape)} do not match")
+    a = a if a.stride(1) == 1 and a.dtype == torch.float32 else a.float().contiguous()
+    b = b if b.stride(1) == 1 and b.dtype == torch.float32 else b.float().contiguous()
+    M, N = a.shape
+    K = b.shape[1]
+    if out is None:
+        out = torch.empty((N, K), dtype=torch.float32, device=a.device)
+        accumulate = False
+    if tuple(out.shape) != (N, K) or out.stride(1) != 1:
+        raise ValueError("gemm_tn: out must be an (N, K) row matrix")
+    ws = torch.empty(max(1, _lib.query("wf_gemm_tn_workspace_bytes", M, N, K)),
+                     dtype=torch.uint8, device=a.device)
+    _lib.call("wf_gemm_tn", a.data_ptr(), max(a.stride(0), N), b.data_ptr(), max(b.stride(0), K),
+              out.data_ptr(), out.stride(0), int(accumulate), ws.data_ptr(), M, N, K, _stream())
+    return out
+
+
 def linear_rows(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
                 gelu_in: bool = False, cache: bool = True, prec: Optional[int] = None,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
