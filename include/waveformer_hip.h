@@ -575,9 +575,10 @@ int wf_interp_adjoint_axis(const float* in, float* out, int64_t outer, int64_t L
  * gradient).  C % 4 == 0.                                                                  */
 int wf_dwconv3d_cl(const float* in, const float* w, const float* bias, int flip, float* out,
                    int64_t B, int64_t C, int64_t D, int64_t H, int64_t W, void* stream);
-/* dw (C, 27) = sum over positions of dy[pos][c] x[pos + offset_k][c].
- * partials: wf_dwconv_wgrad_ws_floats(B*D*H*W, C) floats.                                  */
-int64_t wf_dwconv_wgrad_ws_floats(int64_t positions, int64_t C);
+/* dw (C, 27) = sum over positions of dy[pos][c] x[pos + offset_k][c]: z-streaming LDS-tiled
+ * for C % 32 == 0 (ABI 14), per-tile partials summed in a fixed order (deterministic).
+ * partials: wf_dwconv_wgrad_ws_floats(B, C, D, H, W) floats.                                */
+int64_t wf_dwconv_wgrad_ws_floats(int64_t B, int64_t C, int64_t D, int64_t H, int64_t W);
 int wf_dwconv3d_wgrad(const float* dy, const float* x, float* partials, float* dw, int64_t B,
                       int64_t C, int64_t D, int64_t H, int64_t W, void* stream);
 

@@ -264,6 +264,36 @@ def test_conv1x1_and_convtranspose2_autograd(cin, cout, S, bias):
         m.float()
 
 
+@pytest.mark.parametrize("C_,B,S", [(192, 2, (9, 20, 17)), (32, 1, (3, 5, 40)), (96, 1, (12, 9, 8)),
+                                    (48, 2, (5, 6, 7)), (64, 1, (1, 1, 1))])
+def test_dwconv3d_autograd(C_, B, S):
+    """Depthwise 3^3 conv in training (wfa.DWConv3dK3: ProjectionUpsample.conv1, CCF_FFN.dwconv
+    backward): forward and input gradient on the z-streaming LDS kernel (the gradient with the
+    taps mirrored, round 5), weight gradient on the z-streaming partial-tile kernel summed in a
+    fixed order (C % 32 == 0; the per-position kernels otherwise, C = 48 here) -- against fp64
+    CPU autograd, rel-L2 <= 2e-6 (exact fp32 arithmetic); the weight gradient bitwise
+    repeatable; ragged tiles, a single-position volume."""
+    from waveformer_amd import autograd as wfa
+    x = seeded_randn((B, C_) + S, 60)
+    w = seeded_randn((C_, 1, 3, 3, 3), 61) * 0.3
+    b = seeded_randn((C_,), 62)
+    g = seeded_randn((B, C_) + S, 63)
+    xd, wd, bd = (t.double().requires_grad_(True) for t in (x, w, b))
+    yd = F.conv3d(xd, wd, bd, padding=1, groups=C_)
+    yd.backward(g.double())
+    xg, wg, bg = (t.cuda().requires_grad_(True) for t in (x, w, b))
+    y = wfa.DWConv3dK3.apply(xg, wg, bg)
+    y.backward(g.cuda())
+    assert C.rel_l2(y, yd.detach()) <= 2e-6
+    assert C.rel_l2(xg.grad, xd.grad) <= 2e-6
+    assert C.rel_l2(wg.grad, wd.grad) <= 2e-6
+    assert C.rel_l2(bg.grad, bd.grad) <= 2e-6
+    w1 = wg.grad.clone()
+    wg.grad = None
+    wfa.DWConv3dK3.apply(xg, wg, bg).backward(g.cuda())
+    assert torch.equal(wg.grad, w1)
+
+
 @pytest.mark.parametrize("C_,B,S,sig", [
     (48, 2, (12, 12, 12), True),    # decoder2 level shapes (C 48)
     (96, 1, (6, 7, 9), True),       # ragged planes / rows, z not a multiple of the 8-plane tile

@@ -1,3 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_ddp.py tests/test_gpu_grad128.py tests/test_train_grads.py -s > gpurun_out/g5f_pytest.txt 2>&1; rc=$?; grep -E "grad128:|DDP vs|PASS|FAIL|passed|failed" gpurun_out/g5f_pytest.txt | tail -20; exit $rc
+T=${1:-g5g}
+timeout -k 10 500 python -u -m pytest -x -q --timeout 400 --timeout-method thread tests/test_gpu_decoder.py tests/test_gpu_ddp.py tests/test_gpu_grad128.py -m gpu -s > gpurun_out/${T}_pytest.txt 2>&1; rc=$?; grep -E "grad128:|DDP vs|passed|failed|Error" gpurun_out/${T}_pytest.txt | tail -8; [ $rc -le 1 ] || exit $rc
+tools/gpu_r5.sh $T train

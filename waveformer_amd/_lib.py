@@ -118,7 +118,7 @@ SIGNATURES = {
     "wf_interp_adjoint_axis": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _I64, _P]),
     "wf_interp_adjoint_axis_ac": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P]),
     "wf_dwconv3d_cl": (_I, [_P, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _P]),
-    "wf_dwconv_wgrad_ws_floats": (_I64, [_I64, _I64]),
+    "wf_dwconv_wgrad_ws_floats": (_I64, [_I64] * 5),
     "wf_dwconv3d_wgrad": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_patch_merging_gather": (_I, [_P, _I, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_patch_merging_scatter": (_I, [_P, _I, _P, _I64, _I64, _I64, _I64, _I64, _P]),

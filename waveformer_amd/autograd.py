@@ -273,7 +273,7 @@ class DWConv3dK3(torch.autograd.Function):
             _lib.call("wf_dwconv3d_cl", g.data_ptr(), _f32(w.detach()).data_ptr(), None, 1,
                       dx.data_ptr(), B, C, D, H, W, _s())
         if ctx.needs_input_grad[1]:
-            part = torch.empty(_lib.query("wf_dwconv_wgrad_ws_floats", B * D * H * W, C),
+            part = torch.empty(_lib.query("wf_dwconv_wgrad_ws_floats", B, C, D, H, W),
                                dtype=torch.float32, device=g.device)
             dw = torch.empty(C * 27, dtype=torch.float32, device=g.device)
             _lib.call("wf_dwconv3d_wgrad", g.data_ptr(), xc.data_ptr(), part.data_ptr(),

@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
     const T* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias,
     T* __restrict__ out, float* __restrict__ pstats, int B, int Hd, int D, int H, int W, int ZS,
     double* __restrict__ cstats, const float* __restrict__ ln1_stats,
-    const float* __restrict__ ln1_w, const float* __restrict__ ln1_b) {
+    const float* __restrict__ ln1_w, const float* __restrict__ ln1_b, int flip) {
   static_assert(!LN1 || sizeof(T) == 4, "LN1 staging: fp32 h1");
   constexpr int CH = DW_CH, TX = DW_TX, TY = DW_TY;
   static_assert(CH == DW_STAT_GROUP, "one statistics group per workgroup channel chunk");
@@ -266,11 +266,14 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
   const int tid = threadIdx.x;
   const int cp = tid % (CH / 2), xi = tid / (CH / 2);
 
+  // flip: the taps mirrored (w[26 - k]) -- the input gradient of the same conv (training)
   f32x2 w2[27];
 #pragma unroll
-  for (int k = 0; k < 27; ++k)
-    w2[k] = f32x2{w[(c0 + 2 * cp) * 27 + k], w[(c0 + 2 * cp + 1) * 27 + k]};
-  const f32x2 bv = f32x2{bias[c0 + 2 * cp], bias[c0 + 2 * cp + 1]};
+  for (int k = 0; k < 27; ++k) {
+    const int kk = flip ? 26 - k : k;
+    w2[k] = f32x2{w[(c0 + 2 * cp) * 27 + kk], w[(c0 + 2 * cp + 1) * 27 + kk]};
+  }
+  const f32x2 bv = bias ? f32x2{bias[c0 + 2 * cp], bias[c0 + 2 * cp + 1]} : f32x2{0.f, 0.f};
 
   if (LN1) {
     for (int i = tid; i < CH; i += 256) {
@@ -418,7 +421,7 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
 
 int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, float* pstats,
                     int B, int Hd, int D, int H, int W, int prec, hipStream_t s, double* cstats,
-                    const float* ln1_stats, const float* ln1_w, const float* ln1_b) {
+                    const float* ln1_stats, const float* ln1_w, const float* ln1_b, int flip) {
   if (Hd % DW_CH != 0) return fail(WF_E_SHAPE, "dwconv3d: hidden width must be a multiple of 32");
   // z segment: enough workgroups to fill 256 CUs ~8 deep, but long enough that the two halo
   // planes per segment stay a small overhead
@@ -431,16 +434,16 @@ int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, f
       return fail(WF_E_SHAPE, "dwconv3d: the LN1 staging needs fp32 h1 and LN1 weights");
     hipLaunchKernelGGL((dwconv3d_kernel<float, true>), dim3((unsigned)blocks), dim3(256), 0, s,
                        reinterpret_cast<const float*>(in), w, b, reinterpret_cast<float*>(out),
-                       pstats, B, Hd, D, H, W, ZS, cstats, ln1_stats, ln1_w, ln1_b);
+                       pstats, B, Hd, D, H, W, ZS, cstats, ln1_stats, ln1_w, ln1_b, flip);
   } else if (store32(prec))
     hipLaunchKernelGGL((dwconv3d_kernel<float, false>), dim3((unsigned)blocks), dim3(256), 0, s,
                        reinterpret_cast<const float*>(in), w, b, reinterpret_cast<float*>(out),
-                       pstats, B, Hd, D, H, W, ZS, cstats, nullptr, nullptr, nullptr);
+                       pstats, B, Hd, D, H, W, ZS, cstats, nullptr, nullptr, nullptr, flip);
   else
     hipLaunchKernelGGL((dwconv3d_kernel<uint16_t, false>), dim3((unsigned)blocks), dim3(256), 0,
                        s, reinterpret_cast<const uint16_t*>(in), w, b,
                        reinterpret_cast<uint16_t*>(out), pstats, B, Hd, D, H, W, ZS, cstats,
-                       nullptr, nullptr, nullptr);
+                       nullptr, nullptr, nullptr, flip);
   return check_launch("dwconv3d");
 }
 

@@ -129,7 +129,7 @@ int launch_dwconv_ln_gelu(const void* in, const float* w, const float* b, const 
 int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, float* pstats,
                     int B, int Hd, int D, int H, int W, int prec, hipStream_t s,
                     double* cstats = nullptr, const float* ln1_stats = nullptr,
-                    const float* ln1_w = nullptr, const float* ln1_b = nullptr);
+                    const float* ln1_w = nullptr, const float* ln1_b = nullptr, int flip = 0);
 // per-row {mean, rstd} from np equal-size {mean, M2} partials (Chan et al.), (M, 2)
 int launch_ln_stats_finalize(const float* pstats, int np, int group, float eps, float* out,
                              int64_t M, hipStream_t s);

@@ -51,14 +51,20 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restric
     part[(int64_t)blockIdx.x * N + c] = (red[0][tc] + red[1][tc]) + (red[2][tc] + red[3][tc]);
 }
 
+// one wave per column: lane l sums parts l, l + 64, ... in order, then a fixed xor tree over
+// the lanes (deterministic; the one-thread-per-column form ran a 1024-long dependent chain,
+// ~100 us per call, 47 calls per config-4 step)
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part,
                                                            int64_t P, int64_t N,
                                                            float* __restrict__ out) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (c >= N) return;
   float acc = 0.f;
-  for (int64_t p = 0; p < P; ++p) acc += part[p * N + c];
-  out[c] = acc;
+  for (int64_t p = lane; p < P; p += 64) acc += part[p * N + c];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) out[c] = acc;
 }
 
 int launch_colsum(const float* in, int64_t R, int64_t N, const float* rscale,
@@ -70,7 +76,7 @@ int launch_colsum(const float* in, int64_t R, int64_t N, const float* rscale,
   const int64_t rpp = cdiv(R, P);
   hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)P, (unsigned)cdiv(N, 64)), dim3(256), 0,
                      s, in, R, N, rpp, rscale, rows_per_scale > 0 ? rows_per_scale : R, part);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, s, part,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)cdiv(N, 4)), dim3(256), 0, s, part,
                      P, N, out);
   return check_launch("colsum");
 }
@@ -561,18 +567,24 @@ __global__ __launch_bounds__(256) void attn_db_reduce_kernel(const float* __rest
 // dbias[h][i][j] -- the adjoint of the gather at attention.py:94-97 without atomics: `perm`
 // lists the flat positions grouped by table row (a stable sort of the index), `offsets` (T + 1)
 // delimits each row's group
+// (one wave per (row, head): lane l sums group entries l, l + 64, ... in order, then a fixed
+// xor tree -- deterministic, and 64 gathers in flight per row instead of one dependent chain)
 __global__ __launch_bounds__(256) void rel_pos_bias_bwd_kernel(const float* __restrict__ dbias,
                                                                const int64_t* __restrict__ perm,
                                                                const int64_t* __restrict__ offsets,
                                                                float* __restrict__ dtable,
                                                                int64_t NN, int heads, int64_t T) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (i >= T * heads) return;
   const int64_t r = i / heads;
   const int h = (int)(i - r * heads);
+  const float* db = dbias + (int64_t)h * NN;
   float s = 0.f;
-  for (int64_t k = offsets[r]; k < offsets[r + 1]; ++k) s += dbias[(int64_t)h * NN + perm[k]];
-  dtable[i] = s;
+  for (int64_t k = offsets[r] + lane; k < offsets[r + 1]; k += 64) s += db[perm[k]];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) dtable[i] = s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1071,7 +1083,7 @@ extern "C" int wf_rel_pos_bias_bwd(const float* dbias, const int64_t* perm,
   WF_REQUIRE_PTR(dtable);
   WF_REQUIRE(heads >= 1 && table_rows >= 1, "empty table");
   const int64_t n = table_rows * heads;
-  hipLaunchKernelGGL(rel_pos_bias_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(rel_pos_bias_bwd_kernel, dim3((unsigned)cdiv(n, 4)), dim3(256), 0,
                      (hipStream_t)stream, dbias, perm, offsets, dtable, N * N, (int)heads,
                      table_rows);
   return check_launch("wf_rel_pos_bias_bwd");
@@ -1110,11 +1122,13 @@ extern "C" int wf_dwconv3d_cl(const float* in, const float* w, const float* bias
   WF_REQUIRE_PTR(in);
   WF_REQUIRE_PTR(w);
   WF_REQUIRE_PTR(out);
-  // the forward orientation with a bias and 32-channel groups: the z-streaming LDS-tiled
-  // kernel of CCF_FFN (ffn.hip); the flipped (input-gradient) form keeps the simple one
-  if (!flip && bias && C % 32 == 0)
+  // 32-channel groups: the z-streaming LDS-tiled kernel of CCF_FFN (ffn.hip), forward or
+  // flipped (the input gradient: 1.0x the forward's time instead of the per-output 27-load
+  // kernel below, 4.1 ms per 64^3 x 192 launch at B = 4)
+  if (C % 32 == 0)
     return launch_dwconv3d(in, w, bias, out, nullptr, (int)B, (int)C, (int)D, (int)H, (int)W,
-                           PREC_SPLIT, (hipStream_t)stream);
+                           PREC_SPLIT, (hipStream_t)stream, nullptr, nullptr, nullptr, nullptr,
+                           flip);
   const int64_t n = B * D * H * W * (C / 4);
   hipLaunchKernelGGL(dwconv_cl_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, in, w,
                      bias, flip, out, (int)B, (int)C, (int)D, (int)H, (int)W);
@@ -1137,6 +1151,175 @@ extern "C" int wf_dwconv3d_stats_cl(const float* in, const float* w, const float
                          PREC_SPLIT, s, stats_acc);
 }
 
+namespace wf {
+// ------------------------------------------------------------------------------------------
+// depthwise 3^3 weight gradient, z-streaming: dw[c][k] = sum_p dy[p][c] x[p + off_k][c]
+// A workgroup = (32 channels, one 8 x 16 tile of a z segment), 256 threads = 16 columns x 16
+// channel pairs (the tiling of dwconv3d_kernel, ffn.hip).  The haloed x plane q (10 x 18
+// positions x 32 channels) is staged in LDS once (double buffered, next plane in flight); it
+// meets the output gradients of planes q + 1 (kz = 0), q (kz = 1) and q - 1 (kz = 2), which
+// ride in registers (three rolling sets of the thread's 8 rows).  Each thread accumulates the
+// 27 taps of its channel pair over its positions; the 16 columns are then combined in a fixed
+// order (two xor steps inside the wave, the 4 waves through LDS) and each workgroup writes one
+// partial (27 x 32 floats); a column-sum kernel adds the partials in order.  Replaces the
+// per-position kernel below (27 global 16-B loads per position: 5.2 ms per 64^3 x 192 call).
+constexpr int DWG_CH = 32, DWG_TX = 16, DWG_TY = 8, DWG_PY = DWG_TY + 2, DWG_PX = DWG_TX + 2;
+constexpr int DWG_NV = DWG_CH / 4;                                 // f32x4 per position
+constexpr int DWG_NLD = (DWG_PY * DWG_PX * DWG_NV + 255) / 256;
+
+struct DwgArgs {
+  const float* dy;
+  const float* x;
+  float* part;  // (tiles, C * 27): tile-major, [c][k] inside
+  int B, C, D, H, W, ZS;
+};
+
+__global__ __launch_bounds__(256) void dwconv_wgrad_z_kernel(DwgArgs a) {
+  __shared__ __attribute__((aligned(16))) float pl[2][DWG_PY * DWG_PX * DWG_CH];
+  const int C = a.C, D = a.D, H = a.H, W = a.W;
+  const int ncc = C / DWG_CH, ntx = (W + DWG_TX - 1) / DWG_TX, nty = (H + DWG_TY - 1) / DWG_TY;
+  const int nzs = (D + a.ZS - 1) / a.ZS;
+  int t = blockIdx.x;
+  const int cc = t % ncc;
+  t /= ncc;
+  const int tile = t;  // partial index (spatial tile incl. z segment and sample)
+  const int xt = t % ntx;
+  t /= ntx;
+  const int yt = t % nty;
+  t /= nty;
+  const int zt = t % nzs;
+  const int b = t / nzs;
+  const int x0 = xt * DWG_TX, y0 = yt * DWG_TY, z0 = zt * a.ZS, z1 = min(z0 + a.ZS, D);
+  const int c0 = cc * DWG_CH;
+  const int tid = threadIdx.x;
+  const int cp = tid % (DWG_CH / 2), xi = tid / (DWG_CH / 2);
+  const int xo = x0 + xi;
+  const int64_t sb = (int64_t)b * D * H * W;
+  const float* xs = a.x + sb * C + c0;
+  const float* gs = a.dy + sb * C + c0 + 2 * cp;
+
+  f32x4 stg[DWG_NLD];
+  auto fetch = [&](int p) {
+    const bool pz = p >= 0 && p < D;
+    const int pc = min(max(p, 0), D - 1);
+#pragma unroll
+    for (int j = 0; j < DWG_NLD; ++j) {
+      const int i = min(j * 256 + tid, DWG_PY * DWG_PX * DWG_NV - 1);
+      const int pos = i / DWG_NV, v = i - pos * DWG_NV;
+      const int yy = y0 - 1 + pos / DWG_PX, xx = x0 - 1 + pos % DWG_PX;
+      const bool ok = pz && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const int yc = min(max(yy, 0), H - 1), xc = min(max(xx, 0), W - 1);
+      const f32x4 u = *reinterpret_cast<const f32x4*>(
+          xs + (((int64_t)pc * H + yc) * W + xc) * C + 4 * v);
+      stg[j] = ok ? u : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < DWG_NLD; ++j) {
+      const int i = j * 256 + tid;
+      if (i < DWG_PY * DWG_PX * DWG_NV) *reinterpret_cast<f32x4*>(pl[buf] + (size_t)i * 4) = stg[j];
+    }
+  };
+  // the output gradient rows of plane z (zero outside the segment / volume)
+  auto gload = [&](int z, f32x2 (&g)[DWG_TY]) {
+    const bool zv = z >= z0 && z < z1 && xo < W;
+    const int zc = min(max(z, 0), D - 1), xc = min(xo, W - 1);
+#pragma unroll
+    for (int o = 0; o < DWG_TY; ++o) {
+      const int yo = y0 + o;
+      const f32x2 u = *reinterpret_cast<const f32x2*>(
+          gs + (((int64_t)zc * H + min(yo, H - 1)) * W + xc) * C);
+      g[o] = (zv && yo < H) ? u : f32x2{0.f, 0.f};
+    }
+  };
+
+  f32x2 acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = f32x2{0.f, 0.f};
+  // plane q meets dy of q + 1 (gC, kz = 0), q (gB, kz = 1), q - 1 (gA, kz = 2)
+  f32x2 gA[DWG_TY], gB[DWG_TY], gC[DWG_TY], gN[DWG_TY];
+  gload(z0 - 2, gA);  // zeros
+  gload(z0 - 1, gB);  // zeros
+  gload(z0, gC);
+  fetch(z0 - 1);
+  commit(0);
+  __syncthreads();
+  int buf = 0;
+  for (int q = z0 - 1; q <= z1; ++q) {
+    fetch(q + 1);     // next x plane in flight
+    gload(q + 2, gN); // and the dy rows the next plane needs
+    const float* P = pl[buf] + xi * DWG_CH + 2 * cp;
+#pragma unroll
+    for (int r = 0; r < DWG_PY; ++r) {
+      const f32x2 v0 = *reinterpret_cast<const f32x2*>(P + (r * DWG_PX + 0) * DWG_CH);
+      const f32x2 v1 = *reinterpret_cast<const f32x2*>(P + (r * DWG_PX + 1) * DWG_CH);
+      const f32x2 v2 = *reinterpret_cast<const f32x2*>(P + (r * DWG_PX + 2) * DWG_CH);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int o = r - ky;  // output row fed by input row r through tap ky
+        if (o < 0 || o >= DWG_TY) continue;
+        acc[ky * 3 + 0] += gC[o] * v0;
+        acc[ky * 3 + 1] += gC[o] * v1;
+        acc[ky * 3 + 2] += gC[o] * v2;
+        acc[9 + ky * 3 + 0] += gB[o] * v0;
+        acc[9 + ky * 3 + 1] += gB[o] * v1;
+        acc[9 + ky * 3 + 2] += gB[o] * v2;
+        acc[18 + ky * 3 + 0] += gA[o] * v0;
+        acc[18 + ky * 3 + 1] += gA[o] * v1;
+        acc[18 + ky * 3 + 2] += gA[o] * v2;
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < DWG_TY; ++o) {
+      gA[o] = gB[o];
+      gB[o] = gC[o];
+      gC[o] = gN[o];
+    }
+    commit(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // the 16 columns of a channel pair: lanes cp, cp + 16, cp + 32, cp + 48 of each wave (two
+  // xor steps), then the 4 waves in order through LDS
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+    acc[k].x += __shfl_xor(acc[k].x, 16, 64);
+    acc[k].y += __shfl_xor(acc[k].y, 16, 64);
+    acc[k].x += __shfl_xor(acc[k].x, 32, 64);
+    acc[k].y += __shfl_xor(acc[k].y, 32, 64);
+  }
+  float* red = pl[0];  // [4 waves][27][32 channels]
+  const int wv = tid >> 6, lane = tid & 63;
+  if (lane < 16) {
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      red[(wv * 27 + k) * DWG_CH + 2 * lane] = acc[k].x;
+      red[(wv * 27 + k) * DWG_CH + 2 * lane + 1] = acc[k].y;
+    }
+  }
+  __syncthreads();
+  float* dst = a.part + (int64_t)tile * C * 27;
+  for (int i = tid; i < 27 * DWG_CH; i += 256) {
+    const int k = i / DWG_CH, c = i - k * DWG_CH;
+    const float v = (red[(0 * 27 + k) * DWG_CH + c] + red[(1 * 27 + k) * DWG_CH + c]) +
+                    (red[(2 * 27 + k) * DWG_CH + c] + red[(3 * 27 + k) * DWG_CH + c]);
+    dst[(c0 + c) * 27 + k] = v;
+  }
+}
+
+// z segment length of the z-streaming weight gradient: ~2048 workgroups
+int dwg_zs(int64_t B, int64_t C, int64_t D, int64_t H, int64_t W) {
+  const int64_t base = B * (C / DWG_CH) * cdiv(H, DWG_TY) * cdiv(W, DWG_TX);
+  int ZS = (int)D;
+  while (ZS > 4 && base * cdiv(D, ZS) < 2048) ZS = (ZS + 1) / 2;
+  return ZS;
+}
+int64_t dwg_tiles(int64_t B, int64_t D, int64_t H, int64_t W, int ZS) {
+  return B * cdiv(D, ZS) * cdiv(H, DWG_TY) * cdiv(W, DWG_TX);
+}
+}  // namespace wf
+
 static int64_t wf_dwconv_wgrad_parts(int64_t positions) {
   int64_t p = cdiv(positions, 512);
   return p > 512 ? 512 : (p < 1 ? 1 : p);
@@ -1151,6 +1334,17 @@ extern "C" int wf_dwconv3d_wgrad(const float* dy, const float* x, float* partial
   WF_REQUIRE_PTR(partials);
   WF_REQUIRE_PTR(dw);
   hipStream_t s = (hipStream_t)stream;
+  if (C % DWG_CH == 0 && B * D * H * W * C < ((int64_t)1 << 40)) {
+    DwgArgs g{dy, x, partials, (int)B, (int)C, (int)D, (int)H, (int)W, dwg_zs(B, C, D, H, W)};
+    const int64_t tiles = dwg_tiles(B, D, H, W, g.ZS);
+    WF_REQUIRE(tiles * (C / DWG_CH) < ((int64_t)1 << 31), "too many tiles");
+    hipLaunchKernelGGL(dwconv_wgrad_z_kernel, dim3((unsigned)(tiles * (C / DWG_CH))), dim3(256),
+                       0, s, g);
+    int rc = check_launch("wf_dwconv3d_wgrad");
+    if (rc) return rc;
+    float* tmp = partials + tiles * C * 27;
+    return launch_colsum(partials, tiles, C * 27, nullptr, 0, tmp, dw, s);
+  }
   const int64_t P = B * D * H * W;
   const int64_t parts = wf_dwconv_wgrad_parts(P);
   const int64_t ppb = cdiv(P, parts);
@@ -1163,8 +1357,10 @@ extern "C" int wf_dwconv3d_wgrad(const float* dy, const float* x, float* partial
   return launch_colsum(partials, parts, C * 27, nullptr, 0, tmp, dw, s);
 }
 
-extern "C" int64_t wf_dwconv_wgrad_ws_floats(int64_t positions, int64_t C) {
-  const int64_t parts = wf_dwconv_wgrad_parts(positions);
+extern "C" int64_t wf_dwconv_wgrad_ws_floats(int64_t B, int64_t C, int64_t D, int64_t H,
+                                             int64_t W) {
+  int64_t parts = wf_dwconv_wgrad_parts(B * D * H * W);
+  if (C % DWG_CH == 0) parts = std::max(parts, dwg_tiles(B, D, H, W, dwg_zs(B, C, D, H, W)));
   return parts * C * 27 + colsum_parts(parts) * C * 27;
 }
 

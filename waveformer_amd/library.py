@@ -499,7 +499,8 @@ def ccf_ffn_backward(gout: Tensor, xh: Tensor, n2w: Optional[Tensor], n2b: Optio
     del du2
     # depthwise conv: h2 = dw(u1) + bdw
     ddwb = colsum(dh2)
-    part = torch.empty(_lib.query("wf_dwconv_wgrad_ws_floats", M, hid), dtype=torch.float32,
+    part = torch.empty(_lib.query("wf_dwconv_wgrad_ws_floats", B, hid, D, H, W),
+                       dtype=torch.float32,
                        device=xh.device)
     ddww = torch.empty(hid * 27, dtype=torch.float32, device=xh.device)
     _lib.call("wf_dwconv3d_wgrad", dh2.data_ptr(), u1.data_ptr(), part.data_ptr(),
