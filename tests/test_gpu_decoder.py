@@ -264,6 +264,34 @@ def test_conv1x1_and_convtranspose2_autograd(cin, cout, S, bias):
         m.float()
 
 
+@pytest.mark.parametrize("C_,B,S", [(192, 2, (9, 10, 17)), (96, 1, (16, 16, 16)), (8, 3, (2, 3, 5))])
+def test_group_norm_cl_autograd(C_, B, S):
+    """ProjectionUpsample.norm (GroupNorm(C, C), affine) in training on the channel-last path
+    (wfa.GroupNormCLFn: HIP statistics, one-pass affine apply, the norm_act backward with
+    slope 1): output, input / weight / bias gradients against fp64 CPU autograd, rel-L2 1e-5."""
+    from waveformer_amd import autograd as wfa
+    x = seeded_randn((B, C_) + S, 70) * 2 + 0.5
+    norm = torch.nn.GroupNorm(C_, C_)
+    with torch.no_grad():
+        norm.weight.copy_(seeded_randn((C_,), 71))
+        norm.bias.copy_(seeded_randn((C_,), 72))
+    g = seeded_randn((B, C_) + S, 73)
+    nd = torch.nn.GroupNorm(C_, C_).double()
+    nd.load_state_dict({k: v.double() for k, v in norm.state_dict().items()})
+    xd = x.double().requires_grad_(True)
+    yd = nd(xd)
+    yd.backward(g.double())
+    ng = norm.cuda()
+    xg = x.cuda().contiguous(memory_format=torch.channels_last_3d).requires_grad_(True)
+    y = wfa.group_norm_cl(ng, xg)
+    assert y.is_contiguous(memory_format=torch.channels_last_3d)
+    y.backward(g.cuda())
+    assert C.rel_l2(y, yd.detach()) <= 1e-5
+    assert C.rel_l2(xg.grad, xd.grad) <= 1e-5
+    assert C.rel_l2(ng.weight.grad, nd.weight.grad) <= 1e-5
+    assert C.rel_l2(ng.bias.grad, nd.bias.grad) <= 1e-5
+
+
 @pytest.mark.parametrize("C_,B,S", [(192, 2, (9, 20, 17)), (32, 1, (3, 5, 40)), (96, 1, (12, 9, 8)),
                                     (48, 2, (5, 6, 7)), (64, 1, (1, 1, 1))])
 def test_dwconv3d_autograd(C_, B, S):

@@ -431,6 +431,54 @@ class NormActFn(torch.autograd.Function):
         return da, dr, None, None, None, None
 
 
+class GroupNormCLFn(torch.autograd.Function):
+    """GroupNorm(C, C) with affine (ProjectionUpsample.norm, wave_helper.py:65) on a
+    channel-last tensor in training: per-(sample, channel) statistics on wf_instnorm_stats_cl
+    (fp64 sums), y = x * (rstd gamma) + (beta - mean rstd gamma) in one pass that keeps the
+    layout; backward = wf_norm_act_bwd_cl of the non-affine normalisation (slope 1: no
+    activation) times gamma, whose per-(sample, channel) sums of dy and dy * xhat are the beta /
+    gamma gradients.  The framework's GroupNorm needs NCDHW: a layout copy before and after
+    each call and its two backward kernels (~12 ms per config-4 step at B = 4)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        x = ops.to_cl(x)
+        B, C = x.shape[:2]
+        st = ops.instnorm_stats(x, eps)                        # (B, 2, C) {mean, rstd}
+        scale = st[:, 1] * w                                   # (B, C)
+        shift = b - st[:, 0] * scale
+        y = ops.empty_cl(*x.shape, x.device)
+        torch.addcmul(shift.view(B, C, 1, 1, 1), x, scale.view(B, C, 1, 1, 1), out=y)
+        ctx.save_for_backward(x, w, st)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, st = ctx.saved_tensors
+        g = ops.to_cl(g)
+        B, C, D, H, W = x.shape
+        da = ops.empty_cl(B, C, D, H, W, x.device)
+        ws = torch.empty(_lib.query("wf_norm_act_bwd_workspace_bytes", B, C), dtype=torch.uint8,
+                         device=x.device)
+        _lib.call("wf_norm_act_bwd_cl", g.data_ptr(), ops.cl_ld(g), g.data_ptr(), ops.cl_ld(g),
+                  x.data_ptr(), ops.cl_ld(x), st.data_ptr(), None, 0, None, da.data_ptr(), C,
+                  None, 0, B, C, D * H * W, 1.0, ws.data_ptr(), _s())
+        sums = ws.view(torch.float64).view(B, C, 3).sum(0)     # {sum dy, sum dy*xhat, -}
+        da.mul_(w.view(1, C, 1, 1, 1))
+        dw = sums[:, 1].float() if ctx.needs_input_grad[1] else None
+        db = sums[:, 0].float() if ctx.needs_input_grad[2] else None
+        return da, dw, db, None
+
+
+def group_norm_cl(norm: torch.nn.GroupNorm, x: torch.Tensor) -> torch.Tensor:
+    """norm(x) for a per-channel affine GroupNorm on the channel-last path (training)."""
+    if (norm.num_groups == norm.num_channels and norm.affine and x.is_cuda
+            and x.dtype == torch.float32 and x.dim() == 5 and x.shape[1] % 4 == 0
+            and x.shape[1] <= 1024):
+        return GroupNormCLFn.apply(x, norm.weight, norm.bias, float(norm.eps))
+    return norm(x)
+
+
 def norm_act(a, r=None, slope=0.01, eps=1e-5, eps_r=1e-5, normed_residual=False):
     mode = 0 if r is None else (2 if normed_residual else 1)
     return NormActFn.apply(a, r, float(slope), float(eps), float(eps_r), mode)

@@ -117,7 +117,8 @@ class ProjectionUpsample(nn.Module):
             # and gradients)
             size = tuple(s * self.stride for s in x.shape[2:])
             cv = wfa.conv_train
-            y = cv(self.conv2, self.norm(cv(self.conv1[1], wfa.upsample_cl(x, size))))
+            y = cv(self.conv2, wfa.group_norm_cl(self.norm,
+                                                 cv(self.conv1[1], wfa.upsample_cl(x, size))))
             y = self.act(y)
             if self.use_double_conv:
                 y = cv(self.conv3[2], self.conv3[1](cv(self.conv3[0], y)))
