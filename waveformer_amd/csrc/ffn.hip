@@ -228,12 +228,12 @@ struct Store2<uint16_t> {
 // the plane staging -- ln1_stats (M, 2) {mean, rstd} per position, ln1_w / ln1_b (Hd) -- so
 // the separate LayerNorm + GELU pass over h1 (read + write of the whole tensor) is gone
 // (stages 3 / 4 of the encoder); halo positions outside the volume stay zero.
-template <typename T, bool LN1>
+template <typename T, bool LN1, bool FLIP = false>
 __global__ __launch_bounds__(256) void dwconv3d_kernel(
     const T* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias,
     T* __restrict__ out, float* __restrict__ pstats, int B, int Hd, int D, int H, int W, int ZS,
     double* __restrict__ cstats, const float* __restrict__ ln1_stats,
-    const float* __restrict__ ln1_w, const float* __restrict__ ln1_b, int flip) {
+    const float* __restrict__ ln1_w, const float* __restrict__ ln1_b) {
   static_assert(!LN1 || sizeof(T) == 4, "LN1 staging: fp32 h1");
   constexpr int CH = DW_CH, TX = DW_TX, TY = DW_TY;
   static_assert(CH == DW_STAT_GROUP, "one statistics group per workgroup channel chunk");
@@ -266,11 +266,11 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
   const int tid = threadIdx.x;
   const int cp = tid % (CH / 2), xi = tid / (CH / 2);
 
-  // flip: the taps mirrored (w[26 - k]) -- the input gradient of the same conv (training)
+  // FLIP: the taps mirrored (w[26 - k]) -- the input gradient of the same conv (training)
   f32x2 w2[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) {
-    const int kk = flip ? 26 - k : k;
+    const int kk = FLIP ? 26 - k : k;
     w2[k] = f32x2{w[(c0 + 2 * cp) * 27 + kk], w[(c0 + 2 * cp + 1) * 27 + kk]};
   }
   const f32x2 bv = bias ? f32x2{bias[c0 + 2 * cp], bias[c0 + 2 * cp + 1]} : f32x2{0.f, 0.f};
@@ -423,6 +423,8 @@ int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, f
                     int B, int Hd, int D, int H, int W, int prec, hipStream_t s, double* cstats,
                     const float* ln1_stats, const float* ln1_w, const float* ln1_b, int flip) {
   if (Hd % DW_CH != 0) return fail(WF_E_SHAPE, "dwconv3d: hidden width must be a multiple of 32");
+  if (flip && (ln1_stats || !store32(prec)))
+    return fail(WF_E_SHAPE, "dwconv3d: the mirrored taps are for fp32 data without LN1 staging");
   // z segment: enough workgroups to fill 256 CUs ~8 deep, but long enough that the two halo
   // planes per segment stay a small overhead
   const int64_t base = (int64_t)B * (Hd / DW_CH) * cdiv(H, DW_TY) * cdiv(W, DW_TX);
@@ -434,16 +436,21 @@ int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, f
       return fail(WF_E_SHAPE, "dwconv3d: the LN1 staging needs fp32 h1 and LN1 weights");
     hipLaunchKernelGGL((dwconv3d_kernel<float, true>), dim3((unsigned)blocks), dim3(256), 0, s,
                        reinterpret_cast<const float*>(in), w, b, reinterpret_cast<float*>(out),
-                       pstats, B, Hd, D, H, W, ZS, cstats, ln1_stats, ln1_w, ln1_b, flip);
-  } else if (store32(prec))
+                       pstats, B, Hd, D, H, W, ZS, cstats, ln1_stats, ln1_w, ln1_b);
+  } else if (store32(prec) && flip)
+    hipLaunchKernelGGL((dwconv3d_kernel<float, false, true>), dim3((unsigned)blocks), dim3(256),
+                       0, s, reinterpret_cast<const float*>(in), w, b,
+                       reinterpret_cast<float*>(out), pstats, B, Hd, D, H, W, ZS, cstats,
+                       nullptr, nullptr, nullptr);
+  else if (store32(prec))
     hipLaunchKernelGGL((dwconv3d_kernel<float, false>), dim3((unsigned)blocks), dim3(256), 0, s,
                        reinterpret_cast<const float*>(in), w, b, reinterpret_cast<float*>(out),
-                       pstats, B, Hd, D, H, W, ZS, cstats, nullptr, nullptr, nullptr, flip);
+                       pstats, B, Hd, D, H, W, ZS, cstats, nullptr, nullptr, nullptr);
   else
     hipLaunchKernelGGL((dwconv3d_kernel<uint16_t, false>), dim3((unsigned)blocks), dim3(256), 0,
                        s, reinterpret_cast<const uint16_t*>(in), w, b,
                        reinterpret_cast<uint16_t*>(out), pstats, B, Hd, D, H, W, ZS, cstats,
-                       nullptr, nullptr, nullptr, flip);
+                       nullptr, nullptr, nullptr);
   return check_launch("dwconv3d");
 }
 
@@ -601,9 +608,12 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   // row in one workgroup, which only the A-resident gemm_ares can hold -- it then re-streams
   // the full weight per 16 rows (measured 107 / 145 us per launch at B = 4).  Instead: the
   // K-chunked GEMM with a plain bias epilogue, then one in-place LayerNorm + GELU row pass.
+  // Round 5: gemm_lnw with 8 / 16-wave workgroups holds the whole 768 / 1536-wide row (the
+  // columns split over the waves), so the LayerNorm + GELU run in its epilogue and the
+  // separate pass is gone (WF_FFN_NO_LNW_WIDE=1: the round-4 split path, A/B)
   static const bool no_split_ln1 = getenv("WF_FFN_NO_SPLIT_LN1") != nullptr;
   const bool split_ln1 = !no_split_ln1 && store32(precision) && hidden >= 768 &&
-                         hidden <= 1536;
+                         hidden <= 1536 && !(g.a_map == MAP_IDENTITY && gemm_lnw_wide_shape(g));
   // C = 48 / hidden = 192 (stage 1), opt-in (WF_FFN_FUSED=1): the whole FFN in one kernel
   // (ffn_fused.hip), h1 and h2 stay on chip; stage 2 is that kernel, stages 1 and 3 are part
   // of it.  Off by default: recomputing the 4 x 8 tile's haloed h1 plane (1.875x the pw GEMM,

@@ -23,19 +23,24 @@
 namespace wf {
 
 
-// LW_NTW column tiles per wave (N = 64 LW_NTW), LW_RT row tiles of 16 rows per workgroup:
-// (6, 4) for N = 384 (stage 2).  (3, 8) for the stage-1 N = 192 measured slower than gemm_rows
-// (909 vs 974 volumes/s: K = 48 pads to two 32-wide K-steps and the A staging is exposed)
-template <int P, int KS, int LW_NTW, int LW_RT>
-__global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
-  constexpr int LW_N = 4 * LW_NTW * 16;
+// LW_NTW column tiles per wave (N = 16 NWV LW_NTW), LW_RT row tiles of 16 rows per
+// workgroup, NWV waves: (6, 4, 4) for N = 384 (stage 2).  (3, 8) for the stage-1 N = 192
+// measured slower than gemm_rows (909 vs 974 volumes/s: K = 48 pads to two 32-wide K-steps
+// and the A staging is exposed).  Round 5: the wide rows of stages 3 / 4 (N = 768 on 8 waves,
+// 1536 on 16) -- the whole row in one workgroup, so the LayerNorm + GELU epilogue replaces
+// the K-chunked GEMM + separate ln_act pass (a read and a write of h1)
+template <int NWV> struct LnwBounds { static constexpr int MINW = NWV == 4 ? 2 : 1; };
+template <int P, int KS, int LW_NTW, int LW_RT, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64, LnwBounds<NWV>::MINW) void gemm_lnw_kernel(GemmArgs g) {
+  constexpr int NTH = NWV * 64;
+  constexpr int LW_N = NWV * LW_NTW * 16;
   constexpr bool SPLIT = P == PREC_SPLIT;
   constexpr int NPL = SPLIT ? 2 : 1;
   constexpr int K32 = KS * 32;
   constexpr int AS = K32 + WF_LDS_KPAD;       // LDS row stride (bf16, gemm_common.hpp)
   constexpr int ROWS = LW_RT * 16;
   __shared__ __attribute__((aligned(16))) uint16_t As[NPL * ROWS * AS];
-  __shared__ float red[4][ROWS];
+  __shared__ float red[NWV][ROWS];
   const int K = g.K, N = LW_N;
   const int64_t M = g.M;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -56,7 +61,7 @@ __global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
   // ---- A: rows r0 .. r0 + 63, the n2 LayerNorm (LN_GIVEN) applied, split into LDS
   {
     constexpr int Q = K32 / 4;  // f32x4 per row (zero past K)
-    for (int i = tid; i < ROWS * Q; i += 256) {
+    for (int i = tid; i < ROWS * Q; i += NTH) {
       const int r = i / Q, q = i - r * Q;
       const int64_t row = min(r0 + r, M - 1);
       const int k = 4 * q;
@@ -147,10 +152,17 @@ __global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
     if (g4 == 0) red[wid][rt * 16 + l15] = s;
   }
   __syncthreads();
+  // the waves' partial sums of a row, added in a fixed order
+  auto wsum = [&](int r) {
+    float t = (red[0][r] + red[1][r]) + (red[2][r] + red[3][r]);
+#pragma unroll
+    for (int w = 4; w < NWV; w += 4) t += (red[w][r] + red[w + 1][r]) + (red[w + 2][r] + red[w + 3][r]);
+    return t;
+  };
 #pragma unroll
   for (int rt = 0; rt < LW_RT; ++rt) {
     const int r = rt * 16 + l15;
-    mean[rt] = ((red[0][r] + red[1][r]) + (red[2][r] + red[3][r])) * (1.f / LW_N);
+    mean[rt] = wsum(r) * (1.f / LW_N);
   }
   __syncthreads();  // every wave has read the sums
 #pragma unroll
@@ -169,8 +181,7 @@ __global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
 #pragma unroll
   for (int rt = 0; rt < LW_RT; ++rt) {
     const int r = rt * 16 + l15;
-    rstd[rt] = rsqrtf(((red[0][r] + red[1][r]) + (red[2][r] + red[3][r])) * (1.f / LW_N) +
-                      g.e_eps);
+    rstd[rt] = rsqrtf(wsum(r) * (1.f / LW_N) + g.e_eps);
   }
 #pragma unroll
   for (int t = 0; t < LW_NTW; ++t) {
@@ -196,13 +207,25 @@ __global__ __launch_bounds__(256, 2) void gemm_lnw_kernel(GemmArgs g) {
   }
 }
 
-template <int KS, int NTW, int RT>
+template <int KS, int NTW, int RT, int NWV = 4>
 void go_lnw(const GemmArgs& g, hipStream_t s) {
   const dim3 grid((unsigned)cdiv(g.M, RT * 16));
-  auto k = g.prec == PREC_SPLIT  ? gemm_lnw_kernel<PREC_SPLIT, KS, NTW, RT>
-           : g.prec == PREC_FP16 ? gemm_lnw_kernel<PREC_FP16, KS, NTW, RT>
-                                 : gemm_lnw_kernel<PREC_BF16, KS, NTW, RT>;
-  hipLaunchKernelGGL(k, grid, dim3(256), 0, s, g);
+  auto k = g.prec == PREC_SPLIT  ? gemm_lnw_kernel<PREC_SPLIT, KS, NTW, RT, NWV>
+           : g.prec == PREC_FP16 ? gemm_lnw_kernel<PREC_FP16, KS, NTW, RT, NWV>
+                                 : gemm_lnw_kernel<PREC_BF16, KS, NTW, RT, NWV>;
+  hipLaunchKernelGGL(k, grid, dim3(NWV * 64), 0, s, g);
+}
+
+// the wide-row shapes this kernel takes: the stage-3 pwconv N = 768 (K <= 192) -- 78.7 us
+// against 61.6 + 43.9 for gemm_kc + ln_act_fwd at B = 8 (profiles/r5_lnw_wide_ab.txt).  The
+// stage-4 N = 1536 on 16 waves measured 81.9 against 29.3 + 21.2 (256 workgroups of 16 rows
+// each streaming the 2.4 MB weight: latency-bound), so it stays on the split path unless
+// WF_LNW_WIDE1536=1
+bool gemm_lnw_wide_shape(const GemmArgs& g) {
+  static const bool off = getenv("WF_FFN_NO_LNW_WIDE") != nullptr;  // A/B switch
+  static const bool w1536 = getenv("WF_LNW_WIDE1536") != nullptr;
+  const int ks = (g.K + 31) / 32;
+  return !off && ((g.N == 768 && ks == 6) || (w1536 && g.N == 1536 && ks == 12));
 }
 
 int try_launch_gemm_lnw(const GemmArgs& g, hipStream_t s) {
@@ -212,7 +235,23 @@ int try_launch_gemm_lnw(const GemmArgs& g, hipStream_t s) {
       g.M >= ((int64_t)1 << 31) || g.ldo < g.N || g.ldo % 4 != 0)
     return 0;
   const int ks = (g.K + 31) / 32;
+  static const int wrt = getenv("WF_LNW_WIDE_RT") ? atoi(getenv("WF_LNW_WIDE_RT")) : 4;
+  if (gemm_lnw_wide_shape(g)) {
+    if (g.N == 768) {
+      if (wrt == 2) go_lnw<6, 6, 2, 8>(g, s);
+      else go_lnw<6, 6, 4, 8>(g, s);
+    } else {
+      go_lnw<12, 6, 1, 16>(g, s);
+    }
+    return 1;
+  }
   if (g.N == 384) {
+    // WF_LNW384: the stage-2 shape's (column tiles, row tiles, waves) -- 0: (6, 4, 4) (round
+    // 2, 200.2-201.1 us at B = 8), 1: (3, 4, 8) (196.0), 2 (default): (3, 8, 8), 128 rows per
+    // workgroup, the weight streamed once per 128 rows (194.5; profiles/r5_lnw_wide_ab.txt)
+    static const int v384 = getenv("WF_LNW384") ? atoi(getenv("WF_LNW384")) : 2;
+    if (ks == 3 && v384 == 1) { go_lnw<3, 3, 4, 8>(g, s); return 1; }
+    if (ks == 3 && v384 == 2) { go_lnw<3, 3, 8, 8>(g, s); return 1; }
     switch (ks) {
       case 1: go_lnw<1, 6, 4>(g, s); return 1;
       case 2: go_lnw<2, 6, 4>(g, s); return 1;

@@ -200,5 +200,7 @@ int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s);
 // stage-2 CCF_FFN pwconv (N = 384 with the LayerNorm + GELU epilogue, gemm_lnw.hip): columns
 // split over the waves; returns 1 if it took the shape
 int try_launch_gemm_lnw(const GemmArgs& g, hipStream_t s);
+// the stage-3/4 wide-row pwconv shapes gemm_lnw takes (LayerNorm + GELU epilogue)
+bool gemm_lnw_wide_shape(const GemmArgs& g);
 
 }  // namespace wf
