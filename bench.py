@@ -81,6 +81,9 @@ def parse():
                          "sharded over the ranks and all-gathered over RCCL; train: config 4, "
                          "fwd + DiceCE + bwd + clip + AdamW of the full Waveformer, DDP")
     ap.add_argument("--tta", type=int, default=0, help="sliding: 8-way flip TTA")
+    ap.add_argument("--exchange", default="allgather", choices=["allgather", "allreduce"],
+                    help="sliding: per-round all-gather of window logits + stitch on every rank,"
+                         " or each rank's partial stitch + one all-reduce (SURVEY 8e)")
     ap.add_argument("--miopen-find", type=int, default=0,
                     help="train: cudnn.benchmark (MIOpen find); no convolution of the step runs "
                          "on MIOpen any more (autograd.conv_train), so it only matters for "
@@ -389,7 +392,7 @@ def main_sliding(args, world, rank, dev):
     group = dist.group.WORLD if world > 1 else None
     inf = inferers.SlidingWindowInferer((128,) * 3, sw_batch_size=2, overlap=0.5,
                                         mode="gaussian", cache_roi_weight_map=True,
-                                        process_group=group)
+                                        process_group=group, exchange=args.exchange)
     axes = [0, 1, 2] if args.tta else None
 
     def step():
@@ -433,9 +436,11 @@ def main_sliding(args, world, rank, dev):
                     "random weights",
             "config": {"workload": "SlidingWindowInferer(roi 128^3, sw_batch 2, overlap 0.5, "
                                    "gaussian) over Waveformer 128^3x4, config 3",
-                       "windows": nwin, "tta": bool(axes),
-                       "parallelism": f"windows round-robin over {world} ranks + RCCL "
-                                      f"all-gather of window logits per round"},
+                       "windows": nwin, "tta": bool(axes), "exchange": args.exchange,
+                       "parallelism": f"windows round-robin over {world} ranks + " + (
+                           "RCCL all-gather of window logits per round" if args.exchange ==
+                           "allgather" else "each rank's partial stitch + one RCCL all-reduce "
+                                            "of the (C + 1) full-size planes")},
             "output_checksum": float(y.double().sum().item()),
         }
         rl = {}

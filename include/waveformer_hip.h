@@ -464,6 +464,22 @@ int wf_sliding_window_stitch(const float* patches, int64_t world, int64_t slots_
                              int64_t H, int64_t W, int64_t rd, int64_t rh, int64_t rw,
                              void* stream);
 
+/* The all-reduce exchange of the sharded sliding window (ABI 14): each rank sums
+ * only the windows it predicted -- g % world == rank, held in its local patch rows
+ * j = g / world: patches (slots, C, rd, rh, rw) -- in ascending window order, into
+ * out (B, C + 1, D, H, W): channels [0, C) = sum pred * w, channel C = sum w (no division).
+ * The ranks' outputs are then summed (one all-reduce of (C + 1) x D x H x W per image) and
+ * wf_sliding_window_normalize divides.  world = 1 gives, after normalising, bitwise the
+ * wf_sliding_window_stitch result.                                                          */
+int wf_sliding_window_stitch_partial(const float* patches, int64_t world, int64_t rank,
+                                     const float* importance_map, const int64_t* starts,
+                                     const int64_t* nwin, float* out, int64_t B, int64_t C,
+                                     int64_t D, int64_t H, int64_t W, int64_t rd, int64_t rh,
+                                     int64_t rw, void* stream);
+/* out (B, C, D, H, W) = num[:, :C] / num[:, C] for num (B, C + 1, D, H, W).                */
+int wf_sliding_window_normalize(const float* num, float* out, int64_t B, int64_t C, int64_t D,
+                                int64_t H, int64_t W, void* stream);
+
 /* Flip test-time augmentation merge of Predictor.maybe_mirror_and_predict
  * (light_training/prediction.py:110-160): out = (sum_p flip_p(pred[p])) / npass, summed in
  * pass order.  pred: (npass, C, D, H, W) fp32, pass p computed on the input flipped along the

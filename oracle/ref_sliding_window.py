@@ -126,6 +126,31 @@ def stitch(patches: Tensor, wmap: Tensor, starts: Sequence[Sequence[int]],
     return out
 
 
+def stitch_partial(patches: Tensor, wmap: Tensor, starts: Sequence[Sequence[int]],
+                   image_size: Sequence[int], batch: int, world: int, rank: int) -> Tensor:
+    """The same scatter restricted to one rank's windows (g % world == rank, local row
+    g // world): (batch, C + 1, *image) = [sum pred * w | sum w], no division -- the CPU
+    stand-in of wf_sliding_window_stitch_partial (the all-reduce exchange)."""
+    roi = tuple(patches.shape[2:])
+    slices = [(slice(z, z + roi[0]), slice(y, y + roi[1]), slice(x, x + roi[2]))
+              for z in starts[0] for y in starts[1] for x in starts[2]]
+    nwin = len(slices)
+    C = patches.shape[1]
+    out = torch.zeros((batch, C + 1) + tuple(image_size), dtype=torch.float)
+    w = wmap.reshape(roi).float().cpu()
+    p_all = patches.cpu()
+    for g in range(rank, batch * nwin, world):
+        b, s = g // nwin, slices[g % nwin]
+        out[(slice(b, b + 1), slice(0, C)) + s] += p_all[g // world] * w
+        out[(slice(b, b + 1), slice(C, C + 1)) + s] += w
+    return out
+
+
+def normalize(num: Tensor) -> Tensor:
+    C = num.shape[1] - 1
+    return num[:, :C] / num[:, C:]
+
+
 def tta_merge(pred: Tensor, passes) -> Tensor:
     """The merge half of mirror_and_predict over stacked per-pass predictions (pass p on the
     input flipped along tensor dims passes[p]) -- the wf_tta_merge contract."""

@@ -42,13 +42,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_config3_sharded_sliding_window_vs_reference(tmp_path):
+@pytest.mark.parametrize("exchange", ["allgather", "allreduce"])
+def test_config3_sharded_sliding_window_vs_reference(tmp_path, exchange):
+    """exchange: the per-round all-gather of window logits + stitch on every rank, or (SURVEY
+    8e's alternative) each rank's partial stitch + one all-reduce + divide."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     fx = np.load(FIX)
     world = 2
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
-               WORLD_SIZE=str(world), PYTHONPATH=REPO)
+               WORLD_SIZE=str(world), PYTHONPATH=REPO, WF_SW_EXCHANGE=exchange)
     procs = []
     for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r))

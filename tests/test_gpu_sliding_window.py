@@ -77,6 +77,35 @@ def test_stitch_bit_exact_vs_oracle(world, sb, B):
     assert torch.equal(got.cpu(), ref)
 
 
+@pytest.mark.parametrize("world,B", [(1, 1), (1, 2), (3, 1), (8, 2)])
+def test_stitch_partial_allreduce_vs_oracle(world, B):
+    """The all-reduce exchange (wf_sliding_window_stitch_partial + wf_sliding_window_normalize,
+    ABI 14): each rank's partial bit-exact against the oracle's partial; the rank partials
+    summed (what the all-reduce computes) and normalised against the all-gather stitch --
+    bitwise at one rank, rel-L2 <= 1e-6 when the sums meet in rank order."""
+    from waveformer_amd import inferers, ops
+    img, roi = (30, 26, 21), (12, 10, 9)
+    st = inferers.dense_patch_starts(img, roi, inferers.scan_interval(img, roi, (0.5,) * 3))
+    total = B * len(st[0]) * len(st[1]) * len(st[2])
+    slots = -(-total // world)
+    allp = seeded_randn((total, 3) + roi, 8)
+    wmap = RS.importance_map(roi, "gaussian", (0.125,) * 3)
+    acc = None
+    for r in range(world):
+        local = torch.zeros((slots, 3) + roi)
+        g = torch.arange(r, total, world)
+        local[:len(g)] = allp[g]
+        got = ops.sliding_window_stitch_partial(local.to(DEV), wmap.to(DEV), st, img, B, world, r)
+        assert torch.equal(got.cpu(), RS.stitch_partial(local, wmap, st, img, B, world, r))
+        acc = got if acc is None else acc + got
+    out = ops.sliding_window_normalize(acc)
+    ref = RS.stitch(allp, wmap, st, img, B)
+    if world == 1:
+        assert torch.equal(out.cpu(), ref)
+    else:
+        assert C.rel_l2(out, ref) <= 1e-6
+
+
 def test_stitch_rejects_bad_geometry():
     from waveformer_amd import ops
     p = torch.zeros((2, 1, 4, 4, 4), device=DEV)

@@ -75,16 +75,27 @@ def test_oracle_tta_matches_reference():
     assert torch.equal(y, _fx(name + "_y"))
 
 
-def _product(x, roi, sb, ov, mode, group=None):
+def _product(x, roi, sb, ov, mode, group=None, exchange="allgather"):
     return inferers.sliding_window_inference(x, roi, sb, toy_predictor, overlap=ov, mode=mode,
                                              process_group=group, stitch=RS.stitch,
-                                             weight_map_fn=_cpu_map)
+                                             weight_map_fn=_cpu_map, exchange=exchange,
+                                             partial_stitch=RS.stitch_partial,
+                                             normalize=RS.normalize)
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_host_logic_single_process(name):
     shape, seed, roi, sb, ov, mode = CASES[name]
     y = _product(seeded_randn(shape, seed), roi, sb, ov, mode)
+    assert torch.equal(y, _fx(name + "_y"))
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_host_logic_allreduce_single_process(name):
+    """The all-reduce exchange on one process: each window's weighted sum and weight in window
+    order, then one division -- bitwise the reference's accumulation."""
+    shape, seed, roi, sb, ov, mode = CASES[name]
+    y = _product(seeded_randn(shape, seed), roi, sb, ov, mode, exchange="allreduce")
     assert torch.equal(y, _fx(name + "_y"))
 
 
@@ -125,6 +136,11 @@ def _dist_worker(rank, world, port, names, q):
             shape, seed, roi, sb, ov, mode = CASES[name]
             y = _product(seeded_randn(shape, seed), roi, sb, ov, mode, dist.group.WORLD)
             res[name] = bool(torch.equal(y, _fx(name + "_y")))
+            # the all-reduce exchange: the ranks' partial sums meet in rank order
+            y2 = _product(seeded_randn(shape, seed), roi, sb, ov, mode, dist.group.WORLD,
+                          exchange="allreduce")
+            ref = _fx(name + "_y")
+            res[name + "_allreduce"] = bool(((y2 - ref).norm() / ref.norm()).item() <= 1e-6)
         # fewer windows than ranks (ranks without windows agree on C via all_reduce)
         x = seeded_randn((1, 1, 10, 10, 10), 5)
         y = _product(x, (10, 10, 10), 1, 0.5, "gaussian", dist.group.WORLD)

@@ -96,6 +96,9 @@ SIGNATURES = {
     "wf_sliding_window_stitch": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _I64,
                                       _I64, _I64, _I64, _I64, _P]),
     "wf_tta_merge": (_I, [_P, _P, _I, _P, _I64, _I64, _I64, _I64, _P]),
+    "wf_sliding_window_stitch_partial": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64,
+                                              _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_sliding_window_normalize": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     # training (config 4)
     "wf_window_attention_fwd_train": (_I, [_P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _P,
                                            _I64, _I64, _I64, _I64, _I64, _I64, _I64, _F, _I,

@@ -12,6 +12,8 @@
 // reference's order (product and sum rounded separately, no FMA) with no atomics and one
 // write per output element.  The patches may come from an RCCL all-gather of round-robin
 // shards (see wf_sliding_window_stitch in include/waveformer_hip.h for the row mapping).
+#include <algorithm>
+
 #include "wf_common.hpp"
 
 namespace wf {
@@ -26,6 +28,7 @@ struct StitchArgs {
   int rd, rh, rw;
   int n[3];              // windows per axis (z, y, x)
   int world, sb;         // row mapping of the gathered shards
+  int rank;              // PARTIAL: this rank's windows only (g % world == rank), local rows
   int starts[3][SW_MAX_WIN];
 };
 
@@ -41,6 +44,11 @@ __device__ __forceinline__ void cover(const int* st, int n, int r, int p, int& l
   }
 }
 
+// PARTIAL (the all-reduce exchange, ABI 14): only the windows this rank predicted (g % world
+// == rank, local patch row g / world), summed in window order; out is (B, C + 1, D, H, W):
+// channels [0, C) the weighted sums, channel C the summed weights -- no division (the ranks'
+// partials are all-reduced first, then wf_sliding_window_normalize divides)
+template <bool PARTIAL>
 __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
   // hipcc contracts a*b+c into an FMA by default (also across the inlined __fmul_rn /
   // __fadd_rn intrinsics); the reference rounds the product and the sum separately, so the
@@ -63,17 +71,25 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
   const int64_t R3 = (int64_t)a.rd * a.rh * a.rw;
   const int64_t nwin = (int64_t)a.n[0] * a.n[1] * a.n[2];
   const int64_t S = (int64_t)a.D * a.H * a.W;
-  float* dst = a.out + (int64_t)b * a.C * S + ((int64_t)z * a.H + y) * a.W + x;
+  const int CO = PARTIAL ? a.C + 1 : a.C;
+  float* dst = a.out + (int64_t)b * CO * S + ((int64_t)z * a.H + y) * a.W + x;
+  auto mine = [&](int iz, int iy, int ix) {
+    if (!PARTIAL) return true;
+    const int64_t g = (int64_t)b * nwin + ((int64_t)iz * a.n[1] + iy) * a.n[2] + ix;
+    return g % a.world == a.rank;
+  };
 
   // count map: sum of the window weights in window order (monai/inferers/utils.py:262-269)
   float cnt = 0.f;
   for (int iz = z0; iz <= z1; ++iz)
     for (int iy = y0; iy <= y1; ++iy)
       for (int ix = x0; ix <= x1; ++ix) {
+        if (!mine(iz, iy, ix)) continue;
         const int64_t loc = ((int64_t)(z - a.starts[0][iz]) * a.rh + (y - a.starts[1][iy])) * a.rw +
                             (x - a.starts[2][ix]);
         cnt = cnt + a.map[loc];
       }
+  if (PARTIAL) dst[(int64_t)a.C * S] = cnt;
 
   for (int c0 = 0; c0 < a.C; c0 += 4) {
     const int nc = min(4, a.C - c0);
@@ -81,15 +97,16 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
     for (int iz = z0; iz <= z1; ++iz)
       for (int iy = y0; iy <= y1; ++iy)
         for (int ix = x0; ix <= x1; ++ix) {
+          if (!mine(iz, iy, ix)) continue;
           const int64_t loc =
               ((int64_t)(z - a.starts[0][iz]) * a.rh + (y - a.starts[1][iy])) * a.rw +
               (x - a.starts[2][ix]);
           const float w = a.map[loc];
           // global window index (batch-major, then the 'ij' meshgrid order of
-          // dense_patch_slices) -> row of the gathered patch tensor
+          // dense_patch_slices) -> row of the gathered patch tensor (PARTIAL: the local slot)
           const int64_t g = (int64_t)b * nwin + ((int64_t)iz * a.n[1] + iy) * a.n[2] + ix;
           const int64_t r = g % a.world, j = g / a.world;
-          const int64_t row = ((j / a.sb) * a.world + r) * a.sb + (j % a.sb);
+          const int64_t row = PARTIAL ? j : ((j / a.sb) * a.world + r) * a.sb + (j % a.sb);
           const float* p = a.patches + (row * a.C + c0) * R3 + loc;
 #pragma unroll
           for (int c = 0; c < 4; ++c)
@@ -100,7 +117,21 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
         }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      if (c < nc) dst[(int64_t)(c0 + c) * S] = __fdiv_rn(acc[c], cnt);
+      if (c < nc) dst[(int64_t)(c0 + c) * S] = PARTIAL ? acc[c] : __fdiv_rn(acc[c], cnt);
+  }
+}
+
+// out[b][c] = num[b][c] / num[b][C] (the all-reduced partial stitch)
+__global__ __launch_bounds__(256) void stitch_normalize_kernel(const float* __restrict__ num,
+                                                               float* __restrict__ out, int B,
+                                                               int C, int64_t S) {
+  const int64_t total = (int64_t)B * C * S;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t s = i % S, bc = i / S;
+    const int b = (int)(bc / C);
+    out[i] = __fdiv_rn(num[((int64_t)b * (C + 1) + (bc - (int64_t)b * C)) * S + s],
+                       num[((int64_t)b * (C + 1) + C) * S + s]);
   }
 }
 
@@ -205,11 +236,11 @@ extern "C" int wf_importance_map(int mode, const float* sigma_scale, float* out,
   return check_launch("importance_map");
 }
 
-extern "C" int wf_sliding_window_stitch(const float* patches, int64_t world,
-                                        int64_t slots_per_round, const float* importance_map,
-                                        const int64_t* starts, const int64_t* nwin, float* out,
-                                        int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
-                                        int64_t rd, int64_t rh, int64_t rw, void* stream) {
+static int stitch_launch(const float* patches, int64_t world, int64_t slots_per_round,
+                         int64_t rank, bool partial, const float* importance_map,
+                         const int64_t* starts, const int64_t* nwin, float* out, int64_t B,
+                         int64_t C, int64_t D, int64_t H, int64_t W, int64_t rd, int64_t rh,
+                         int64_t rw, void* stream) {
   WF_REQUIRE_PTR(patches);
   WF_REQUIRE_PTR(importance_map);
   WF_REQUIRE_PTR(starts);
@@ -232,6 +263,8 @@ extern "C" int wf_sliding_window_stitch(const float* patches, int64_t world,
   a.rw = (int)rw;
   a.world = (int)world;
   a.sb = (int)slots_per_round;
+  WF_REQUIRE(rank >= 0 && rank < world, "rank out of range");
+  a.rank = (int)rank;
   const int64_t size[3] = {D, H, W}, roi[3] = {rd, rh, rw};
   int64_t off = 0;
   for (int ax = 0; ax < 3; ++ax) {
@@ -252,7 +285,43 @@ extern "C" int wf_sliding_window_stitch(const float* patches, int64_t world,
     off += nwin[ax];
   }
   const int64_t total = B * D * H * W;
-  hipLaunchKernelGGL(stitch_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
-                     (hipStream_t)stream, a);
+  if (partial)
+    hipLaunchKernelGGL(stitch_kernel<true>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                       (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(stitch_kernel<false>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                       (hipStream_t)stream, a);
   return check_launch("sliding_window_stitch");
+}
+
+extern "C" int wf_sliding_window_stitch(const float* patches, int64_t world,
+                                        int64_t slots_per_round, const float* importance_map,
+                                        const int64_t* starts, const int64_t* nwin, float* out,
+                                        int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                                        int64_t rd, int64_t rh, int64_t rw, void* stream) {
+  return stitch_launch(patches, world, slots_per_round, 0, false, importance_map, starts, nwin,
+                       out, B, C, D, H, W, rd, rh, rw, stream);
+}
+
+extern "C" int wf_sliding_window_stitch_partial(const float* patches, int64_t world,
+                                                int64_t rank, const float* importance_map,
+                                                const int64_t* starts, const int64_t* nwin,
+                                                float* out, int64_t B, int64_t C, int64_t D,
+                                                int64_t H, int64_t W, int64_t rd, int64_t rh,
+                                                int64_t rw, void* stream) {
+  return stitch_launch(patches, world, 1, rank, true, importance_map, starts, nwin, out, B, C, D,
+                       H, W, rd, rh, rw, stream);
+}
+
+extern "C" int wf_sliding_window_normalize(const float* num, float* out, int64_t B, int64_t C,
+                                           int64_t D, int64_t H, int64_t W, void* stream) {
+  WF_REQUIRE_PTR(num);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE(B >= 1 && C >= 1 && D >= 1 && H >= 1 && W >= 1, "empty output");
+  const int64_t S = D * H * W;
+  const int64_t total = B * C * S;
+  hipLaunchKernelGGL(stitch_normalize_kernel,
+                     dim3((unsigned)std::min<int64_t>(cdiv(total, 256), 65536)), dim3(256), 0,
+                     (hipStream_t)stream, num, out, (int)B, (int)C, S);
+  return check_launch("sliding_window_normalize");
 }

@@ -15,7 +15,9 @@ What is MI355X-specific:
     `sw_batch_size`, and after every round the per-window logits are all-gathered over RCCL
     (`all_gather_into_tensor`, async, so round k's exchange overlaps round k+1's forward)
     into one (rounds, W, sw_batch, C, *roi) buffer.  Every rank then stitches the full
-    output; the padded slots of the last round are zeros and never read.
+    output; the padded slots of the last round are zeros and never read.  The alternative
+    exchange (exchange="allreduce") stitches each rank's own windows into weighted
+    sums + weights and all-reduces those once per case.
   * The importance map and the stitch are HIP kernels (`ops.importance_map`,
     `ops.sliding_window_stitch`): one thread per output voxel gathers the windows covering
     it in the reference's order and divides by the summed weights -- no count-map tensor,
@@ -31,6 +33,7 @@ NotImplementedError instead of silently doing something else.
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Callable, List, Optional, Sequence, Tuple
 
 import torch
@@ -142,12 +145,23 @@ def sliding_window_inference(inputs: torch.Tensor, roi_size, sw_batch_size: int,
                              with_coord: bool = False, *args: Any,
                              process_group=None, stitch: Optional[Callable] = None,
                              weight_map_fn: Optional[Callable] = None,
+                             exchange: Optional[str] = None,
+                             partial_stitch: Optional[Callable] = None,
+                             normalize: Optional[Callable] = None,
                              **kwargs: Any) -> torch.Tensor:
     """monai.inferers.sliding_window_inference for 3-D NCDHW inputs and a predictor returning
     one tensor of the window's spatial size.  See the module docstring for `process_group`.
 
-    `stitch` / `weight_map_fn` default to the HIP kernels; tests substitute the CPU oracle to
-    exercise the sharding logic on a CPU (gloo) process group."""
+    exchange (default: WF_SW_EXCHANGE or "allgather"): how the ranks' windows meet --
+      "allgather": every round's window logits are all-gathered and every rank stitches the
+        whole case in the reference's window order (bitwise MONAI's sums);
+      "allreduce": each rank stitches only its own windows into weighted sums + summed weights
+        (ops.sliding_window_stitch_partial), ONE all-reduce of those (C + 1) full-size planes,
+        then a division (ops.sliding_window_normalize) -- the cheaper exchange SURVEY 8e names
+        (one (C + 1) x D x H x W payload instead of every window's logits); the sums then
+        meet in rank order, so the result equals the all-gather one to fp32 rounding.
+    `stitch` / `weight_map_fn` / `partial_stitch` / `normalize` default to the HIP kernels;
+    tests substitute the CPU oracle to exercise the sharding logic on a CPU (gloo) group."""
     if process_fn is not None or (buffer_steps is not None and buffer_steps > 0) or with_coord:
         raise NotImplementedError("process_fn / buffer_steps / with_coord are not used by "
                                   "WaveFormer's prediction path and are not implemented")
@@ -164,6 +178,12 @@ def sliding_window_inference(inputs: torch.Tensor, roi_size, sw_batch_size: int,
     world, rank = _group_info(process_group)
     stitch = stitch or ops.sliding_window_stitch
     weight_map_fn = weight_map_fn or ops.importance_map
+    exchange = exchange or os.environ.get("WF_SW_EXCHANGE", "allgather")
+    if exchange not in ("allgather", "allreduce"):
+        raise ValueError(f"exchange must be 'allgather' or 'allreduce', got {exchange!r}")
+    reduce_mode = exchange == "allreduce"
+    partial_stitch = partial_stitch or ops.sliding_window_stitch_partial
+    normalize = normalize or ops.sliding_window_normalize
 
     B = inputs.shape[0]
     image_size_ = tuple(int(v) for v in inputs.shape[2:])
@@ -212,8 +232,14 @@ def sliding_window_inference(inputs: torch.Tensor, roi_size, sw_batch_size: int,
             out_k = out_k.float()
         if buf is None:
             C = out_k.shape[1] if out_k is not None else C_out
-            buf = torch.zeros((rounds, world, sw_batch_size, C) + roi, dtype=torch.float32,
-                              device=sw_device)
+            # all-reduce: this rank's windows only, local slot order (slot j = window
+            # rank + j * world); all-gather: every rank's, per round
+            shape = (rounds, 1 if reduce_mode else world, sw_batch_size, C) + roi
+            buf = torch.zeros(shape, dtype=torch.float32, device=sw_device)
+        if reduce_mode:
+            if out_k is not None:
+                buf[k, 0, :len(live)].copy_(out_k)
+            continue
         mine = buf[k, rank] if world == 1 else torch.zeros_like(buf[k, rank])
         if out_k is not None:
             mine[:len(live)].copy_(out_k)
@@ -223,8 +249,15 @@ def sliding_window_inference(inputs: torch.Tensor, roi_size, sw_batch_size: int,
                                                         async_op=True), mine))
     for work, _ in pending:
         work.wait()
-    out = stitch(buf.view((-1,) + tuple(buf.shape[3:])), wmap, starts, image_size, B,
-                 world, sw_batch_size)
+    if reduce_mode:
+        part = partial_stitch(buf.view((-1,) + tuple(buf.shape[3:])), wmap, starts, image_size,
+                              B, world, rank)
+        if world > 1:
+            dist.all_reduce(part, op=dist.ReduceOp.SUM, group=process_group)
+        out = normalize(part)
+    else:
+        out = stitch(buf.view((-1,) + tuple(buf.shape[3:])), wmap, starts, image_size, B,
+                     world, sw_batch_size)
     if any(pad):
         # remove padding (monai/inferers/utils.py:303-316; outputs share the roi's resolution)
         z0, y0, x0 = pad[4], pad[2], pad[0]
@@ -253,7 +286,8 @@ class SlidingWindowInferer:
                  sw_device=None, device=None, progress: bool = False,
                  cache_roi_weight_map: bool = False, cpu_thresh: Optional[int] = None,
                  buffer_steps: Optional[int] = None, buffer_dim: int = -1,
-                 with_coord: bool = False, process_group=None) -> None:
+                 with_coord: bool = False, process_group=None,
+                 exchange: Optional[str] = None) -> None:
         if mode not in ops.BLEND_MODES:
             raise ValueError(f"mode must be one of {sorted(ops.BLEND_MODES)}, got {mode!r}")
         self.roi_size = roi_size
@@ -271,6 +305,7 @@ class SlidingWindowInferer:
         self.buffer_dim = buffer_dim
         self.with_coord = with_coord
         self.process_group = process_group
+        self.exchange = exchange
         self.roi_weight_map = None
         self._cache = cache_roi_weight_map
 
@@ -290,7 +325,7 @@ class SlidingWindowInferer:
             inputs, self.roi_size, self.sw_batch_size, network, self.overlap, self.mode,
             self.sigma_scale, self.padding_mode, self.cval, self.sw_device, device,
             self.progress, self.roi_weight_map, None, buffer_steps, buffer_dim, self.with_coord,
-            *args, process_group=self.process_group, **kwargs)
+            *args, process_group=self.process_group, exchange=self.exchange, **kwargs)
 
 
 # ------------------------------------------------------------------------------------------

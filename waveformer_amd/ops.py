@@ -1346,6 +1346,41 @@ def sliding_window_stitch(patches: torch.Tensor, weight_map: torch.Tensor,
     return out
 
 
+def sliding_window_stitch_partial(patches: torch.Tensor, weight_map: torch.Tensor,
+                                  starts: Sequence[Sequence[int]], image_size: Sequence[int],
+                                  batch: int, world: int, rank: int) -> torch.Tensor:
+    """This rank's share of the stitch for the all-reduce exchange: (batch, C + 1, *image)
+    with the weighted sums of the windows g % world == rank (local rows g // world of
+    `patches`) and, in channel C, their summed weights (wf_sliding_window_stitch_partial)."""
+    _check(patches, "patches")
+    _check(weight_map, "importance_map")
+    rows, C = patches.shape[:2]
+    roi = tuple(patches.shape[2:])
+    if tuple(weight_map.shape) != roi:
+        raise ValueError(f"sliding_window_stitch_partial: map {tuple(weight_map.shape)} != roi {roi}")
+    nwin = [len(s) for s in starts]
+    total = batch * nwin[0] * nwin[1] * nwin[2]
+    if rows < -(-total // world):
+        raise ValueError(f"sliding_window_stitch_partial: {rows} rows < {-(-total // world)}")
+    D, H, W = (int(v) for v in image_size)
+    out = torch.empty((batch, C + 1, D, H, W), dtype=torch.float32, device=patches.device)
+    flat = [int(s) for ax in starts for s in ax]
+    _lib.call("wf_sliding_window_stitch_partial", patches.data_ptr(), int(world), int(rank),
+              weight_map.data_ptr(), (ctypes.c_int64 * len(flat))(*flat),
+              (ctypes.c_int64 * 3)(*nwin), out.data_ptr(), batch, C, D, H, W, *roi, _stream())
+    return out
+
+
+def sliding_window_normalize(num: torch.Tensor) -> torch.Tensor:
+    """(B, C + 1, D, H, W) summed partials -> (B, C, D, H, W) = num[:, :C] / num[:, C]."""
+    _check(num, "num")
+    B, C1, D, H, W = num.shape
+    out = torch.empty((B, C1 - 1, D, H, W), dtype=torch.float32, device=num.device)
+    _lib.call("wf_sliding_window_normalize", num.data_ptr(), out.data_ptr(), B, C1 - 1, D, H, W,
+              _stream())
+    return out
+
+
 def tta_merge(pred: torch.Tensor, passes: Sequence[Sequence[int]]) -> torch.Tensor:
     """(P, C, D, H, W) per-pass predictions on flipped inputs -> (1, C, D, H, W) average of the
     flipped-back passes (light_training/prediction.py:123-155).  passes[p] lists the flipped
