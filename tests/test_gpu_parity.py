@@ -415,6 +415,72 @@ def test_ccf_ffn_stage34_ln1_fuse_subprocess():
     assert worst <= 5e-5, worst
 
 
+_MERGE_SHAPES = ((2, 8, 8, 8), (1, 6, 10, 6), (1, 64, 64, 64))
+
+
+def _merge48_outputs(prec):
+    """PatchMerging 1 -> 2 (C = 48: merge.hip's resident-weight kernel unless WF_MERGE_RES=0)
+    over _MERGE_SHAPES, with the oracle's fp64 outputs."""
+    import waveformer_amd.network_models as NM
+    from oracle.weight_rule import rule_state_dict
+    from waveformer_amd import ops
+    outs = []
+    for i, shape in enumerate(_MERGE_SHAPES):
+        m = NM.PatchMerging(48, norm_layer=C._ln6())
+        sd = rule_state_dict(m.state_dict())
+        m.load_state_dict(sd)
+        m = m.to(DEV)
+        x = seeded_randn(shape + (48,), 60 + i) * 1.5 + 0.25
+        ref = R.patch_merging({k: v.double() for k, v in sd.items()}, "", x.double())
+        with torch.no_grad(), ops.precision(prec):
+            out = ops.patch_merging(x.to(DEV), m.norm, m.reduction)
+        outs.append((out.cpu(), ref))
+    return outs
+
+
+@pytest.mark.parametrize("prec,tol", [("bf16x3", 1e-5), ("fp16", 2e-3)])
+def test_patch_merging_c48_resident_vs_oracle(prec, tol):
+    """The stage 1 -> 2 merge on merge.hip (weight resident in LDS, persistent 12-wave
+    workgroups, no barrier after the staging): ragged row count (45 rows: a partial 16-row
+    tile) and a 64^3 volume (2048 tiles over 256 workgroups), against the fp64 oracle
+    (wave_helper.py:173-194 with quirk Q3)."""
+    for out, ref in _merge48_outputs(prec):
+        assert out.shape == ref.shape
+        assert C.rel_l2(out, ref.float()) <= tol
+
+
+_MERGE_CHILD = r"""
+import sys, torch
+sys.path.insert(0, '.')
+from tests import test_gpu_parity as T
+outs = T._merge48_outputs(sys.argv[1])
+torch.save([o for o, _ in outs], sys.argv[2])
+print("MERGE_CHILD_OK")
+"""
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "fp16"])
+def test_patch_merging_c48_resident_bitwise_vs_gemm_kc(prec, tmp_path):
+    """merge.hip keeps gemm_kc's LN_COMPUTE arithmetic and order (shifted one-pass moments,
+    k-step MFMA accumulation, fp16 operands rounded from the fp32 value): bit-identical outputs
+    to gemm_kc (8-wave workgroups at the small shapes, 16-wave at 64^3).  WF_MERGE_RES=0 (read
+    once per process) runs gemm_kc in a child process."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dst = str(tmp_path / "kc.pt")
+    env = dict(os.environ, WF_MERGE_RES="0", PYTHONPATH=repo)
+    r = subprocess.run([sys.executable, "-c", _MERGE_CHILD, prec, dst], cwd=repo, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "MERGE_CHILD_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+    kc = torch.load(dst, weights_only=True)
+    for (out, _), o_kc in zip(_merge48_outputs(prec), kc):
+        d = (out - o_kc).abs()
+        rows = (d.reshape(-1, out.shape[-1]) > 0).any(-1)
+        assert torch.equal(out, o_kc), (tuple(out.shape), int((d > 0).sum()), float(d.max()),
+                                        int(rows.sum()), rows.nonzero()[:8].flatten().tolist())
+
+
 @pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11)])
 @pytest.mark.parametrize("block", [False, True])
 def test_ccf_ffn_stage2_staged_path_vs_oracle(shape, block, monkeypatch):

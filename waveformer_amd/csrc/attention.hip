@@ -493,8 +493,14 @@ __device__ __forceinline__ int kswz(int row) {  // 16-B chunk XOR of a K row (se
 #ifndef WF_ATTN_MFMA_SUM
 #define WF_ATTN_MFMA_SUM 1
 #endif
-#ifndef WF_ATTN_BPERMUTE  // 1: the round-3 __shfl_xor (ds_bpermute) max exchange, for A/B
-#define WF_ATTN_BPERMUTE 0
+// WF_ATTN_BPERMUTE: the per-tile max exchange across the 4 key groups of a query column as
+// __shfl_xor (ds_bpermute, LDS crossbar; default) or as v_permlane16/32_swap (VALU, 0).  The
+// round-5 kernel-trace A/B (profiles/r5_attention_ab.txt) has the bpermute form 162.8 vs
+// 169.1 us per B = 8 stage-1 launch: the kernel's VALU is its tighter resource, and the swap
+// form adds VALU work.  A software-pipelined variant (tile t + 1's score MFMAs issued before
+// tile t's softmax) measured 174.8 us and was dropped.
+#ifndef WF_ATTN_BPERMUTE
+#define WF_ATTN_BPERMUTE 1
 #endif
 template <int P>
 __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict__ qkv,
@@ -574,10 +580,9 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
     float lsum = 0.f;  // this lane's 16 keys of each tile; the 4 key groups are summed at the end
 #endif
     float mrun = -INFINITY;
-#pragma unroll 2
-    for (int t = 0; t < 8; ++t) {  // 64-key tiles (one z slice of the window each)
+    // S^T of 64-key tile t: 4 sub-tiles of 16 keys, the accumulator starting at the bias
+    auto scores = [&](int t, f32x4 (&s)[4]) {
       const float* bt = tbr + rb + 23 * t;
-      f32x4 s[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ks[(t * 64 + kt * 16 + l15) * KS + kch]);
@@ -585,6 +590,11 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
         s[kt] = mma32<P>(a, b1, bias);
         if (SPLIT) s[kt] = mma32<P>(a, b2, s[kt]);
       }
+    };
+#pragma unroll 2
+    for (int t = 0; t < 8; ++t) {  // 64-key tiles (one z slice of the window each)
+      f32x4 s[4];
+      scores(t, s);
       float tmax = mrun;  // a chain, so the compiler pairs it into v_max3_f32
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)

@@ -820,5 +820,6 @@ extern "C" int wf_patch_merging_fwd(const float* x, const float* ln_w, const flo
   g.out = out;
   g.out_bf16 = 0;
   g.ldo = 2 * C;
+  if (try_launch_merge_resident(g, (hipStream_t)stream)) return check_launch("wf_patch_merging_fwd");
   return launch_gemm(g, (hipStream_t)stream, "wf_patch_merging_fwd");
 }

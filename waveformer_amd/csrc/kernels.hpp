@@ -197,6 +197,9 @@ int launch_ffn_fused(const DwFcArgs& a, int prec, hipStream_t s);
 // K-chunked MFMA GEMM (gemm_kc.hip) for the shapes whose weight does not fit gemm_rows' LDS
 // in one column chunk; returns 1 if it took the shape
 int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s);
+// PatchMerging 1 -> 2 (C = 48) with the whole weight resident in LDS (merge.hip); returns 1
+// if it took the shape
+int try_launch_merge_resident(const GemmArgs& g, hipStream_t s);
 // stage-2 CCF_FFN pwconv (N = 384 with the LayerNorm + GELU epilogue, gemm_lnw.hip): columns
 // split over the waves; returns 1 if it took the shape
 int try_launch_gemm_lnw(const GemmArgs& g, hipStream_t s);
