@@ -18,6 +18,10 @@
 // so each call site compiles to straight-line code with 32-bit index math.
 #include "gemm_common.hpp"
 
+#ifndef WF_ROWS_DBG  // 1: timing-experiment build (GemmArgs::dbg phase skips; never the shipped library)
+#define WF_ROWS_DBG 0
+#endif
+
 namespace wf {
 
 // NTH = 768 (LN + GELU epilogue with fp32 output; WF_GEMM_ROWS_12W=0 for the 8-wave one): 12 waves per
@@ -247,8 +251,14 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
         gmean = g.a_stats[2 * arow_n];
         grstd = g.a_stats[2 * arow_n + 1];
       }
+#if WF_ROWS_DBG
+      if (!(g.dbg & 4)) {
+#endif
       kstep(0, v0);
       if (K32 > 32) kstep(32, v1);
+#if WF_ROWS_DBG
+      }
+#endif
     } else {
       // k loop with a one-step register prefetch of the A fragment (last step: the next tile's)
 #pragma unroll 1
@@ -318,7 +328,11 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
       const int col = c0 + t * 16 + 4 * g4;
       const int colc = min(col, N - 4);
       f32x4 v = acc[t];
+#if WF_ROWS_DBG
+      if (EPI == EPI_LN_GELU && !(g.dbg & 2)) {
+#else
       if (EPI == EPI_LN_GELU) {
+#endif
         // elw / elb hold HALF the LayerNorm affine (staged x 0.5, exact): the normalised
         // value comes out as GELU's half input; (v - mean) * rstd as one FMA per pair
         const f32x4 lw = *reinterpret_cast<const f32x4*>(elw + t * 16 + 4 * g4);
@@ -401,9 +415,14 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
         for (int j = 0; j < SROWS * RC / 64; ++j) {
           const int c = j * 64 + lane, r = c / RC, c4 = c - r * RC;
           const f32x4 v = *reinterpret_cast<const f32x4*>(ostg + r * OST + 4 * c4);
+#if WF_ROWS_DBG
+          const int doff = (g.dbg & 1) ? 0x7fffff00 : 0;  // past the descriptor: dropped
+#else
+          constexpr int doff = 0;
+#endif
           __builtin_amdgcn_raw_buffer_store_b128(
               __builtin_bit_cast(u32x4, v), orsrc,
-              (int)(((tile * 16 + half * SROWS + r) * g.ldo + 4 * c4) * 4), 0, 0);
+              doff + (int)(((tile * 16 + half * SROWS + r) * g.ldo + 4 * c4) * 4), 0, 0);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -423,7 +442,9 @@ static bool rows_w12(const GemmArgs& g) {
 }
 
 template <int NT, int MAP, int EPI>
-static void go_rows(const GemmArgs& g, dim3 grid, size_t lds, hipStream_t s) {
+static void go_rows(const GemmArgs& g0, dim3 grid, size_t lds, hipStream_t s) {
+  GemmArgs g = g0;
+  g.dbg = WF_ROWS_DBG && getenv("WF_ROWS_DBG") ? atoi(getenv("WF_ROWS_DBG")) : 0;
   void (*kern)(GemmArgs);
   if constexpr (EPI == EPI_LN_GELU && MAP == MAP_IDENTITY) {
     if (rows_w12(g)) {  // lds already holds the 12 x 8-row output staging (host below)

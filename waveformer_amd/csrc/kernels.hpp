@@ -96,6 +96,7 @@ struct GemmArgs {
   const float* r_ln_b;
   const float* r_scale;  //   per-sample factor on the added branch (DropPath) or NULL
   int64_t rows_per_sample; // M / B for r_scale
+  int dbg;               // timing experiments only (builds with WF_ROWS_DBG=1): phases skipped
   float* o_pstats;       // EPI_STORE (gemm_kc): if non-NULL, per (row, column chunk) {mean, M2}
                          //   of the stored values, (M, N / chunk, 2) -- LN statistics partials
 };
