@@ -303,8 +303,9 @@ def test_ccf_ffn_stage1_batch_beyond_tb4_range():
                                    (1, 16, 16, 16)])
 @pytest.mark.parametrize("block", [False, True])
 def test_ccf_ffn_stage2_vs_oracle(shape, block):
-    """C = 96, hidden = 384 (encoder stage 2): the pwconv + LN1 + GELU GEMM with the columns
-    split over the waves (gemm_lnw.hip; rows not a multiple of its 64-row tile included), then
+    """C = 96, hidden = 384 (encoder stage 2): the pwconv + LN1 + GELU GEMM (pw2.hip's
+    resident-weight kernel for bf16x3 / fp16, gemm_lnw.hip for bf16; rows not a multiple of the
+    16-row tile included), then
     the fused back half (ffn_dwfc.hip's ffn_dwfc2_kernel: depthwise conv, LN2 + GELU, fc and
     the Q4 residual with h2 on chip; ragged 4 x 4 tiles, z segments shorter than the volume
     at (1, 20, 8, 8)) -- same bars as stage 1."""
@@ -479,6 +480,63 @@ def test_patch_merging_c48_resident_bitwise_vs_gemm_kc(prec, tmp_path):
         rows = (d.reshape(-1, out.shape[-1]) > 0).any(-1)
         assert torch.equal(out, o_kc), (tuple(out.shape), int((d > 0).sum()), float(d.max()),
                                         int(rows.sum()), rows.nonzero()[:8].flatten().tolist())
+
+
+_FFN2_SHAPES = ((2, 8, 8, 8), (1, 5, 6, 11), (8, 32, 32, 32))
+
+
+def _stage2_ffn_outputs(prec):
+    """The stage-2 CCF_FFN inside a Block (norm2 statistics given, Q4 residual) over
+    _FFN2_SHAPES; the last is the B = 8 bench shape (262,144 rows: 16,384 tiles over 256
+    persistent workgroups)."""
+    import waveformer_amd.network_models as NM
+    from oracle.weight_rule import rule_state_dict
+    from waveformer_amd import ops
+    outs = []
+    for i, shape in enumerate(_FFN2_SHAPES):
+        mlp = NM.CCF_FFN(96, 384, img_size=shape[1:])
+        mlp.load_state_dict(rule_state_dict(mlp.state_dict()))
+        mlp = mlp.eval().to(DEV)
+        norm2 = torch.nn.LayerNorm(96, eps=1e-6)
+        with torch.no_grad():
+            norm2.weight.copy_(seeded_randn((96,), 34) * 0.2 + 1)
+            norm2.bias.copy_(seeded_randn((96,), 35) * 0.1)
+        norm2 = norm2.to(DEV)
+        x = seeded_randn(shape + (96,), 70 + i).to(DEV)
+        bs = torch.linspace(0.5, 2.0, shape[0]).to(DEV)
+        with torch.no_grad(), ops.precision(prec):
+            stats = ops.msfuse([], x, 1e-6)[1]
+            outs.append(ops.ccf_ffn(x, stats, norm2, mlp, bs).cpu())
+    return outs
+
+
+_FFN2_CHILD = r"""
+import sys, torch
+sys.path.insert(0, '.')
+from tests import test_gpu_parity as T
+torch.save(T._stage2_ffn_outputs(sys.argv[1]), sys.argv[2])
+print("FFN2_CHILD_OK")
+"""
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "fp16"])
+def test_stage2_pwconv_resident_bitwise_vs_gemm_lnw(prec, tmp_path):
+    """pw2.hip (weight resident, whole rows per wave) keeps gemm_lnw<3, 3, 8, 8>'s arithmetic
+    and order -- split products per column tile, the row moments as its 8 waves' partials in its
+    tree order: the stage-2 FFN outputs are bit-identical.  WF_PW2_RES=0 (read once per
+    process) runs gemm_lnw in a child process."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dst = str(tmp_path / "lnw.pt")
+    env = dict(os.environ, WF_PW2_RES="0", PYTHONPATH=repo)
+    r = subprocess.run([sys.executable, "-c", _FFN2_CHILD, prec, dst], cwd=repo, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "FFN2_CHILD_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+    ref = torch.load(dst, weights_only=True)
+    for out, o_ref in zip(_stage2_ffn_outputs(prec), ref):
+        d = (out - o_ref).abs()
+        assert torch.equal(out, o_ref), (tuple(out.shape), int((d > 0).sum()), float(d.max()))
 
 
 @pytest.mark.parametrize("shape", [(2, 8, 8, 8), (1, 5, 6, 11)])

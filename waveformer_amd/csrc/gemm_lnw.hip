@@ -234,6 +234,7 @@ int try_launch_gemm_lnw(const GemmArgs& g, hipStream_t s) {
       !(g.a_ln == LN_NONE || g.a_ln == LN_GIVEN) || g.a_C != g.K || g.K % 8 != 0 ||
       g.M >= ((int64_t)1 << 31) || g.ldo < g.N || g.ldo % 4 != 0)
     return 0;
+  if (try_launch_pw2_resident(g, s)) return 1;
   const int ks = (g.K + 31) / 32;
   static const int wrt = getenv("WF_LNW_WIDE_RT") ? atoi(getenv("WF_LNW_WIDE_RT")) : 4;
   if (gemm_lnw_wide_shape(g)) {

@@ -201,6 +201,9 @@ int try_launch_gemm_kc(const GemmArgs& g, hipStream_t s);
 // PatchMerging 1 -> 2 (C = 48) with the whole weight resident in LDS (merge.hip); returns 1
 // if it took the shape
 int try_launch_merge_resident(const GemmArgs& g, hipStream_t s);
+// the stage-2 CCF_FFN pwconv (K = 96, N = 384) with the whole weight resident in LDS (pw2.hip);
+// returns 1 if it took the shape
+int try_launch_pw2_resident(const GemmArgs& g, hipStream_t s);
 // stage-2 CCF_FFN pwconv (N = 384 with the LayerNorm + GELU epilogue, gemm_lnw.hip): columns
 // split over the waves; returns 1 if it took the shape
 int try_launch_gemm_lnw(const GemmArgs& g, hipStream_t s);
