@@ -502,6 +502,9 @@ __device__ __forceinline__ int kswz(int row) {  // 16-B chunk XOR of a K row (se
 #ifndef WF_ATTN_BPERMUTE
 #define WF_ATTN_BPERMUTE 1
 #endif
+#ifndef WF_ATTN_T4  // 1: bias quads as single ds_read_b128 (A/B; 0: four scalar reads)
+#define WF_ATTN_T4 1
+#endif
 template <int P>
 __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict__ qkv,
                                                           const float* __restrict__ table,
@@ -518,7 +521,13 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
   constexpr int VQ = (N / 4) * VB;
   __shared__ __attribute__((aligned(16))) uint16_t Ks[N * KS];
   __shared__ __attribute__((aligned(16))) uint16_t Vq[2 * VQ];
+#if WF_ATTN_T4
+  // the reversed table as overlapping quads: tq[i] = {tbr[i], tbr[i+1], tbr[i+2], tbr[i+3]},
+  // so a lane's 4 consecutive bias values are one aligned ds_read_b128
+  __shared__ __attribute__((aligned(16))) f32x4 tq[TBLN];
+#else
   __shared__ __attribute__((aligned(16))) float tbr[TBLN + 1];  // reversed, x log2 e
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int qs, h;
   int64_t bw;
@@ -528,7 +537,20 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
   const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
 
   for (int i = tid; i < TBLN; i += 512)
+#if WF_ATTN_T4
+  {
+    // tq[j].c = tbr[j + c] = table[TBLN - 1 - j - c] (0 past the end: never read)
+    const float v = table[(int64_t)i * heads + h] * 1.4426950408889634f;
+    const int j = TBLN - 1 - i;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (j - c >= 0) reinterpret_cast<float*>(&tq[j - c])[c] = v;
+    if (j >= TBLN - 3)
+      for (int c = TBLN - j; c < 4; ++c) reinterpret_cast<float*>(&tq[j])[c] = 0.f;
+  }
+#else
     tbr[TBLN - 1 - i] = table[(int64_t)i * heads + h] * 1.4426950408889634f;
+#endif
   for (int it = tid; it < N * 2; it += 512) {  // K: (key, 8-value chunk)
     const int key = it >> 1, ch = it & 1, sw = kswz(key);
     bf16x8 hi = z8, lo = z8;
@@ -582,11 +604,19 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
     float mrun = -INFINITY;
     // S^T of 64-key tile t: 4 sub-tiles of 16 keys, the accumulator starting at the bias
     auto scores = [&](int t, f32x4 (&s)[4]) {
+#if WF_ATTN_T4
+      const f32x4* bq = tq + rb + 23 * t;
+#else
       const float* bt = tbr + rb + 23 * t;
+#endif
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ks[(t * 64 + kt * 16 + l15) * KS + kch]);
+#if WF_ATTN_T4
+        const f32x4 bias = bq[30 * kt];
+#else
         const f32x4 bias = f32x4{bt[30 * kt], bt[30 * kt + 1], bt[30 * kt + 2], bt[30 * kt + 3]};
+#endif
         s[kt] = mma32<P>(a, b1, bias);
         if (SPLIT) s[kt] = mma32<P>(a, b2, s[kt]);
       }
