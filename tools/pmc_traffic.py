@@ -44,7 +44,8 @@ def load(root, counter):
 WIDE16 = ("dwt3d_haar_fwd_kernel", "idwt3d_haar_cl4_kernel", "idwt3d_haar_nc4_kernel",
           "msfuse_row_kernel", "ffn_dwfc_sb_kernel", "ffn_dwfc_ws_kernel", "ffn_dwfc2_kernel",
           "gemm_rows_kernel", "gemm_kc_kernel", "gemm_lnw_kernel", "dwconv_ln_gelu_kernel",
-          "proj_out_kernel", "ffn_dwfc_tb4_kernel", "ffn_dwfc_tb_kernel", "attn_tbl_kernel")
+          "proj_out_kernel", "ffn_dwfc_tb4_kernel", "ffn_dwfc_tb_kernel", "attn_tbl_kernel",
+          "merge_res_kernel", "pw2_res_kernel")
 
 
 def rule_of(name):
