@@ -348,7 +348,12 @@ struct MsfuseArgs {
   float* stats;
   float eps;
   int B, C, D, H, W;
+  int dbg;  // timing experiments only (builds with MSF_DBG=1): phases skipped
 };
+
+#ifndef MSF_DBG
+#define MSF_DBG 0
+#endif
 
 __device__ __forceinline__ void lin_index(int o, int in, int out, int& i0, int& i1, float& l0,
                                           float& l1) {
@@ -470,7 +475,13 @@ __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
   }
   int roff[4];
   int ro = 0;
+#if MSF_DBG
+  const int nsrc_stage = (a.dbg & 2) ? 0 : a.nsrc;
+  for (int s = 0; s < a.nsrc; ++s) roff[s] = 0;
+  for (int s = 0; s < nsrc_stage; ++s) {
+#else
   for (int s = 0; s < a.nsrc; ++s) {
+#endif
     roff[s] = ro;
     const int sd = a.sd[s], sh = a.sh[s], sw = a.sw[s];
     int z0, z1, y0, y1;
@@ -521,7 +532,11 @@ __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
       const int c4 = min(gl + j * G, C4 - 1);
       const f32x4 o = (x == xf ? scp[j] : sc[c4]) + acc[j] * bs;
       v[j] = live[j] ? o : f32x4{0, 0, 0, 0};
+#if MSF_DBG
+      if (live[j] && (!(a.dbg & 1) || o.x == 1234.5f)) dst[c4] = o;
+#else
       if (live[j]) dst[c4] = o;
+#endif
     }
     if (a.stats) {
       float mean, rstd;
@@ -693,6 +708,7 @@ extern "C" int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, in
   a.D = (int)D;
   a.H = (int)H;
   a.W = (int)W;
+  a.dbg = MSF_DBG && getenv("MSF_DBG") ? atoi(getenv("MSF_DBG")) : 0;
   const int64_t total = B * D * H * W;
   int64_t rlds = 0;
   for (int s = 0; s < nsrc; ++s) rlds += (int64_t)a.sw[s] * C * 4;
