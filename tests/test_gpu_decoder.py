@@ -611,3 +611,75 @@ def test_dwconv3d_fused_channel_stats(B, C_, S):
     assert C.rel_l2(st, ref) <= 1e-6
     want = F.conv3d(x.contiguous(), w, b, padding=1, groups=C_)
     assert C.rel_l2(y1, want) <= 1e-6
+
+
+
+
+# (precision, Cin, Cout, (B, D, H, W), fp16 input, statistics): shapes that take the wide-chunk
+# kernel (W > 32, Cout % 48 == 0, >= 512 workgroups of the 4-row plan; every Cin with
+# WF_CONV_WIDE_MINCIN=1); Cin 40 / 104 = an odd number of 8-channel chunks, Cout 96 = two column
+# blocks, W 70 / 100 = ragged x tiles
+_WIDE_CASES = (("fp16", 96, 48, (2, 24, 32, 70), False, True),
+               ("bf16", 48, 96, (1, 32, 24, 100), False, False),
+               ("fp16", 40, 48, (2, 32, 32, 36), False, True),
+               ("fp16", 48, 48, (2, 64, 48, 40), True, True),
+               ("bf16x3", 96, 48, (2, 24, 32, 70), False, True),
+               ("bf16x3", 104, 96, (1, 20, 40, 100), False, False))
+_WIDE_CHILD = r"""
+import sys, torch
+sys.path.insert(0, '.')
+from tests.test_gpu_decoder import _wide_outputs
+torch.save(_wide_outputs(), sys.argv[1])
+print("WIDE_CHILD_OK")
+"""
+
+
+def _wide_outputs():
+    from waveformer_amd import ops
+    outs = []
+    for i, (prec, cin, cout, shp, xh, stats) in enumerate(_WIDE_CASES):
+        B, D, H, W = shp
+        x = (seeded_randn((B, cin, D, H, W), 150 + i) + 0.25).cuda()
+        x = x.contiguous(memory_format=torch.channels_last_3d)
+        if xh:
+            x = x.half().contiguous(memory_format=torch.channels_last_3d)
+        w = (seeded_randn((cout, cin, 3, 3, 3), 160 + i) * (cin * 27) ** -0.5).cuda()
+        b = seeded_randn((cout,), 170 + i).cuda()
+        with ops.precision(prec):
+            r = ops.conv3d_k3(x, w, b, norm_eps=1e-5 if stats else None)
+        outs.append(tuple(t.cpu() for t in r) if stats else (r.cpu(),))
+    return outs
+
+
+def _wide_child(tmp_path, name, **env_over):
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dst = str(tmp_path / name)
+    env = dict(os.environ, PYTHONPATH=repo, **env_over)
+    r = subprocess.run([sys.executable, "-c", _WIDE_CHILD, dst], cwd=repo, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "WIDE_CHILD_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+    return torch.load(dst, weights_only=True)
+
+
+def test_conv3d_k3_wide_chunks_bitwise(tmp_path):
+    """conv3d_k3w_kernel (16 channels per 64-B load, 8-wave workgroups of 8 x 64 outputs; one
+    8-channel chunk's hi / lo per step under bf16x3) runs each output's K reduction in the
+    8-channel kernels' order on the same operands: outputs bitwise equal to WF_CONV_WIDE=0, the
+    fused InstanceNorm statistics equal to fp32 summation-order level (both sides in child
+    processes: the switches are read once per process); the fp64 CPU convolution at the bars."""
+    wide = _wide_child(tmp_path, "wide.pt", WF_CONV_WIDE="1", WF_CONV_WIDE_MINCIN="1")
+    narrow = _wide_child(tmp_path, "narrow.pt", WF_CONV_WIDE="0")
+    for case, g, want in zip(_WIDE_CASES, wide, narrow):
+        assert torch.equal(g[0], want[0]), (case, float((g[0] - want[0]).abs().max()))
+        if len(g) > 1:
+            assert C.rel_l2(g[1], want[1]) <= 1e-6, case
+    for i in (1, 5):  # bf16 and bf16x3 against the fp64 convolution
+        prec, cin, cout, (B, D, H, W), _, _ = _WIDE_CASES[i]
+        x = seeded_randn((B, cin, D, H, W), 150 + i) + 0.25
+        w = seeded_randn((cout, cin, 3, 3, 3), 160 + i) * (cin * 27) ** -0.5
+        b = seeded_randn((cout,), 170 + i)
+        want = F.conv3d(x.double(), w.double(), b.double(), padding=1)
+        assert C.rel_l2(wide[i][0], want) <= (1e-5 if prec == "bf16x3" else 1e-2), prec

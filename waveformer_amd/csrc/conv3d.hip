@@ -31,6 +31,10 @@
 
 namespace wf {
 
+#ifndef WF_CONV_DBG  // 1: timing-experiment build (Conv3Args::dbg phase skips; never the shipped library)
+#define WF_CONV_DBG 0
+#endif
+
 constexpr int kConvCC = 8;                           // input channels per LDS chunk
 constexpr int kConvKS = (27 * kConvCC + 31) / 32;    // K-steps of 32 per chunk (7)
 
@@ -53,6 +57,8 @@ struct Conv3Args {
   int zfirst;         // tile order: z fastest (1) or x fastest (0)
   const uint16_t* xh; // XH kernels: the input as fp16 (the operands WF_PREC_FP16 stages; same
                       // positions / ldx as x)
+  int dbg;            // WF_CONV_DBG builds: 1 no activation loads, 2 no activation LDS stores,
+                      // 4 no weight loads, 8 no weight LDS stores, 16 no MFMA K loop
 };
 
 // RW output rows per wave (wave w: rows w, w + 4, ...): RW = 2 halves the weight-fragment LDS
@@ -165,6 +171,15 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
     // channels past Cin (the last chunk when Cin % 8 != 0) read channel 0 instead: the
     // address stays inside the tensor, commit() zeroes the value
     const int c = ch * kConvCC + 4 * q;
+#if WF_CONV_DBG
+    if (a.dbg & 1) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (XH) sah[j] = bf16x4{(short)ch, 0, 0, 0};
+        else sa[j] = f32x4{(float)ch, 0.f, 0.f, 0.f};
+      }
+    } else
+#endif
     if constexpr (XH) {
       const uint16_t* xs = a.xh + (c < a.Cin ? c : 0);
 #pragma unroll
@@ -174,6 +189,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) sa[j] = *reinterpret_cast<const f32x4*>(xs + goff[j]);
     }
+#if WF_CONV_DBG
+    if (a.dbg & 4) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sw[w] = bf16x8{(short)ch, 0, 0, 0, 0, 0, 0, 0};
+      return;
+    }
+#endif
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const int i = min(tid + 256 * w, NFRAG * 64 - 1);
@@ -186,8 +208,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   };
   auto commit = [&](int ch) {
     const bool cok = ch * kConvCC + 4 * q < a.Cin;
+#if WF_CONV_DBG
+    const bool skip_a = a.dbg & 2, skip_w = a.dbg & 8;
+#else
+    constexpr bool skip_a = false, skip_w = false;
+#endif
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
+    for (int j = 0; j < NJ && !skip_a; ++j) {
       const int pos = p0 + PSTEP * j;
       if (j == NJ - 1 && pos >= NPOS) break;
       if constexpr (XH) {
@@ -209,7 +236,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
       if (SPLIT) *reinterpret_cast<bf16x4*>(s_lo + pos * PS + 4 * q) = l;
     }
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
+    for (int w = 0; w < NW && !skip_w; ++w) {
       const int i = tid + 256 * w;
       if (w == NW - 1 && i >= NFRAG * 64) break;
       *reinterpret_cast<bf16x8*>(s_w + i * 8) = sw[w];
@@ -225,6 +252,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
     __syncthreads();
     // the next chunk's global reads fly during this chunk's MFMAs: no vmcnt wait below
     if (ch + 1 < ch_end) fetch(ch + 1);
+#if WF_CONV_DBG
+    if (a.dbg & 16) {
+      // keep the staged values live (so the loads / stores are not removed) without MFMAs
+      acc[0][0][0].x += (float)lb[tid & 63] + (float)lw[0];
+      continue;
+    }
+#endif
 #pragma unroll
     for (int s = 0; s < kConvKS; ++s) {
       bf16x8 wh[CO_T], wl[CO_T];
@@ -343,6 +377,316 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Wide-chunk variant (non-split operands, W > 32, Cout % 48 == 0; round 5).  Phase removal in
+// the WF_CONV_DBG build (profiles/r5_conv_phase_skip.txt) put 39 % of the 96 -> 48 fp16 launch
+// on the activation LOADS alone: an 8-channel chunk reads 32 B of every halo position, one
+// quarter of a 128-B line, and the next chunk's quarter comes back through L2 again -- the
+// kernel is bound by L2 -> CU line traffic, not by MFMA or LDS.  Here a workgroup of 8 waves
+// owns an 8-row x 64-column tile (wave w = row w) and stages 16 channels per step (64 B of
+// every fp32 position, 32 B fp16), as two 8-channel K sub-chunks of 7 steps each behind one
+// barrier pair:
+//   * half the line traffic per staged byte, 3.9 instead of 4.6 halo positions per output,
+//     and each weight chunk in LDS serves 512 outputs instead of 256;
+//   * activations [position][16 ch] (32 B) with 16 B of padding after every 8 positions, so a
+//     ds_read_b128 over 16 consecutive positions touches 16 distinct 4-bank groups;
+//   * one workgroup per CU (108 KB of LDS), 2 waves per SIMD as before.
+// The arithmetic per output is the 8-channel kernel's (same K order, same operands): outputs
+// are bitwise those of conv3d_k3_kernel (tests/test_gpu_decoder.py).
+//
+// PREC_SPLIT (bf16 hi + lo operands): the same 16-channel (64-B) loads, but a position's 32 B
+// of LDS hold the hi and lo halves of ONE 8-channel chunk, so a load feeds two steps: lanes
+// q = 0, 1 commit the first chunk, q = 2, 3 the second, and the next load is issued after the
+// second commit.  The weight step is one chunk's 7 K-steps x {hi, lo} fragments.
+template <int P, bool XH>
+__global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
+  constexpr bool SPLIT = P == PREC_SPLIT;
+  static_assert(!XH || P == PREC_FP16, "fp16 input only with fp16 operands");
+  constexpr int CO_T = 3, NT = 4, NWV = 8;
+  constexpr int TX = 16 * NT, TY = NWV, HX = TX + 2, HY = TY + 2;
+  constexpr int NPOS = 3 * HY * HX;                  // 1980 halo positions
+  constexpr int CW = 2 * kConvCC;                    // 16 channels staged per step
+  constexpr int PB = CW * 2;                         // 32 B per position
+  constexpr int NFRAG = 2 * kConvKS * CO_T;          // 42 weight fragments per step
+  constexpr int NW = (NFRAG * 64 + 511) / 512;       // 16-B weight pieces per thread
+  constexpr int QN = XH ? CW / 8 : CW / 4;           // lanes per position (16 B each)
+  constexpr int PSTEP = 512 / QN;
+  constexpr int NJ = (NPOS * QN + 511) / 512;
+  constexpr int ACT_B = NPOS * PB + (NPOS / 8 + 1) * 16;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  char* s_act = reinterpret_cast<char*>(lds);
+  uint16_t* s_w = reinterpret_cast<uint16_t*>(s_act + ACT_B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  auto paddr = [](int p) { return p * PB + (p >> 3) * 16; };  // byte offset of position p
+
+  int64_t t = blockIdx.x;
+  if ((a.nblocks & 7) == 0) t = (t & 7) * (a.nblocks >> 3) + (t >> 3);
+  int tx, ty, z, b;
+  if (a.zfirst) {
+    z = (int)(t % a.D);
+    t /= a.D;
+    tx = (int)(t % a.tiles_x);
+    t /= a.tiles_x;
+    ty = (int)(t % a.tiles_y);
+    b = (int)(t / a.tiles_y);
+  } else {
+    tx = (int)(t % a.tiles_x);
+    t /= a.tiles_x;
+    ty = (int)(t % a.tiles_y);
+    t /= a.tiles_y;
+    z = (int)(t % a.D);
+    b = (int)(t / a.D);
+  }
+  const int x0 = tx * TX, y0 = ty * TY;
+  const int co0 = blockIdx.y * (16 * CO_T);
+
+  f32x4 acc[CO_T][NT];
+#pragma unroll
+  for (int m = 0; m < CO_T; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0, 0, 0, 0};
+
+  // B fragment of K-step s (sub-chunk 0): tap (32 s + 8 g4) / 8 at halo position (tap's z,
+  // wid + tap's y, l15 + tap's x) + 16 n; sub-chunk 1 reads the 16 B after it
+  // (16 positions later = 2 padded groups later: paddr(p + 16 n) = paddr(p) + 544 n)
+  uint32_t boff[kConvKS];
+#pragma unroll
+  for (int s = 0; s < kConvKS; ++s) {
+    const int tap = min((32 * s + 8 * g4) / kConvCC, 26);
+    const int tz = tap / 9, tyy = (tap / 3) % 3, txx = tap % 3;
+    boff[s] = (uint32_t)paddr((tz * HY + wid + tyy) * HX + txx + l15);
+  }
+  const int q = tid % QN, p0 = tid / QN;
+  uint32_t goff[NJ];
+  uint32_t gmask = 0;
+  {
+    const int64_t plane = (int64_t)a.H * a.W;
+    const int64_t sample = (int64_t)b * a.D * plane;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int pos = min(p0 + PSTEP * j, NPOS - 1);
+      const int hx = pos % HX, r = pos / HX;
+      const int hy = r % HY, hz = r / HY;
+      const int gz = z + hz - 1, gy = y0 + hy - 1, gx = x0 + hx - 1;
+      const bool ok = p0 + PSTEP * j < NPOS && gz >= 0 && gz < a.D && gy >= 0 && gy < a.H &&
+                      gx >= 0 && gx < a.W;
+      const int cz = min(max(gz, 0), a.D - 1), cy = min(max(gy, 0), a.H - 1),
+                cx = min(max(gx, 0), a.W - 1);
+      goff[j] = (uint32_t)((sample + cz * plane + (int64_t)cy * a.W + cx) * a.ldx);
+      gmask |= ok ? (1u << j) : 0u;
+    }
+  }
+  const int64_t cblk = a.Cout / 16;
+  // steps: 16 channels each (the last may hold one 8-channel chunk); SPLIT: one chunk each
+  const int nst = SPLIT ? a.nch : (a.nch + 1) / 2;
+
+  f32x4 sa[XH ? 1 : NJ];
+  bf16x8 sah[XH ? NJ : 1];
+  bf16x8 sw[NW];
+  // activations of step st (SPLIT: of steps st, st + 1, st even)
+  auto fetch_act = [&](int st) {
+    // channels past Cin read channel 0 (in range); commit() zeroes them
+    const int c = (SPLIT ? st / 2 : st) * CW + (XH ? 8 : 4) * q;
+    if constexpr (XH) {
+      const uint16_t* xs = a.xh + (c < a.Cin ? c : 0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) sah[j] = *reinterpret_cast<const bf16x8*>(xs + goff[j]);
+    } else {
+      const float* xs = a.x + (c < a.Cin ? c : 0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) sa[j] = *reinterpret_cast<const f32x4*>(xs + goff[j]);
+    }
+  };
+  // weight fragments of step st: f = (sub * 7 + step) * CO_T + m for chunks 2 st, 2 st + 1 (a
+  // missing second chunk, odd nch, reads the first one's: never used); SPLIT: f = (step * 2 +
+  // plane) * CO_T + m of chunk st, the packed order
+  auto fetch_w = [&](int st) {
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int i = min(tid + 512 * w, NFRAG * 64 - 1);
+      const int f = i >> 6, ln = i & 63;
+      const int m = f % CO_T, ss = f / CO_T;
+      int64_t frag;
+      if constexpr (SPLIT) {
+        frag = ((int64_t)st * kConvKS * 2 + ss) * cblk + co0 / 16 + m;
+      } else {
+        const int sub = ss / kConvKS, step = ss - sub * kConvKS;
+        const int ch = min(2 * st + sub, a.nch - 1);
+        frag = ((int64_t)(ch * kConvKS + step) * 2) * cblk + co0 / 16 + m;
+      }
+      sw[w] = *reinterpret_cast<const bf16x8*>(a.w + (frag * 64 + ln) * 8);
+    }
+  };
+  auto fetch = [&](int st) {
+    if (!SPLIT || (st & 1) == 0) fetch_act(st);
+    fetch_w(st);
+  };
+  auto commit = [&](int st) {
+    const int c = (SPLIT ? st / 2 : st) * CW + (XH ? 8 : 4) * q;
+    const bool cok = c < a.Cin;
+    // SPLIT: this step's chunk is held by lanes q >> 1 == st & 1 (uniform per 2 lanes)
+    const bool mine = !SPLIT || (q >> 1) == (st & 1);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int pos = p0 + PSTEP * j;
+      if (j == NJ - 1 && pos >= NPOS) break;
+      const bool ok = cok && ((gmask >> j) & 1u);
+      if constexpr (SPLIT) {
+        if (mine) {
+          const f32x4 v = ok ? sa[j] : f32x4{0, 0, 0, 0};
+          bf16x4 h, l;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint16_t hb = op_cvt<P>(v[e]);
+            h[e] = (short)hb;
+            l[e] = op_lo<P>(v[e], hb);
+          }
+          *reinterpret_cast<bf16x4*>(s_act + paddr(pos) + 8 * (q & 1)) = h;
+          *reinterpret_cast<bf16x4*>(s_act + paddr(pos) + 16 + 8 * (q & 1)) = l;
+        }
+      } else if constexpr (XH) {
+        const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+        *reinterpret_cast<bf16x8*>(s_act + paddr(pos) + 16 * q) = ok ? sah[j] : z8;
+      } else {
+        const f32x4 v = ok ? sa[j] : f32x4{0, 0, 0, 0};
+        bf16x4 h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[e] = (short)op_cvt<P>(v[e]);
+        *reinterpret_cast<bf16x4*>(s_act + paddr(pos) + 8 * q) = h;
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int i = tid + 512 * w;
+      if (w == NW - 1 && i >= NFRAG * 64) break;
+      *reinterpret_cast<bf16x8*>(s_w + i * 8) = sw[w];
+    }
+  };
+  const char* lw = reinterpret_cast<const char*>(s_w) + lane * 16;
+
+  fetch(0);
+  for (int st = 0; st < nst; ++st) {
+    __syncthreads();  // every wave is done with the previous step's LDS
+    commit(st);
+    __syncthreads();
+    if (st + 1 < nst) fetch(st + 1);
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int s = 0; s < kConvKS; ++s) {
+        bf16x8 wh[CO_T], wl[CO_T];
+#pragma unroll
+        for (int m = 0; m < CO_T; ++m) {
+          wh[m] = *reinterpret_cast<const bf16x8*>(lw + ((s * 2 + 0) * CO_T + m) * 1024);
+          wl[m] = *reinterpret_cast<const bf16x8*>(lw + ((s * 2 + 1) * CO_T + m) * 1024);
+        }
+        bf16x8 bh[NT], bl[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          bh[n] = *reinterpret_cast<const bf16x8*>(s_act + boff[s] + 544 * n);
+          bl[n] = *reinterpret_cast<const bf16x8*>(s_act + boff[s] + 544 * n + 16);
+        }
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int m = 0; m < CO_T; ++m) {
+            acc[m][n] = mma32<P>(wh[m], bl[n], acc[m][n]);
+            acc[m][n] = mma32<P>(wl[m], bh[n], acc[m][n]);
+            acc[m][n] = mma32<P>(wh[m], bh[n], acc[m][n]);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;
+    }
+    const int nsub = 2 * st + 1 < a.nch ? 2 : 1;
+    for (int sub = 0; sub < nsub; ++sub) {
+#pragma unroll
+      for (int s = 0; s < kConvKS; ++s) {
+        bf16x8 wh[CO_T];
+#pragma unroll
+        for (int m = 0; m < CO_T; ++m)
+          wh[m] = *reinterpret_cast<const bf16x8*>(lw + ((sub * kConvKS + s) * CO_T + m) * 1024);
+        bf16x8 bh[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          bh[n] = *reinterpret_cast<const bf16x8*>(s_act + boff[s] + 544 * n + 16 * sub);
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int m = 0; m < CO_T; ++m) acc[m][n] = mma32<P>(wh[m], bh[n], acc[m][n]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+  // InstanceNorm statistics (as conv3d_k3_kernel, over 8 waves)
+  if (a.stats) {
+    f32x4 ps[CO_T], pq[CO_T];
+    const bool rowok = y0 + wid < a.H;
+#pragma unroll
+    for (int m = 0; m < CO_T; ++m) {
+      ps[m] = f32x4{0, 0, 0, 0};
+      pq[m] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const bool ok = rowok && x0 + 16 * n + l15 < a.W;
+        f32x4 v = acc[m][n];
+        if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + co0 + 16 * m + 4 * g4);
+        if (ok) {
+          ps[m] += v;
+          pq[m] += v * v;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ps[m][i] = group_sum<16>(ps[m][i]);
+        pq[m][i] = group_sum<16>(pq[m][i]);
+      }
+    }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // [8 waves][CO_T * 16][2]
+    if (l15 == 0) {
+#pragma unroll
+      for (int m = 0; m < CO_T; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 16 * m + 4 * g4 + i;
+          red[(wid * CO_T * 16 + c) * 2 + 0] = ps[m][i];
+          red[(wid * CO_T * 16 + c) * 2 + 1] = pq[m][i];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < CO_T * 16 * 2; i += 512) {
+      const int c = i >> 1, mom = i & 1;
+      float tt = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) tt += red[(w * CO_T * 16 + c) * 2 + mom];
+      atomicAdd(a.stats + ((int64_t)b * a.Cout + co0 + c) * 2 + mom, (double)tt);
+    }
+  }
+
+  const int gy = y0 + wid;
+  if (gy >= a.H) return;
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int gx = x0 + 16 * n + l15;
+    if (gx >= a.W) continue;
+    float* o = a.out + (((int64_t)(b * a.D + z) * a.H + gy) * a.W + gx) * a.ldo;
+#pragma unroll
+    for (int m = 0; m < CO_T; ++m) {
+      const int co = co0 + 16 * m + 4 * g4;
+      f32x4 v = acc[m][n];
+      if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + co);
+      *reinterpret_cast<f32x4*>(o + co) = v;
+    }
+  }
+}
+
+static size_t conv3w_lds() {
+  constexpr int NPOS = 3 * 10 * 66;
+  return (size_t)NPOS * 32 + (NPOS / 8 + 1) * 16 + (size_t)2 * kConvKS * 3 * 1024;
+}
+
 // out[p][c] = sum_z part[z][p][c], z ascending (the split-K partials, bias in part[0])
 __global__ void splitk_sum_kernel(const float* __restrict__ part, float* __restrict__ out,
                                   int64_t ldo, int C, int64_t P, int ksplit) {
@@ -364,6 +708,37 @@ inline int conv3_ksplit(int64_t wgs, int nch) {
   return (wgs < 512 && nch > 1) ? (int)std::min<int64_t>(nch, cdiv(1024, wgs)) : 1;
 }
 
+// the wide-chunk kernel (conv3d_k3w_kernel): fp16 / bf16 operands, Cout % 48 == 0, W > 32, no
+// split-K; WF_CONV_WIDE=0 keeps the 8-channel kernels
+static bool conv3w_ok(const Conv3Args& a, int prec, int64_t wgs) {
+  static const bool on = !getenv("WF_CONV_WIDE") || getenv("WF_CONV_WIDE")[0] != '0';
+  // Cin > 88: at 48 input channels (3 steps per tile) the exposed per-tile prologue of the one
+  // workgroup per CU costs more than the wider loads save (profiles/r5_conv_wide_ab.txt)
+  static const int min_cin = getenv("WF_CONV_WIDE_MINCIN") ? atoi(getenv("WF_CONV_WIDE_MINCIN")) : 89;
+  return on && a.Cout % 48 == 0 && a.W > 32 && wgs >= 512 && a.Cin >= min_cin &&
+         (!a.xh || a.Cin % 8 == 0);
+}
+
+static int launch_conv3w(const Conv3Args& a0, int prec, hipStream_t stream) {
+  Conv3Args a = a0;
+  a.tiles_x = (int)cdiv(a.W, 64);
+  a.tiles_y = (int)cdiv(a.H, 8);
+  a.nblocks = (int64_t)a.B * a.D * a.tiles_y * a.tiles_x;
+  if (a.nblocks >= ((int64_t)1 << 31)) return fail(WF_E_SHAPE, "wf_conv3d_k3_fwd: too many tiles");
+  a.ksplit = 1;
+  static const int zf = getenv("WF_CONV_ZFIRST") ? atoi(getenv("WF_CONV_ZFIRST")) : 1;
+  a.zfirst = zf;
+  auto kern = a.xh ? conv3d_k3w_kernel<PREC_FP16, true>
+              : prec == PREC_SPLIT ? conv3d_k3w_kernel<PREC_SPLIT, false>
+              : prec == PREC_FP16 ? conv3d_k3w_kernel<PREC_FP16, false>
+                                  : conv3d_k3w_kernel<PREC_BF16, false>;
+  const size_t lds = conv3w_lds();
+  set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)a.nblocks, (unsigned)(a.Cout / 48), 1), dim3(512), lds,
+                     stream, a);
+  return check_launch("wf_conv3d_k3_fwd (wide chunks)");
+}
+
 template <int CO_T, int NT, int RW = 1>
 static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   Conv3Args a = a0;
@@ -383,15 +758,23 @@ static int launch_conv3(const Conv3Args& a0, int prec, hipStream_t stream) {
   const int64_t wgs = a.nblocks * (a.Cout / (16 * CO_T));
   a.nblocks_pos = (int64_t)a.B * a.D * a.H * a.W;
   a.ksplit = a.part ? conv3_ksplit(wgs, a.nch) : 1;
+  if (a.ksplit == 1 && conv3w_ok(a, prec, wgs)) return launch_conv3w(a0, prec, stream);
   dim3 grid((unsigned)a.nblocks, (unsigned)(a.Cout / (16 * CO_T)), (unsigned)a.ksplit);
   const bool post_stats = a.stats && a.ksplit > 1;  // partial outputs: a separate pass below
   static const int zf = getenv("WF_CONV_ZFIRST") ? atoi(getenv("WF_CONV_ZFIRST")) : 1;
   a.zfirst = zf;
+  a.dbg = WF_CONV_DBG && getenv("WF_CONV_DBG") ? atoi(getenv("WF_CONV_DBG")) : 0;
+  // WF_CONV_PIPE=1 (A/B): non-split kernels without the per-K-step scheduling fence, so the
+  // next step's fragment reads can be issued under the current step's MFMAs
+  static const bool pipe = getenv("WF_CONV_PIPE") && getenv("WF_CONV_PIPE")[0] == '1';
   {
-    auto kern = a.xh                ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, false, RW, true>
+    auto kern = a.xh                ? (pipe ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, true, RW, true>
+                                            : conv3d_k3_kernel<CO_T, NT, PREC_FP16, false, RW, true>)
                 : prec == PREC_SPLIT  ? conv3d_k3_kernel<CO_T, NT, PREC_SPLIT, false, 1>
-                : prec == PREC_FP16 ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, false, RW>
-                                    : conv3d_k3_kernel<CO_T, NT, PREC_BF16, false, RW>;
+                : prec == PREC_FP16 ? (pipe ? conv3d_k3_kernel<CO_T, NT, PREC_FP16, true, RW>
+                                            : conv3d_k3_kernel<CO_T, NT, PREC_FP16, false, RW>)
+                                    : (pipe ? conv3d_k3_kernel<CO_T, NT, PREC_BF16, true, RW>
+                                            : conv3d_k3_kernel<CO_T, NT, PREC_BF16, false, RW>);
     set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
   }
