@@ -17,6 +17,7 @@ SHAPES = [  # (precision, B, Cin, Cout, S, fp16 input)
 ]
 ITERS = int(os.environ.get("ITERS", "6"))
 ONLY = os.environ.get("ONLY")  # comma-separated shape indices
+EPS = None if os.environ.get("STATS", "1") == "0" else 1e-5  # fused InstanceNorm statistics
 for i, (prec, B, cin, cout, s, xh) in enumerate(SHAPES):
     if ONLY and str(i) not in ONLY.split(","):
         continue
@@ -26,12 +27,12 @@ for i, (prec, B, cin, cout, s, xh) in enumerate(SHAPES):
     w = torch.randn(cout, cin, 3, 3, 3, device="cuda") * (cin * 27) ** -0.5
     b = torch.randn(cout, device="cuda")
     with ops.precision(prec):
-        ops.conv3d_k3(x, w, b, norm_eps=1e-5)
+        ops.conv3d_k3(x, w, b, norm_eps=EPS)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(ITERS):
-            ops.conv3d_k3(x, w, b, norm_eps=1e-5)
+            ops.conv3d_k3(x, w, b, norm_eps=EPS)
         e1.record()
         torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / ITERS * 1e3
