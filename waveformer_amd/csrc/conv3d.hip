@@ -488,6 +488,16 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
   auto fetch_act = [&](int st) {
     // channels past Cin read channel 0 (in range); commit() zeroes them
     const int c = (SPLIT ? st / 2 : st) * CW + (XH ? 8 : 4) * q;
+#if WF_CONV_DBG
+    if (a.dbg & 1) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (XH) sah[j] = bf16x8{(short)st, 0, 0, 0, 0, 0, 0, 0};
+        else sa[j] = f32x4{(float)st, 0.f, 0.f, 0.f};
+      }
+      return;
+    }
+#endif
     if constexpr (XH) {
       const uint16_t* xs = a.xh + (c < a.Cin ? c : 0);
 #pragma unroll
@@ -502,6 +512,13 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
   // missing second chunk, odd nch, reads the first one's: never used); SPLIT: f = (step * 2 +
   // plane) * CO_T + m of chunk st, the packed order
   auto fetch_w = [&](int st) {
+#if WF_CONV_DBG
+    if (a.dbg & 4) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sw[w] = bf16x8{(short)st, 0, 0, 0, 0, 0, 0, 0};
+      return;
+    }
+#endif
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const int i = min(tid + 512 * w, NFRAG * 64 - 1);
@@ -527,8 +544,13 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
     const bool cok = c < a.Cin;
     // SPLIT: this step's chunk is held by lanes q >> 1 == st & 1 (uniform per 2 lanes)
     const bool mine = !SPLIT || (q >> 1) == (st & 1);
+#if WF_CONV_DBG
+    const bool skip_a = a.dbg & 2, skip_w = a.dbg & 8;
+#else
+    constexpr bool skip_a = false, skip_w = false;
+#endif
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
+    for (int j = 0; j < NJ && !skip_a; ++j) {
       const int pos = p0 + PSTEP * j;
       if (j == NJ - 1 && pos >= NPOS) break;
       const bool ok = cok && ((gmask >> j) & 1u);
@@ -557,7 +579,7 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
       }
     }
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
+    for (int w = 0; w < NW && !skip_w; ++w) {
       const int i = tid + 512 * w;
       if (w == NW - 1 && i >= NFRAG * 64) break;
       *reinterpret_cast<bf16x8*>(s_w + i * 8) = sw[w];
@@ -571,6 +593,12 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
     commit(st);
     __syncthreads();
     if (st + 1 < nst) fetch(st + 1);
+#if WF_CONV_DBG
+    if (a.dbg & 16) {
+      acc[0][0].x += (float)s_act[tid & 63] + (float)lw[0];
+      continue;
+    }
+#endif
     if constexpr (SPLIT) {
 #pragma unroll
       for (int s = 0; s < kConvKS; ++s) {
@@ -728,6 +756,7 @@ static int launch_conv3w(const Conv3Args& a0, int prec, hipStream_t stream) {
   a.ksplit = 1;
   static const int zf = getenv("WF_CONV_ZFIRST") ? atoi(getenv("WF_CONV_ZFIRST")) : 1;
   a.zfirst = zf;
+  a.dbg = WF_CONV_DBG && getenv("WF_CONV_DBG") ? atoi(getenv("WF_CONV_DBG")) : 0;
   auto kern = a.xh ? conv3d_k3w_kernel<PREC_FP16, true>
               : prec == PREC_SPLIT ? conv3d_k3w_kernel<PREC_SPLIT, false>
               : prec == PREC_FP16 ? conv3d_k3w_kernel<PREC_FP16, false>
