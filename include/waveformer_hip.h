@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 14
+#define WF_ABI_VERSION 15
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
@@ -99,6 +99,13 @@ int wf_patch_embed_fwd(const float* x, const float* w, const float* bias, float*
 int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float* ln_b, float ln_eps,
                       float* bands, int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
                       void* stream);
+/* The LL band alone (ABI 15): ll (B, D/2, H/2, W/2, C) bitwise equal to band 0 of
+ * wf_dwt3d_haar_fwd.  For a Block whose detail bands nobody reads (wave_helper.py:509 keeps
+ * only the LAST block's hf of each stage, waveformer.py:288-292): the 7 detail stores are
+ * dropped, 8/9 of the launch's writes.                                                     */
+int wf_dwt3d_haar_fwd_ll(const float* x, const float* ln_w, const float* ln_b, float ln_eps,
+                         float* ll, int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                         void* stream);
 
 /* ---- a11: multi-level Haar synthesis ------------------------------------------------- */
 /* Replaces ptwt.waverec3((LL,) + hf, 'db1') at network_models/idwt_upsample.py:160 and the

@@ -65,6 +65,64 @@ def test_dwt_haar_vs_oracle(C_, ln):
         assert C.rel_l2(det[k], det_ref[k]) <= 1e-5, k
 
 
+@pytest.mark.parametrize("C_", [8, 48, 96, 192, 40])
+@pytest.mark.parametrize("ln", [False, True])
+def test_dwt_haar_ll_only_bitwise(C_, ln):
+    """wf_dwt3d_haar_fwd_ll (the Blocks whose detail bands are discarded) is bitwise band 0 of
+    the 8-band kernel, with and without the fused norm1."""
+    from waveformer_amd import ops
+    x = cuda(seeded_randn((2, 8, 6, 10, C_), 11) * 3 + 0.5)
+    lnp = (cuda(seeded_randn((C_,), 12) * 0.2 + 1), cuda(seeded_randn((C_,), 13) * 0.1), 1e-6)
+    bands = ops.dwt3d_haar(x, lnp if ln else None)
+    ll = ops.dwt3d_haar_ll(x, lnp if ln else None)
+    assert ll.shape == bands[0].shape and torch.equal(ll, bands[0])
+
+
+def test_encoder_block_hf_skip_keeps_outputs():
+    """The encoder runs every Block but a stage's last on the LL-only DWT in inference; its
+    outputs and the returned hf dicts (the last Blocks') equal a run that computes every
+    Block's detail bands (the flag forced off), bitwise."""
+    import waveformer_amd.network_models as NM
+    from waveformer_amd.network_models import wave_helper as WH
+    torch.manual_seed(0)
+    m = NM.MultiscaleTransformer(img_size=(32, 32, 32), in_chans=4,
+                                 num_heads=[1, 1, 1, 1]).eval().to(DEV)
+    x = cuda(seeded_randn((1, 4, 32, 32, 32), 14))
+    with torch.no_grad():
+        outs, hf = m(x)
+        orig = WH.Block._ll_levels
+        calls = []
+
+        def spy(self, *a):
+            calls.append(1)
+            return orig(self, *a)
+        WH.Block._ll_levels = spy
+        try:
+            m(x)
+        finally:
+            WH.Block._ll_levels = orig
+        assert calls, "the LL-only path did not run"
+        saved = WH.Block.__dict__["_hf_unused"]
+
+        class _Never:  # forces the flag off for every Block: the full 8-band DWT everywhere
+            def __get__(self, obj, typ=None):
+                return False
+
+            def __set__(self, obj, v):
+                pass
+        WH.Block._hf_unused = _Never()
+        try:
+            outs2, hf2 = m(x)
+        finally:
+            WH.Block._hf_unused = saved
+    for a, b in zip(outs, outs2):
+        assert torch.equal(a, b)
+    for da, db in zip(hf, hf2):
+        for ta, tb in zip(da, db):
+            for k in ta:
+                assert torch.equal(ta[k], tb[k]), k
+
+
 @pytest.mark.parametrize("levels,C_,base", [(1, 192, (2, 2, 2)), (2, 96, (2, 3, 2)),
                                             (3, 48, (1, 2, 2)), (3, 8, (2, 2, 2)),
                                             (4, 16, (1, 1, 1))])

@@ -33,6 +33,7 @@ SIGNATURES = {
     "wf_debug_poison_lds": (_I, [_I64, _I, _P]),
     "wf_patch_embed_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwt3d_haar_fwd": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
+    "wf_dwt3d_haar_fwd_ll": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar": (_I, [_P, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_idwt3d_haar_cl": (_I, [_P, _I64, _I64, _I64, _P, _P, _I, _P, _I64, _I64, _I64, _I64,
                                _I64, _I64, _I64, _P]),
@@ -129,7 +130,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 _lock = threading.Lock()
 _lib = None
 _err = None

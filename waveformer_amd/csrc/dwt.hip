@@ -18,7 +18,9 @@ constexpr float kHaar3 = 0.35355339059327373f;  // (1/sqrt 2)^3
 
 // Forward: one row group per OUTPUT position; lanes over channels.
 // x (B,D,H,W,C) channel-last -> bands (8,B,D/2,H/2,W/2,C); band k bits (bd,bh,bw) = k>>2,k>>1,k.
-template <int G, int V, bool LN>
+// NB = 8: all bands; NB = 1: the LL band alone (the detail butterflies are dead code then;
+// band 0's sums are formed in the same order, so LL is bitwise the 8-band kernel's)
+template <int G, int V, bool LN, int NB = 8>
 __global__ __launch_bounds__(256) void dwt3d_haar_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ ln_w, const float* __restrict__ ln_b,
     float ln_eps, float* __restrict__ bands, int B, int C, int D, int H, int W) {
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256) void dwt3d_haar_fwd_kernel(
     }
     const int64_t obase = g * C;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < NB; ++k) {
       f32x4* dst = reinterpret_cast<f32x4*>(bands + k * band_stride + obase);
 #pragma unroll
       for (int j = 0; j < V; ++j)
@@ -407,9 +409,10 @@ __global__ __launch_bounds__(256) void idwt3d_haar_nc4_kernel(IdwtArgs a) {
 
 using namespace wf;
 
-extern "C" int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float* ln_b,
-                                 float ln_eps, float* bands, int64_t B, int64_t C, int64_t D,
-                                 int64_t H, int64_t W, void* stream) {
+template <int NB>
+static int dwt_haar_fwd(const float* x, const float* ln_w, const float* ln_b, float ln_eps,
+                        float* bands, int64_t B, int64_t C, int64_t D, int64_t H, int64_t W,
+                        void* stream) {
   WF_REQUIRE(B >= 1 && C >= 4 && C % 4 == 0, "need B >= 1 and C a positive multiple of 4");
   WF_REQUIRE(D >= 2 && H >= 2 && W >= 2 && D % 2 == 0 && H % 2 == 0 && W % 2 == 0,
              "D, H, W must be even (ptwt 'zero' mode with odd sizes is not supported)");
@@ -425,13 +428,13 @@ extern "C" int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float*
     int64_t blocks = cdiv(total, gpb);
     if (blocks > 8192) blocks = 8192;
     if (ln)
-      hipLaunchKernelGGL((dwt3d_haar_fwd_kernel<G, V, true>), dim3((unsigned)blocks), dim3(256),
-                         0, (hipStream_t)stream, x, ln_w, ln_b, ln_eps, bands, (int)B, (int)C,
-                         (int)D, (int)H, (int)W);
+      hipLaunchKernelGGL((dwt3d_haar_fwd_kernel<G, V, true, NB>), dim3((unsigned)blocks),
+                         dim3(256), 0, (hipStream_t)stream, x, ln_w, ln_b, ln_eps, bands, (int)B,
+                         (int)C, (int)D, (int)H, (int)W);
     else
-      hipLaunchKernelGGL((dwt3d_haar_fwd_kernel<G, V, false>), dim3((unsigned)blocks), dim3(256),
-                         0, (hipStream_t)stream, x, ln_w, ln_b, ln_eps, bands, (int)B, (int)C,
-                         (int)D, (int)H, (int)W);
+      hipLaunchKernelGGL((dwt3d_haar_fwd_kernel<G, V, false, NB>), dim3((unsigned)blocks),
+                         dim3(256), 0, (hipStream_t)stream, x, ln_w, ln_b, ln_eps, bands, (int)B,
+                         (int)C, (int)D, (int)H, (int)W);
     return check_launch("wf_dwt3d_haar_fwd");
   };
   // C = 48 (stage 1, the 400 MB launch): 16 lanes x 1 float4 per position instead of 4 x 3
@@ -439,6 +442,18 @@ extern "C" int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float*
   static const bool wide = getenv("WF_DWT_G4") == nullptr;
   if (wide && C == 48) return go(ic<16>{}, ic<1>{});
   return dispatch_gv(C / 4, go);
+}
+
+extern "C" int wf_dwt3d_haar_fwd(const float* x, const float* ln_w, const float* ln_b,
+                                 float ln_eps, float* bands, int64_t B, int64_t C, int64_t D,
+                                 int64_t H, int64_t W, void* stream) {
+  return dwt_haar_fwd<8>(x, ln_w, ln_b, ln_eps, bands, B, C, D, H, W, stream);
+}
+
+extern "C" int wf_dwt3d_haar_fwd_ll(const float* x, const float* ln_w, const float* ln_b,
+                                    float ln_eps, float* ll, int64_t B, int64_t C, int64_t D,
+                                    int64_t H, int64_t W, void* stream) {
+  return dwt_haar_fwd<1>(x, ln_w, ln_b, ln_eps, ll, B, C, D, H, W, stream);
 }
 
 static int idwt_launch(const float* ll, int64_t ll_bstride, int64_t ll_cs, int64_t ll_ps,

@@ -449,6 +449,19 @@ class Block(nn.Module):
             return self.multi_scale_forward(x)
         return self.single_scale_forward(x)
 
+    # Set by MultiscaleTransformer.forward_features around the call of a Block whose detail
+    # bands it discards (every Block of a stage but the last keeps none: waveformer.py:288-292):
+    # inference then runs the LL-only DWT (wf_dwt3d_haar_fwd_ll) and returns no hf dicts.
+    _hf_unused = False
+
+    def _ll_levels(self, x, ln1, n):
+        """n LL-only Haar levels (norm1 fused into the first): [LL], fine -> coarse."""
+        lls, cur = [], x
+        for i in range(n):
+            cur = ops.dwt3d_haar_ll(cur, (ln1[0], ln1[1], float(ln1[2])) if i == 0 else None)
+            lls.append(cur)
+        return lls
+
     def _levels(self, x, ln1, n):
         """n one-level Haar DWTs (norm1 fused into the first): [band buffers], fine -> coarse."""
         bands, cur = [], x
@@ -472,6 +485,11 @@ class Block(nn.Module):
         if self.level > 0:
             self.dwt_downsamples._check()
             n = self.attn_computation_level
+            if (self._hf_unused and x.is_cuda and not torch.is_grad_enabled()
+                    and not torch.compiler.is_compiling()):
+                srcs = [self.attn.forward_raster(ll) for ll in self._ll_levels(x, ln1, n)]
+                xh, stats = _OPS.msfuse(srcs, x, s_attn, float(self.norm2.eps), True)
+                return ffn_op(xh, stats, self.norm2, self.mlp, s_mlp), ()
             side = _side_stream(x.device) if n > 1 and _concurrent_levels(x) else None
             if side is None:
                 bands = self._levels(x, ln1, n)

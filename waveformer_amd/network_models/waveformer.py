@@ -8,6 +8,7 @@ is proj_out's transposed write of each stage output to NCDHW (the tensors the de
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import List, Tuple
 
@@ -19,6 +20,10 @@ from .. import autograd as wfa
 from .. import ops
 from ..blocks import PatchEmbed as _MonaiPatchEmbed
 from .wave_helper import Block, PatchMerging
+
+
+# WF_HF_SKIP=0 (A/B): every Block computes its detail bands, as the reference does
+_HF_SKIP = os.environ.get("WF_HF_SKIP", "1") != "0"
 
 
 class MultiscaleTransformer(nn.Module):
@@ -121,8 +126,15 @@ class MultiscaleTransformer(nn.Module):
             if s > 0:
                 x = getattr(self, f"downsample_{s}")(x)
             x_h = None
-            for blk in getattr(self, f"block{s + 1}"):
-                r = blk(x)
+            blocks = getattr(self, f"block{s + 1}")
+            for i, blk in enumerate(blocks):
+                # only the stage's last Block's hf is kept (waveformer.py:288-292): the others
+                # run the LL-only DWT in inference
+                blk._hf_unused = _HF_SKIP and not train and i < len(blocks) - 1
+                try:
+                    r = blk(x)
+                finally:
+                    blk._hf_unused = False
                 if isinstance(r, tuple):
                     x, x_h = r
                 else:

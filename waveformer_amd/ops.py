@@ -365,6 +365,24 @@ def dwt3d_haar(x_cl: torch.Tensor, ln: Optional[Tuple[torch.Tensor, torch.Tensor
     return bands
 
 
+def dwt3d_haar_ll(x_cl: torch.Tensor, ln: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None
+                  ) -> torch.Tensor:
+    """The LL band of dwt3d_haar alone (wf_dwt3d_haar_fwd_ll): (B,D,H,W,C) -> (B,D/2,H/2,W/2,C),
+    bitwise band 0 of dwt3d_haar, for Blocks whose detail bands are never read."""
+    _check(x_cl, "x")
+    B, D, H, W, C = x_cl.shape
+    ll = torch.empty((B, D // 2, H // 2, W // 2, C), dtype=torch.float32, device=x_cl.device)
+    lw = lb = None
+    eps = 0.0
+    if ln is not None:
+        lw, lb, eps = ln
+        _check(lw, "ln_w")
+        _check(lb, "ln_b")
+    _lib.call("wf_dwt3d_haar_fwd_ll", x_cl.data_ptr(), _ptr(lw), _ptr(lb), float(eps),
+              ll.data_ptr(), B, C, D, H, W, _stream())
+    return ll
+
+
 def bands_to_coeffs(bands: torch.Tensor) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
     """(8,B,d,h,w,C) bands -> (LL, detail dict) as NCDHW-shaped (channel-last strided) views,
     the structure ptwt.wavedec3(level=1) returns (wave_helper.py:350-353)."""
