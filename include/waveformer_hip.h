@@ -89,6 +89,15 @@ int wf_debug_poison_lds(int64_t blocks, int lds_bytes, void* stream);
 int wf_patch_embed_fwd(const float* x, const float* w, const float* bias, float* out,
                        int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W,
                        void* stream);
+/* PatchEmbed fused with the first Block's norm1 + Haar LL (ABI 15; inference, when that Block's
+ * detail bands are dropped): out as wf_patch_embed_fwd (exactly the same values), ll =
+ * LL(LayerNorm(out; ln_w, ln_b, ln_eps)) (B, D/2, H/2, W/2, Cout) as wf_dwt3d_haar_fwd_ll would
+ * give it up to the LayerNorm moments' summation order.  Cin 4 or 1, Cout 48, D/H/W even,
+ * W <= 64.                                                                                 */
+int wf_patch_embed_ll_fwd(const float* x, const float* w, const float* bias, float* out,
+                          const float* ln_w, const float* ln_b, float ln_eps, float* ll,
+                          int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H, int64_t W,
+                          void* stream);
 
 /* ---- a1: 1-level Haar analysis ----------------------------------------------------- */
 /* Replaces ptwt.wavedec3(x, 'db1', level=1, mode='zero') at network_models/wave_helper.py:350,

@@ -78,10 +78,28 @@ def test_dwt_haar_ll_only_bitwise(C_, ln):
     assert ll.shape == bands[0].shape and torch.equal(ll, bands[0])
 
 
+@pytest.mark.parametrize("B,cin,S", [(2, 4, (32, 16, 128)), (1, 1, (20, 12, 36))])
+def test_patch_embed_ll_fused(B, cin, S):
+    """wf_patch_embed_ll_fwd: the stage-1 activation bitwise equal to wf_patch_embed_fwd, and
+    the first Block's level-1 LL equal to the LL-only DWT of it (norm1 fused) up to the
+    LayerNorm moments' summation order (rel-L2 <= 1e-6)."""
+    from waveformer_amd import ops
+    x = cuda(seeded_randn((B, cin) + S, 15))
+    w = cuda(seeded_randn((48, cin, 2, 2, 2), 16) * 0.2)
+    bias = cuda(seeded_randn((48,), 17))
+    ln = (cuda(seeded_randn((48,), 18) * 0.2 + 1), cuda(seeded_randn((48,), 19) * 0.1), 1e-6)
+    out, ll = ops.patch_embed_ll(x, w, bias, ln)
+    ref = ops.patch_embed(x, w, bias)
+    assert torch.equal(out, ref)
+    assert C.rel_l2(ll, ops.dwt3d_haar_ll(ref, ln)) <= 1e-6
+
+
 def test_encoder_block_hf_skip_keeps_outputs():
-    """The encoder runs every Block but a stage's last on the LL-only DWT in inference; its
-    outputs and the returned hf dicts (the last Blocks') equal a run that computes every
-    Block's detail bands (the flag forced off), bitwise."""
+    """The encoder runs every Block but a stage's last on the LL-only DWT in inference (the
+    first one on the LL the fused PatchEmbed kernel forms); its outputs and the returned hf
+    dicts (the last Blocks') equal a run that computes every Block's detail bands (the flag
+    forced off) up to the fused kernel's LayerNorm-moment rounding, carried through the four
+    stages (rel-L2 <= 1e-5; measured 1.6e-6; the encoder's bar against the oracle is 1e-4)."""
     import waveformer_amd.network_models as NM
     from waveformer_amd.network_models import wave_helper as WH
     torch.manual_seed(0)
@@ -116,11 +134,11 @@ def test_encoder_block_hf_skip_keeps_outputs():
         finally:
             WH.Block._hf_unused = saved
     for a, b in zip(outs, outs2):
-        assert torch.equal(a, b)
+        assert C.rel_l2(a, b) <= 1e-5
     for da, db in zip(hf, hf2):
         for ta, tb in zip(da, db):
             for k in ta:
-                assert torch.equal(ta[k], tb[k]), k
+                assert C.rel_l2(ta[k], tb[k]) <= 1e-5, k
 
 
 @pytest.mark.parametrize("levels,C_,base", [(1, 192, (2, 2, 2)), (2, 96, (2, 3, 2)),

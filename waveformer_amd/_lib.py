@@ -31,6 +31,8 @@ SIGNATURES = {
     "wf_cast_f32_to_f16x2": (_I, [_P, _P, _I64, _P]),
     "wf_cast_f32_to_f16x2_multi": (_I, [_P, _I64, _I64, _P]),
     "wf_debug_poison_lds": (_I, [_I64, _I, _P]),
+    "wf_patch_embed_ll_fwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64,
+                                   _I64, _P]),
     "wf_patch_embed_fwd": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwt3d_haar_fwd": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_dwt3d_haar_fwd_ll": (_I, [_P, _P, _P, _F, _P, _I64, _I64, _I64, _I64, _I64, _P]),

@@ -86,6 +86,122 @@ __global__ __launch_bounds__(256) void patch_embed_lane_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// PatchEmbed + the first Block's norm1 + Haar LL (round 5; inference, when the stage's first
+// Block drops its detail bands): the lane kernel above with a workgroup = the 2 x 2 output rows
+// (z + dz, y + dy) of one (z, y) pair, wave 2 dz + dy, lane = x (W <= 64, even).  Each lane
+// keeps its position's COUT outputs in registers, so norm1's two-pass moments cost no
+// exchange; after one barrier the LL of every 2 x 2 x 2 cube is formed from the LDS rows in the
+// Haar butterfly order of dwt3d_haar_fwd_kernel (x, then y, then z).  The stage-1 activation is
+// written as before; the LL (B, D/2, H/2, W/2, COUT) replaces that Block's LL-only DWT launch,
+// which re-read the whole 402 MB activation (B = 8).
+// ---------------------------------------------------------------------------------------
+template <int CIN, int COUT>
+__global__ __launch_bounds__(256) void patch_embed_ll_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ out, const float* __restrict__ ln_w, const float* __restrict__ ln_b,
+    float ln_eps, float* __restrict__ ll, int D, int H, int W) {
+  constexpr int K = CIN * 8;
+  constexpr int RS = COUT + 4;
+  constexpr int C4 = COUT / 4;
+  __shared__ __attribute__((aligned(16))) float tile[4][64 * RS];
+  __shared__ float2 mst[4][64];  // {mean, rstd} of each position
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int hp = H >> 1, dp = D >> 1;
+  int64_t t = blockIdx.x;
+  const int yp = (int)(t % hp);
+  t /= hp;
+  const int zp = (int)(t % dp);
+  const int64_t b = t / dp;
+  const int zo = 2 * zp + (wv >> 1), yo = 2 * yp + (wv & 1);
+  const int xo = min(lane, W - 1);
+  const int W2 = 2 * W, H2 = 2 * H, D2 = 2 * D;
+  float v[K];
+#pragma unroll
+  for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const float2 u = *reinterpret_cast<const float2*>(
+            x + (((b * CIN + ci) * D2 + 2 * zo + dz) * H2 + 2 * yo + dy) * W2 + 2 * xo);
+        v[ci * 8 + dz * 4 + dy * 2] = u.x;
+        v[ci * 8 + dz * 4 + dy * 2 + 1] = u.y;
+      }
+  float* row = &tile[wv][lane * RS];
+  constexpr int KH = K > 16 ? 16 : K;
+  float o[COUT];
+#pragma unroll
+  for (int c4 = 0; c4 < C4; ++c4) {
+    float a[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a[e] = bias ? bias[4 * c4 + e] : 0.f;
+#pragma unroll
+    for (int k0 = 0; k0 < K; k0 += KH) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float* wc = w + (4 * c4 + e) * K + k0;
+#pragma unroll
+        for (int k = 0; k < KH; ++k) a[e] = fmaf(v[k0 + k], wc[k], a[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[4 * c4 + e] = a[e];
+    *reinterpret_cast<f32x4*>(row + 4 * c4) = f32x4{a[0], a[1], a[2], a[3]};
+  }
+  // norm1's moments of this position (two-pass, as row_stats)
+  {
+    float sm = 0.f;
+#pragma unroll
+    for (int c4 = 0; c4 < C4; ++c4)
+      sm += (o[4 * c4] + o[4 * c4 + 1]) + (o[4 * c4 + 2] + o[4 * c4 + 3]);
+    const float mean = sm / (float)COUT;
+    float q = 0.f;
+#pragma unroll
+    for (int c4 = 0; c4 < C4; ++c4) {
+      const float d0 = o[4 * c4] - mean, d1 = o[4 * c4 + 1] - mean, d2 = o[4 * c4 + 2] - mean,
+                  d3 = o[4 * c4 + 3] - mean;
+      q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    }
+    mst[wv][lane] = float2{mean, rsqrtf(q / (float)COUT + ln_eps)};
+  }
+  // the activation row (W positions x COUT, contiguous channel-last) with 1 KB stores
+  {
+    const int64_t p0 = ((b * D + zo) * H + yo) * W;
+    float* dst = out + p0 * COUT;
+    const int nval = W * C4;
+#pragma unroll
+    for (int j = 0; j < C4; ++j) {
+      const int e = j * 64 + lane;
+      if (e < nval) {
+        const int pos = e / C4, c = (e - pos * C4) * 4;
+        *reinterpret_cast<f32x4*>(dst + 4 * (int64_t)e) =
+            *reinterpret_cast<const f32x4*>(&tile[wv][pos * RS + c]);
+      }
+    }
+  }
+  __syncthreads();
+  // LL of the W/2 cubes x C4 channel quads: n = 4 dz + 2 dy + dx, butterflies x, y, z
+  const int wp = W >> 1;
+  const int64_t lbase = ((b * dp + zp) * hp + yp) * (int64_t)wp;
+  for (int it = threadIdx.x; it < wp * C4; it += 256) {
+    const int lx = it / C4, q4 = it - lx * C4;
+    const f32x4 gw = *reinterpret_cast<const f32x4*>(ln_w + 4 * q4);
+    const f32x4 gb = *reinterpret_cast<const f32x4*>(ln_b + 4 * q4);
+    f32x4 c[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int wn = ((n >> 2) << 1) | ((n >> 1) & 1), ln = 2 * lx + (n & 1);
+      const float2 ms = mst[wn][ln];
+      const f32x4 val = *reinterpret_cast<const f32x4*>(&tile[wn][ln * RS + 4 * q4]);
+      c[n] = (val - ms.x) * ms.y * gw + gb;
+    }
+    const f32x4 s01 = c[0] + c[1], s23 = c[2] + c[3], s45 = c[4] + c[5], s67 = c[6] + c[7];
+    const f32x4 r = ((s01 + s23) + (s45 + s67)) * 0.35355339059327373f;
+    *reinterpret_cast<f32x4*>(ll + (lbase + lx) * COUT + 4 * q4) = r;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // PatchEmbed, streaming variant (Cin = 4, Cout % 4 == 0, W % 2 == 0: the encoder's 4 -> 48
 // stem): a persistent workgroup walks groups of R output rows; the next group's 2x2 input
 // rows are loaded into registers (8 float4 per thread at R = 4) while the current group is
@@ -614,6 +730,34 @@ __global__ __launch_bounds__(256) void proj_out_kernel(const float* __restrict__
 }  // namespace wf
 
 using namespace wf;
+
+extern "C" int wf_patch_embed_ll_fwd(const float* x, const float* w, const float* bias,
+                                     float* out, const float* ln_w, const float* ln_b,
+                                     float ln_eps, float* ll, int64_t B, int64_t Cin,
+                                     int64_t Cout, int64_t D, int64_t H, int64_t W, void* stream) {
+  WF_REQUIRE(B >= 1 && D >= 2 && H >= 2 && W >= 2, "empty tensor");
+  WF_REQUIRE(Cout == 48 && (Cin == 4 || Cin == 1),
+             "PatchEmbed + LL: Cin 4 or 1, Cout 48 (the encoder stem)");
+  WF_REQUIRE(D % 2 == 0 && H % 2 == 0 && W % 2 == 0 && W <= 64,
+             "PatchEmbed + LL: even output sizes, W <= 64");
+  WF_REQUIRE(B * D * H * W * Cout < ((int64_t)1 << 31), "tensor too large");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(w);
+  WF_REQUIRE_PTR(out);
+  WF_REQUIRE_PTR(ln_w);
+  WF_REQUIRE_PTR(ln_b);
+  WF_REQUIRE_PTR(ll);
+  const unsigned blocks = (unsigned)(B * (D / 2) * (H / 2));
+  if (Cin == 4)
+    hipLaunchKernelGGL((patch_embed_ll_kernel<4, 48>), dim3(blocks), dim3(256), 0,
+                       (hipStream_t)stream, x, w, bias, out, ln_w, ln_b, ln_eps, ll, (int)D,
+                       (int)H, (int)W);
+  else
+    hipLaunchKernelGGL((patch_embed_ll_kernel<1, 48>), dim3(blocks), dim3(256), 0,
+                       (hipStream_t)stream, x, w, bias, out, ln_w, ln_b, ln_eps, ll, (int)D,
+                       (int)H, (int)W);
+  return check_launch("wf_patch_embed_ll_fwd");
+}
 
 extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* bias, float* out,
                                   int64_t B, int64_t Cin, int64_t Cout, int64_t D, int64_t H,

@@ -453,12 +453,18 @@ class Block(nn.Module):
     # bands it discards (every Block of a stage but the last keeps none: waveformer.py:288-292):
     # inference then runs the LL-only DWT (wf_dwt3d_haar_fwd_ll) and returns no hf dicts.
     _hf_unused = False
+    # ... and, for the first Block of stage 1, the level-1 LL the fused PatchEmbed kernel
+    # already formed from its output (wf_patch_embed_ll_fwd), or None
+    _ll_given = None
 
     def _ll_levels(self, x, ln1, n):
         """n LL-only Haar levels (norm1 fused into the first): [LL], fine -> coarse."""
         lls, cur = [], x
         for i in range(n):
-            cur = ops.dwt3d_haar_ll(cur, (ln1[0], ln1[1], float(ln1[2])) if i == 0 else None)
+            if i == 0 and self._ll_given is not None:
+                cur = self._ll_given
+            else:
+                cur = ops.dwt3d_haar_ll(cur, (ln1[0], ln1[1], float(ln1[2])) if i == 0 else None)
             lls.append(cur)
         return lls
 

@@ -117,8 +117,16 @@ class MultiscaleTransformer(nn.Module):
             raise TypeError("waveformer_amd: float32 input expected")
         pe = self.patch_embed.proj
         train = wfa.needs_grad(x_rgb, *self.parameters())
+        ll0 = None  # the first Block's level-1 LL, formed by the fused PatchEmbed kernel
+        b0 = self.block1[0]
         if train:
             x = wfa.PatchEmbedFn.apply(x_rgb.contiguous(), pe.weight.contiguous(), pe.bias)
+        elif (_HF_SKIP and len(self.block1) > 1 and b0.ms_attention and b0.level > 0
+              and x_rgb.is_cuda and not torch.compiler.is_compiling()):
+            r = ops.patch_embed_ll(x_rgb.contiguous(), pe.weight.contiguous(), pe.bias,
+                                   (b0.norm1.weight, b0.norm1.bias, b0.norm1.eps))
+            x, ll0 = r if r is not None else (
+                ops.patch_embed(x_rgb.contiguous(), pe.weight.contiguous(), pe.bias), None)
         else:
             x = ops.patch_embed(x_rgb.contiguous(), pe.weight.contiguous(), pe.bias)
         outs, outs_hf = [], []
@@ -131,10 +139,12 @@ class MultiscaleTransformer(nn.Module):
                 # only the stage's last Block's hf is kept (waveformer.py:288-292): the others
                 # run the LL-only DWT in inference
                 blk._hf_unused = _HF_SKIP and not train and i < len(blocks) - 1
+                blk._ll_given = ll0 if (s == 0 and i == 0 and blk._hf_unused) else None
                 try:
                     r = blk(x)
                 finally:
                     blk._hf_unused = False
+                    blk._ll_given = None
                 if isinstance(r, tuple):
                     x, x_h = r
                 else:

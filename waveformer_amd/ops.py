@@ -345,6 +345,33 @@ def patch_embed(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tens
     return out
 
 
+def patch_embed_ll(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                   ln: Tuple[torch.Tensor, torch.Tensor, float]
+                   ) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+    """patch_embed fused with the first Block's norm1 + Haar LL (wf_patch_embed_ll_fwd):
+    (out, LL of LayerNorm(out)), or None when the shape is not the kernel's (Cin 1 / 4, Cout 48,
+    even output sizes, output W <= 64)."""
+    B, Cin, D2, H2, W2 = x.shape
+    Cout = weight.shape[0]
+    D, H, W = D2 // 2, H2 // 2, W2 // 2
+    if (Cout != 48 or Cin not in (1, 4) or tuple(weight.shape) != (Cout, Cin, 2, 2, 2)
+            or D2 % 2 or H2 % 2 or W2 % 2 or D % 2 or H % 2 or W % 2 or W > 64):
+        return None
+    _check(x, "x")
+    _check(weight, "weight")
+    lw, lb, eps = ln
+    _check(lw, "ln_w")
+    _check(lb, "ln_b")
+    if bias is not None:
+        _check(bias, "bias")
+    out = torch.empty((B, D, H, W, Cout), dtype=torch.float32, device=x.device)
+    ll = torch.empty((B, D // 2, H // 2, W // 2, Cout), dtype=torch.float32, device=x.device)
+    _lib.call("wf_patch_embed_ll_fwd", x.data_ptr(), weight.data_ptr(), _ptr(bias),
+              out.data_ptr(), lw.data_ptr(), lb.data_ptr(), float(eps), ll.data_ptr(), B, Cin,
+              Cout, D, H, W, _stream())
+    return out, ll
+
+
 # ------------------------------------------------------------------------------------------
 # a1: Haar analysis
 # ------------------------------------------------------------------------------------------
