@@ -743,8 +743,9 @@ static bool conv3w_ok(const Conv3Args& a, int prec, int64_t wgs) {
   // Cin > 88: at 48 input channels (3 steps per tile) the exposed per-tile prologue of the one
   // workgroup per CU costs more than the wider loads save (profiles/r5_conv_wide_ab.txt)
   static const int min_cin = getenv("WF_CONV_WIDE_MINCIN") ? atoi(getenv("WF_CONV_WIDE_MINCIN")) : 89;
+  // fp16 input: 16-B loads of 8 channels (16-B aligned rows and channel offsets)
   return on && a.Cout % 48 == 0 && a.W > 32 && wgs >= 512 && a.Cin >= min_cin &&
-         (!a.xh || a.Cin % 8 == 0);
+         (!a.xh || (a.Cin % 8 == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.xh & 15) == 0));
 }
 
 static int launch_conv3w(const Conv3Args& a0, int prec, hipStream_t stream) {
