@@ -121,14 +121,7 @@ def test_encoder_block_hf_skip_keeps_outputs():
             WH.Block._ll_levels = orig
         assert calls, "the LL-only path did not run"
         saved = WH.Block.__dict__["_hf_unused"]
-
-        class _Never:  # forces the flag off for every Block: the full 8-band DWT everywhere
-            def __get__(self, obj, typ=None):
-                return False
-
-            def __set__(self, obj, v):
-                pass
-        WH.Block._hf_unused = _Never()
+        WH.Block._hf_unused = property(lambda self: False)  # every Block: all 8 bands
         try:
             outs2, hf2 = m(x)
         finally:

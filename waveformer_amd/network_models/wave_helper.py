@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 from typing import Optional, Tuple
 
 import torch
@@ -369,6 +370,9 @@ class WaveletTransform3D(nn.Module):
 # (1536 workgroups, two per CU) leaves no CU slots for the side branch until its tail, and the
 # bench measured no gain beyond noise (1117.6 / 1113.4 vs 1118.5 / 1108.4 volumes/s).
 _MS_STREAMS = os.environ.get("WF_MS_STREAMS", "0") == "1"
+# per-thread {id(Block): level-1 LL or None} of the Blocks whose hf the running encoder
+# forward discards (see Block._hf_unused)
+HF_SKIP = threading.local()
 _SIDE = {}
 
 
@@ -449,13 +453,18 @@ class Block(nn.Module):
             return self.multi_scale_forward(x)
         return self.single_scale_forward(x)
 
-    # Set by MultiscaleTransformer.forward_features around the call of a Block whose detail
-    # bands it discards (every Block of a stage but the last keeps none: waveformer.py:288-292):
-    # inference then runs the LL-only DWT (wf_dwt3d_haar_fwd_ll) and returns no hf dicts.
-    _hf_unused = False
-    # ... and, for the first Block of stage 1, the level-1 LL the fused PatchEmbed kernel
-    # already formed from its output (wf_patch_embed_ll_fwd), or None
-    _ll_given = None
+    # MultiscaleTransformer.forward_features marks, for the duration of one call and in this
+    # thread only (HF_SKIP), a Block whose detail bands it discards (every Block of a stage but
+    # the last keeps none: waveformer.py:288-292): inference then runs the LL-only DWT
+    # (wf_dwt3d_haar_fwd_ll) and returns no hf dicts -- and the first Block of stage 1 takes
+    # its level-1 LL from the fused PatchEmbed kernel (wf_patch_embed_ll_fwd).
+    @property
+    def _hf_unused(self):
+        return id(self) in getattr(HF_SKIP, "blocks", {})
+
+    @property
+    def _ll_given(self):
+        return getattr(HF_SKIP, "blocks", {}).get(id(self))
 
     def _ll_levels(self, x, ln1, n):
         """n LL-only Haar levels (norm1 fused into the first): [LL], fine -> coarse."""

@@ -19,6 +19,7 @@ import torch.nn.init as init
 from .. import autograd as wfa
 from .. import ops
 from ..blocks import PatchEmbed as _MonaiPatchEmbed
+from . import wave_helper as WH
 from .wave_helper import Block, PatchMerging
 
 
@@ -138,13 +139,12 @@ class MultiscaleTransformer(nn.Module):
             for i, blk in enumerate(blocks):
                 # only the stage's last Block's hf is kept (waveformer.py:288-292): the others
                 # run the LL-only DWT in inference
-                blk._hf_unused = _HF_SKIP and not train and i < len(blocks) - 1
-                blk._ll_given = ll0 if (s == 0 and i == 0 and blk._hf_unused) else None
+                skip = _HF_SKIP and not train and i < len(blocks) - 1
+                WH.HF_SKIP.blocks = {id(blk): ll0 if s == 0 and i == 0 else None} if skip else {}
                 try:
                     r = blk(x)
                 finally:
-                    blk._hf_unused = False
-                    blk._ll_given = None
+                    WH.HF_SKIP.blocks = {}
                 if isinstance(r, tuple):
                     x, x_h = r
                 else:
