@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 15
+#define WF_ABI_VERSION 16
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
@@ -450,6 +450,10 @@ int wf_patch_merging_fwd(const float* x, const float* ln_w, const float* ln_b, f
  * x channel-last (B, S, C) (S = D*H*W) -> out NCDHW (B, C, S).  normalize=0 only transposes. */
 int wf_proj_out_fwd(const float* x, float* out, int normalize, float eps, int64_t B,
                     int64_t C, int64_t S, void* stream);
+/* proj_out for a channel-last consumer (the full model's encoder2-4 / encoder10 UnetResBlocks,
+ * network_backbone.py:387-392): the same non-affine LayerNorm, x (M, C) -> out (M, C), values
+ * bitwise those wf_proj_out_fwd writes, with no NCDHW round trip.                           */
+int wf_proj_out_cl_fwd(const float* x, float* out, float eps, int64_t M, int64_t C, void* stream);
 
 /* ---- sliding-window inference (config 3) ----------------------- */
 /* Replaces monai.data.utils.compute_importance_map (monai/data/utils.py:1088-1138) as called

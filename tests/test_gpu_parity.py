@@ -278,6 +278,40 @@ def test_proj_out_layernorm_ncdhw(C_, S):
     assert torch.equal(out.cpu(), x.permute(0, 4, 1, 2, 3))
 
 
+@pytest.mark.parametrize("C_,S", [(48, 4096), (96, 512), (192, 64), (384, 8), (384, 1000),
+                                  (40, 333), (8, 65)])
+def test_proj_out_channel_last_bitwise(C_, S):
+    """wf_proj_out_cl_fwd: proj_out's values (bitwise) as an NCDHW-shaped channels_last_3d
+    tensor the UnetResBlocks read without a transpose."""
+    from waveformer_amd import ops
+    x = cuda(seeded_randn((2, S, 1, 1, C_), 5) * 2 + 1)
+    for norm in (True, False):
+        cl = ops.proj_out_cl(x, norm)
+        assert cl.shape == (2, C_, S, 1, 1) and ops.cl_ld(cl) == C_
+        assert torch.equal(cl.contiguous(), ops.proj_out(x, norm))
+
+
+def test_full_model_channel_last_outs_bitwise():
+    """The full model's inference hands the encoder's stage outputs over channel-last (no
+    NCDHW write + transpose back); its logits are bitwise those of the NCDHW hand-over."""
+    import waveformer_amd.network_models as NM
+    from waveformer_amd.network_models import network_backbone as NB
+    torch.manual_seed(0)
+    m = NM.Waveformer(img_size=(32,) * 3, in_chans=4, out_chans=4,
+                      num_heads=[1, 1, 1, 1]).eval().to(DEV)
+    x = cuda(seeded_randn((1, 4, 32, 32, 32), 15))
+    saved = NB._CL_OUTS
+    try:
+        with torch.no_grad():
+            NB._CL_OUTS = True
+            a = m(x)
+            NB._CL_OUTS = False
+            b = m(x)
+    finally:
+        NB._CL_OUTS = saved
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("cin,S", [(4, 32), (1, 32), (4, 128)])
 def test_patch_embed(cin, S):
     from waveformer_amd import ops

@@ -95,6 +95,7 @@ SIGNATURES = {
     "wf_patch_merging_fwd": (_I, [_P, _P, _P, _F, _P, _I, _P, _I64, _I64, _I64, _I64, _I64,
                                   _I, _P]),
     "wf_proj_out_fwd": (_I, [_P, _P, _I, _F, _I64, _I64, _I64, _P]),
+    "wf_proj_out_cl_fwd": (_I, [_P, _P, _F, _I64, _I64, _P]),
     "wf_importance_map": (_I, [_I, _P, _P, _I64, _I64, _I64, _P]),
     "wf_sliding_window_stitch": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _I64,
                                       _I64, _I64, _I64, _I64, _P]),
@@ -132,7 +133,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 _lock = threading.Lock()
 _lib = None
 _err = None

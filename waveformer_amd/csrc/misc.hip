@@ -727,6 +727,33 @@ __global__ __launch_bounds__(256) void proj_out_kernel(const float* __restrict__
   }
 }
 
+// proj_out for a channel-last consumer: (M, C) -> non-affine LayerNorm -> (M, C).  The same
+// row groups, row_stats and (v - mean) * rstd as proj_out_kernel, so the values are bitwise
+// those of the NCDHW write; the full model's UnetResBlocks read this layout directly instead
+// of transposing proj_out's NCDHW result back (one read + one write per stage output).
+template <int G, int V>
+__global__ __launch_bounds__(256) void proj_out_cl_kernel(const float* __restrict__ x,
+                                                          float* __restrict__ out, float eps,
+                                                          int64_t M, int C) {
+  const int C4 = C >> 2;
+  const int gl = threadIdx.x & (G - 1);
+  const int64_t m = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
+  if (m >= M) return;  // uniform per group: the group's shuffles see only live rows
+  bool live[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) live[j] = gl + j * G < C4;
+  const f32x4* row = reinterpret_cast<const f32x4*>(x + m * C);
+  f32x4* dst = reinterpret_cast<f32x4*>(out + m * C);
+  f32x4 v[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) v[j] = live[j] ? row[gl + j * G] : f32x4{0, 0, 0, 0};
+  float mean, rstd;
+  row_stats<G, V>(v, live, (float)C, eps, mean, rstd);
+#pragma unroll
+  for (int j = 0; j < V; ++j)
+    if (live[j]) dst[gl + j * G] = (v[j] - mean) * rstd;
+}
+
 }  // namespace wf
 
 using namespace wf;
@@ -887,5 +914,20 @@ extern "C" int wf_proj_out_fwd(const float* x, float* out, int normalize, float 
     hipLaunchKernelGGL((proj_out_kernel<G, V>), dim3((unsigned)blocks), dim3(256), lds,
                        (hipStream_t)stream, x, out, normalize, eps, (int)B, (int)C, S, (int)TP);
     return check_launch("wf_proj_out_fwd");
+  });
+}
+
+extern "C" int wf_proj_out_cl_fwd(const float* x, float* out, float eps, int64_t M, int64_t C,
+                                  void* stream) {
+  WF_REQUIRE(M >= 1 && C >= 4 && C % 4 == 0, "C must be a positive multiple of 4");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(out);
+  return dispatch_gv(C / 4, [&](auto G_, auto V_) -> int {
+    constexpr int G = decltype(G_)::value, V = decltype(V_)::value;
+    const int64_t blocks = cdiv(M, 256 / G);
+    WF_REQUIRE(blocks < ((int64_t)1 << 31), "too many rows");
+    hipLaunchKernelGGL((proj_out_cl_kernel<G, V>), dim3((unsigned)blocks), dim3(256), 0,
+                       (hipStream_t)stream, x, out, eps, M, (int)C);
+    return check_launch("wf_proj_out_cl_fwd");
   });
 }

@@ -10,6 +10,7 @@ blocks.py) -- no MIOpen convolution on any path.
 """
 from __future__ import annotations
 
+import os
 from typing import Tuple, Union
 
 import torch
@@ -24,6 +25,9 @@ from ..blocks import UnetOutBlock, UnetrBasicBlock, UnetrUpBlock
 from .idwt_upsample import UnetrIDWTBlock
 from .wave_helper import ProjectionUpsample
 from .waveformer import MultiscaleTransformer
+
+# WF_CL_OUTS=0 (A/B): the encoder hands NCDHW stage outputs over, as the reference's proj_out
+_CL_OUTS = os.environ.get("WF_CL_OUTS", "1") != "0"
 
 
 class ProjectionHead(nn.Module):
@@ -159,9 +163,12 @@ class Waveformer(nn.Module):
             return self._forward(x_in)
 
     def _forward(self, x_in: torch.Tensor) -> torch.Tensor:
-        outs, outs_hf = self.waveformer_encoder(x_in)
+        infer = x_in.is_cuda and not torch.is_grad_enabled()
+        # inference: the stage outputs come channel-last, the layout encoder2-4 / encoder10 read
+        # (proj_out's NCDHW write and ops.to_cl's transpose back are skipped; same values)
+        outs, outs_hf = self.waveformer_encoder(x_in, channel_last=infer and _CL_OUTS)
         fs0 = self.decoder1.transp_conv.conv.out_channels
-        if x_in.is_cuda and not torch.is_grad_enabled():
+        if infer:
             # inference: encoder1 writes straight into channels [fs0, 2 fs0) of decoder1's
             # channel-last concat buffer (blocks.UnetrUpBlock finds it there, no skip copy)
             B, _, D, H, W = x_in.shape

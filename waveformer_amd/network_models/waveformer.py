@@ -108,10 +108,12 @@ class MultiscaleTransformer(nn.Module):
         if hasattr(self, 'logger'):
             self.logger.info(f"Load model, Time usage: {time.time() - t0}")
 
-    def forward_features(self, x_rgb: torch.Tensor, normalize: bool = True
-                         ) -> Tuple[List[torch.Tensor], List]:
+    def forward_features(self, x_rgb: torch.Tensor, normalize: bool = True, *,
+                         channel_last: bool = False) -> Tuple[List[torch.Tensor], List]:
         """waveformer.py:260-322: PatchEmbed -> 4 stages (Blocks, PatchMerging) -> proj_out.
-        Returns (outs: 4 NCDHW tensors, outs_hf: the last block's detail dicts of stages 1-3)."""
+        Returns (outs: 4 NCDHW tensors, outs_hf: the last block's detail dicts of stages 1-3).
+        channel_last (inference only): the outs are NCDHW-shaped channels_last_3d tensors of the
+        same values -- the layout the full model's UnetResBlocks read (network_backbone.py)."""
         if self.patch_norm:
             raise NotImplementedError("waveformer_amd: patch_norm=True is not implemented")
         if x_rgb.dtype != torch.float32:
@@ -152,15 +154,17 @@ class MultiscaleTransformer(nn.Module):
             B, D, H, W, C = x.shape
             if train:
                 outs.append(wfa.ProjOutFn.apply(x, bool(normalize), 1e-5))
+            elif channel_last:
+                outs.append(ops.proj_out_cl(x, normalize))
             else:
                 outs.append(ops.proj_out(x, normalize))
             if s < 3:
                 outs_hf.append(x_h if x_h is not None else ())
         return outs, outs_hf
 
-    def forward(self, x_rgb: torch.Tensor):
+    def forward(self, x_rgb: torch.Tensor, *, channel_last: bool = False):
         with ops.weight_scope(self):  # split weights rebuilt once per forward (one launch)
-            return self.forward_features(x_rgb)
+            return self.forward_features(x_rgb, channel_last=channel_last)
 
     def flops(self) -> int:
         return 0

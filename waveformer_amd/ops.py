@@ -1452,3 +1452,17 @@ def proj_out(x_cl: torch.Tensor, normalize: bool, eps: float = 1e-5) -> torch.Te
     _lib.call("wf_proj_out_fwd", x_cl.data_ptr(), out.data_ptr(), int(bool(normalize)),
               float(eps), B, C, D * H * W, _stream())
     return out
+
+
+def proj_out_cl(x_cl: torch.Tensor, normalize: bool, eps: float = 1e-5) -> torch.Tensor:
+    """proj_out's values as an NCDHW-shaped channels_last_3d tensor (the layout the decoder's
+    UnetResBlocks read): no NCDHW write and no transpose back.  Bitwise equal to proj_out."""
+    _check(x_cl, "x")
+    B, D, H, W, C = x_cl.shape
+    out = torch.empty_like(x_cl)
+    if normalize:
+        _lib.call("wf_proj_out_cl_fwd", x_cl.data_ptr(), out.data_ptr(), float(eps),
+                  B * D * H * W, C, _stream())
+    else:
+        out.copy_(x_cl)
+    return out.permute(0, 4, 1, 2, 3)
