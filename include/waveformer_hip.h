@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 16
+#define WF_ABI_VERSION 17
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
@@ -317,6 +317,16 @@ int wf_upsample_trilinear_cl(const float* in, float* out, int64_t B, int64_t C, 
 int wf_upsample_trilinear_add_cl(const float* in, float* out, int64_t B, int64_t C, int64_t d,
                                  int64_t h, int64_t w, int64_t D, int64_t H, int64_t W,
                                  int align_corners, void* stream);
+/* ProjectionUpsample.conv1 fused (wave_helper.py:33-81, inference): nn.Upsample(trilinear,
+ * align_corners) x (B, d, h, wd, C) channel-last -> depthwise 3^3 conv (zero padding on the
+ * up-sampled volume) -> out (B, D, H, W, C) channel-last, the up-sampled tensor never stored;
+ * its values are bitwise wf_upsample_trilinear_cl's.  stats_acc (B, C, 2) fp64: the outputs'
+ * per-channel sum / sum of squares (zeroed here), for wf_instnorm_finalize.  C % 32 == 0,
+ * bias required, W >= 2 wd (each 16-column tile's haloed source span <= 12 columns).        */
+int wf_upsample_dwconv3d_stats_cl(const float* in, const float* w, const float* bias, float* out,
+                                  double* stats_acc, int64_t B, int64_t C, int64_t d, int64_t h,
+                                  int64_t wd, int64_t D, int64_t H, int64_t W, int align_corners,
+                                  void* stream);
 /* UnetOutBlock (monai dynunet_block.py:188-210, network_backbone.py:407): 1x1x1 conv of the
  * channel-last x (B, P positions ldx floats apart, K channels) with weight (N, K) + bias (N)
  * into the NCDHW out (B, N, P).  K % 4 == 0, K <= 120, N <= 16; fp32 FMAs.                  */

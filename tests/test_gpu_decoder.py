@@ -683,3 +683,37 @@ def test_conv3d_k3_wide_chunks_bitwise(tmp_path):
         b = seeded_randn((cout,), 170 + i)
         want = F.conv3d(x.double(), w.double(), b.double(), padding=1)
         assert C.rel_l2(wide[i][0], want) <= (1e-5 if prec == "bf16x3" else 1e-2), prec
+
+
+@pytest.mark.parametrize("ac", [True, False])
+@pytest.mark.parametrize("B,C_,src,s", [(2, 32, (5, 6, 7), 2), (1, 192, (6, 5, 7), 4),
+                                         (1, 96, (3, 9, 12), 2), (2, 64, (4, 4, 5), (2, 3, 4)),
+                                         (1, 32, (2, 2, 20), 2)])
+def test_upsample_dwconv3d_fused_bitwise(B, C_, src, s, ac):
+    """ProjectionUpsample.conv1 fused (wf_upsample_dwconv3d_stats_cl): bitwise the two-kernel
+    path (wf_upsample_trilinear_cl, then wf_dwconv3d_stats_cl) in the output and in the
+    GroupNorm statistics, and within fp32 rounding of F.interpolate + F.conv3d in fp64."""
+    from waveformer_amd import ops
+    st = (s,) * 3 if isinstance(s, int) else s
+    dst = tuple(a * b for a, b in zip(src, st))
+    x = seeded_randn((B, C_) + src, 12).cuda().contiguous(memory_format=torch.channels_last_3d)
+    w = seeded_randn((C_, 1, 3, 3, 3), 13).cuda() * 0.3
+    b = seeded_randn((C_,), 14).cuda()
+    got, gst = ops.upsample_dwconv3d_cl(x, dst, w, b, 1e-5, ac)
+    up = ops.upsample_cl(x, dst, ac)
+    want, wst = ops.dwconv3d_cl(up, w, b, norm_eps=1e-5)
+    assert torch.equal(got, want)
+    assert torch.equal(gst, wst)
+    ref = F.conv3d(F.interpolate(x.double().cpu(), size=dst, mode="trilinear", align_corners=ac),
+                   w.double().cpu(), b.double().cpu(), padding=1, groups=C_)
+    assert C.rel_l2(got, ref) <= 1e-6
+
+
+def test_upsample_dwconv3d_declines_unsupported():
+    from waveformer_amd import ops
+    x = torch.zeros((1, 48, 4, 4, 4), device="cuda")
+    w, b = torch.zeros((48, 1, 3, 3, 3), device="cuda"), torch.zeros(48, device="cuda")
+    assert ops.upsample_dwconv3d_cl(x, (8, 8, 8), w, b, 1e-5) is None      # C % 32
+    x = torch.zeros((1, 32, 4, 4, 4), device="cuda")
+    w, b = torch.zeros((32, 1, 3, 3, 3), device="cuda"), torch.zeros(32, device="cuda")
+    assert ops.upsample_dwconv3d_cl(x, (8, 8, 6), w, b, 1e-5) is None      # x factor < 2

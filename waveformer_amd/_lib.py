@@ -96,6 +96,7 @@ SIGNATURES = {
                                   _I, _P]),
     "wf_proj_out_fwd": (_I, [_P, _P, _I, _F, _I64, _I64, _I64, _P]),
     "wf_proj_out_cl_fwd": (_I, [_P, _P, _F, _I64, _I64, _P]),
+    "wf_upsample_dwconv3d_stats_cl": (_I, [_P, _P, _P, _P, _P] + [_I64] * 8 + [_I, _P]),
     "wf_importance_map": (_I, [_I, _P, _P, _I64, _I64, _I64, _P]),
     "wf_sliding_window_stitch": (_I, [_P, _I64, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _I64,
                                       _I64, _I64, _I64, _I64, _P]),
@@ -133,7 +134,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 _lock = threading.Lock()
 _lib = None
 _err = None

@@ -47,6 +47,9 @@ def _std_init(m: nn.Module) -> None:
         _conv_fan_out_init(m)
 
 
+# WF_UPDW=0 (A/B): ProjectionUpsample stores the up-sampled tensor and convolves it after
+_UPDW = os.environ.get("WF_UPDW", "1") != "0"
+
 class DropPath(nn.Module):
     """Per-sample stochastic depth (timm semantics).  Block never calls forward(): it asks for
     the per-sample factors and hands them to the fused kernels (branch_scale)."""
@@ -143,11 +146,18 @@ class ProjectionUpsample(nn.Module):
         P = size[0] * size[1] * size[2]
         xc = ops.to_cl(x)
         dw = self.conv1[1]
-        up = ops.upsample_cl(xc, size, True)
-        if dw.bias is not None and C % 32 == 0:
+        # up-sampling fused into the depthwise conv's plane staging (the 8x / 64x larger
+        # up-sampled tensor is never written and re-read), GroupNorm statistics in its epilogue
+        r = ops.upsample_dwconv3d_cl(xc, size, dw.weight, dw.bias, self.norm.eps) \
+            if _UPDW else None
+        if r is not None:
+            y, st = r
+        elif dw.bias is not None and C % 32 == 0:
+            up = ops.upsample_cl(xc, size, True)
             # GroupNorm(C, C) statistics accumulated in the depthwise conv's epilogue
             y, st = ops.dwconv3d_cl(up, dw.weight, dw.bias, norm_eps=self.norm.eps)
         else:
+            up = ops.upsample_cl(xc, size, True)
             y = ops.dwconv3d_cl(up, dw.weight, dw.bias)
             st = ops.instnorm_stats(y, self.norm.eps)                   # (B, 2, C)
         scale = st[:, 1] * self.norm.weight                              # (B, C)

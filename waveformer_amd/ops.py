@@ -1003,6 +1003,32 @@ def dwconv3d_cl(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tens
     return out
 
 
+def upsample_dwconv3d_cl(x: torch.Tensor, size, weight: torch.Tensor, bias: torch.Tensor,
+                         norm_eps: float, align_corners: bool = True):
+    """dwconv3d_cl(upsample_cl(x, size, align_corners), weight, bias, norm_eps) in one kernel
+    (wf_upsample_dwconv3d_stats_cl): the up-sampled tensor is never stored.  Returns (out,
+    stats) as dwconv3d_cl, or None where the fused kernel does not apply (C % 32, an x
+    up-sampling factor below 2) -- the caller then takes the two-kernel path."""
+    x = x if (cl_ld(x) == x.shape[1]) else x.contiguous(memory_format=torch.channels_last_3d)
+    B, C, d, h, w = x.shape
+    D, H, W = (int(v) for v in size)
+    if C % 32 or W < 2 * w or bias is None:
+        return None
+    if tuple(weight.shape) != (C, 1, 3, 3, 3):
+        raise ValueError(f"upsample_dwconv3d_cl: weight {tuple(weight.shape)} is not ({C},1,3,3,3)")
+    _check(weight, "weight")
+    _check(bias, "bias")
+    out = empty_cl(B, C, D, H, W, x.device)
+    acc = torch.empty((B, C, 2), dtype=torch.float64, device=x.device)
+    _lib.call("wf_upsample_dwconv3d_stats_cl", x.data_ptr(), weight.data_ptr(), bias.data_ptr(),
+              out.data_ptr(), acc.data_ptr(), B, C, d, h, w, D, H, W, int(bool(align_corners)),
+              _stream())
+    stats = torch.empty((B, 2, C), dtype=torch.float32, device=x.device)
+    _lib.call("wf_instnorm_finalize", acc.data_ptr(), stats.data_ptr(), B, C, D * H * W,
+              float(norm_eps), _stream())
+    return out, stats
+
+
 def conv3d_k3_wgrad(x: torch.Tensor, dy: torch.Tensor, wshape) -> torch.Tensor:
     """dW of conv3d_k3 (wf_conv3d_k3_wgrad): x (B, Cin, D, H, W), dy (B, Cout, D, H, W), both
     channel-last (copied to it otherwise) -> (Cout, Cin, 3, 3, 3) fp32."""
