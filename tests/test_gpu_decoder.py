@@ -688,7 +688,7 @@ def test_conv3d_k3_wide_chunks_bitwise(tmp_path):
 @pytest.mark.parametrize("ac", [True, False])
 @pytest.mark.parametrize("B,C_,src,s", [(2, 32, (5, 6, 7), 2), (1, 192, (6, 5, 7), 4),
                                          (1, 96, (3, 9, 12), 2), (2, 64, (4, 4, 5), (2, 3, 4)),
-                                         (1, 32, (2, 2, 20), 2)])
+                                         (1, 32, (2, 2, 20), 2), (1, 32, (3, 4, 4), (1, 2, 2))])
 def test_upsample_dwconv3d_fused_bitwise(B, C_, src, s, ac):
     """ProjectionUpsample.conv1 fused (wf_upsample_dwconv3d_stats_cl): bitwise the two-kernel
     path (wf_upsample_trilinear_cl, then wf_dwconv3d_stats_cl) in the output and in the
@@ -717,3 +717,5 @@ def test_upsample_dwconv3d_declines_unsupported():
     x = torch.zeros((1, 32, 4, 4, 4), device="cuda")
     w, b = torch.zeros((32, 1, 3, 3, 3), device="cuda"), torch.zeros(32, device="cuda")
     assert ops.upsample_dwconv3d_cl(x, (8, 8, 6), w, b, 1e-5) is None      # x factor < 2
+    assert ops.upsample_dwconv3d_cl(x, (8, 6, 8), w, b, 1e-5) is None      # y factor < 2
+    assert ops.upsample_dwconv3d_cl(x, (5, 8, 8), w, b, 1e-5) is not None  # any z factor

@@ -1007,12 +1007,12 @@ def upsample_dwconv3d_cl(x: torch.Tensor, size, weight: torch.Tensor, bias: torc
                          norm_eps: float, align_corners: bool = True):
     """dwconv3d_cl(upsample_cl(x, size, align_corners), weight, bias, norm_eps) in one kernel
     (wf_upsample_dwconv3d_stats_cl): the up-sampled tensor is never stored.  Returns (out,
-    stats) as dwconv3d_cl, or None where the fused kernel does not apply (C % 32, an x
+    stats) as dwconv3d_cl, or None where the fused kernel does not apply (C % 32, an x or y
     up-sampling factor below 2) -- the caller then takes the two-kernel path."""
     x = x if (cl_ld(x) == x.shape[1]) else x.contiguous(memory_format=torch.channels_last_3d)
     B, C, d, h, w = x.shape
     D, H, W = (int(v) for v in size)
-    if C % 32 or W < 2 * w or bias is None:
+    if C % 32 or W < 2 * w or H < 2 * h or bias is None:  # the kernel's staging spans
         return None
     if tuple(weight.shape) != (C, 1, 3, 3, 3):
         raise ValueError(f"upsample_dwconv3d_cl: weight {tuple(weight.shape)} is not ({C},1,3,3,3)")
