@@ -43,13 +43,19 @@ sys.path.insert(0, REPO)
 METRIC = "128³×4 volumes/sec fwd (1/2/4/8 MI355X) + Dice Δ vs reference"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table (spec)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
-# bench op name -> kernel-name substring in the PMC summary (profiles/*pmc*.json)
+# bench op name -> regular expression over the kernel names of the PMC summary
+# (profiles/*pmc*.json).  The Haar forward's template is <G, V, LN, BANDS>: the 8-band launch
+# (dwt3d_haar) and the LL-only one (dwt3d_haar_ll, the Blocks whose detail bands the encoder
+# drops) are different instantiations and must not be confused (a
+# substring match returned the LL-only kernel's 453 MB for the 805 MB 8-band launch).
 PMC_KERNEL = {"ccf_ffn_dwconv": "ffn_fused_kernel" if os.environ.get("WF_FFN_FUSED")
               else "ffn_dwfc_kernel" if os.environ.get("WF_FFN_DWFC_CLASSIC")
               else "ffn_dwfc_ws_kernel" if os.environ.get("WF_FFN_DWFC_WS")
               else "ffn_dwfc_sb_kernel" if os.environ.get("WF_FFN_DWFC_SB")
               else "ffn_dwfc_tb_kernel" if os.environ.get("WF_FFN_DWFC_TB", "4") == "1"
-              else "ffn_dwfc_tb4_kernel", "dwt3d_haar": "dwt3d_haar_fwd",
+              else "ffn_dwfc_tb4_kernel",
+              "dwt3d_haar": r"dwt3d_haar_fwd_kernel<\d+, \d+, (true|false), 8>",
+              "dwt3d_haar_ll": r"dwt3d_haar_fwd_kernel<\d+, \d+, (true|false), 1>",
               "window_attention": "attn_tbl_kernel",
               "msfuse": "msfuse", "proj_out": "proj_out"}
 
@@ -157,6 +163,8 @@ class OpTimer:
         "ccf_ffn_dwconv": _dw_bytes,
         # 1-level Haar: read the (B,D,H,W,C) input once, write 8 bands of 1/8 size
         "dwt3d_haar": lambda a, kw, out: 2 * a[0].numel() * 4,
+        # its LL band alone: read the input once, write 1/8 of it
+        "dwt3d_haar_ll": lambda a, kw, out: a[0].numel() * 4 + out.numel() * 4,
         # out = shortcut + sum trilinear(src): read shortcut + sources, write out + 8 B stats/row
         "msfuse": lambda a, kw, out: (2 * a[1].numel() + sum(s.numel() for s in a[0])) * 4
         + (0 if out[1] is None else out[1].numel() * 4),
@@ -213,11 +221,13 @@ class OpTimer:
                 "rate": big / (avg_ms * 1e-3), "issue": max(i for _, _, i in sel)}
 
 
-def pmc_traffic(kernel_substr, batch, grid=None):
+def pmc_traffic(kernel_re, batch, grid=None):
     """HBM bytes per launch from the newest profiles/*pmc*.json written by tools/pmc_traffic.py
     whose PMC passes ran at this per-GPU batch (summaries without the field were taken at 4);
-    None when no summary matches.  With `grid` (the timed launch's size in work-items) the
-    entry of that launch shape; None when the summary has no per-shape record of it."""
+    None when no summary matches.  `kernel_re` is searched in the kernel names; over every
+    matching kernel, the largest launch's bytes (the op timers time the largest launch class),
+    or with `grid` (the timed launch's size in work-items) the entry of that launch shape."""
+    import re
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True)
     for f in files:
         try:
@@ -226,12 +236,14 @@ def pmc_traffic(kernel_substr, batch, grid=None):
             continue
         if "kernels" not in d or d.get("per_gpu_batch", 4) != batch:
             continue
-        for k, v in d["kernels"].items():
-            if kernel_substr in k:
-                if grid is None:
-                    return v.get("hbm_bytes_per_launch_largest")
-                return v.get("by_grid", {}).get(str(grid), {}).get("hbm_bytes_per_launch")
-        return None
+        hits = [v for k, v in d["kernels"].items() if re.search(kernel_re, k)]
+        if grid is not None:
+            vals = [v.get("by_grid", {}).get(str(grid), {}).get("hbm_bytes_per_launch")
+                    for v in hits]
+        else:
+            vals = [v.get("hbm_bytes_per_launch_largest") for v in hits]
+        vals = [x for x in vals if x is not None]
+        return max(vals) if vals else None
     return None
 
 
@@ -248,7 +260,7 @@ def pmc_valu(kernel_substr, batch):
         if d.get("per_gpu_batch") != batch:
             continue
         for k, v in d["kernels"].items():
-            if kernel_substr in k:
+            if __import__("re").search(kernel_substr, k):
                 v = dict(v)
                 if v.get("valu_cycles_per_inst") != 2:
                     v["valu_issue_frac"] = round(v["valu_issue_frac"] / 2, 4)
@@ -477,9 +489,11 @@ def main_train(args, world, rank, dev):
     batch args.batch, as BraTSTrainer does it (3_train.py:96-102, trainer.py:458-466):
     DiceCE(to_onehot_y, softmax) -> backward -> clip_grad_norm_(12) -> AdamW(1e-4).  N > 1: DDP
     over RCCL (bucketed all-reduce of the fp32 gradients, overlapped with the backward).
-    Encoder forward = HIP kernels (bf16x3 MFMA), encoder backward = HIP kernels + hipBLASLt
-    fp32 GEMM gradients, decoder 3^3 convolutions = HIP forward / input- / weight-gradient
-    kernels, 1x1 / transposed convs = hipBLASLt GEMMs (no MIOpen convolution, no find)."""
+    Encoder forward = HIP kernels (bf16x3 MFMA), encoder backward = HIP kernels + the
+    library's MFMA GEMMs (bf16x3 data gradients, wf_gemm_tn weight gradients), decoder 3^3
+    convolutions = HIP forward / input- / weight-gradient kernels, 1x1 / transposed convs = the
+    same MFMA GEMMs (no MIOpen convolution, no find; torch.mm only for the 4-channel shapes).
+    AdamW runs fused (one kernel per step for all parameters)."""
     import waveformer_amd.network_models as NM
     from waveformer_amd.losses import DiceCELoss
     torch.manual_seed(0)
@@ -495,7 +509,9 @@ def main_train(args, world, rank, dev):
         ddp = torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[dev.index], bucket_cap_mb=64, gradient_as_bucket_view=True,
             find_unused_parameters=True)  # as the reference trainer (trainer.py:355-358)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4)
+    # fused: one multi-tensor kernel per step instead of the foreach path's ~10 elementwise
+    # passes over the parameters (the same AdamW update, trainer.py:452-466)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=True)
     loss_fn = DiceCELoss(to_onehot_y=True, softmax=True)
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     x = torch.randn(args.batch, 4, args.img, args.img, args.img, device=dev, generator=g)
@@ -638,7 +654,8 @@ def main():
 
     roof_op = args.roofline_op if args.roofline_op != "auto" else "ccf_ffn_dwconv"
     timers = {n: OpTimer(n) for n in dict.fromkeys(
-        [roof_op, "dwt3d_haar", "msfuse", "window_attention"] + (["conv3d_k3"] if full else []))}
+        [roof_op, "dwt3d_haar", "dwt3d_haar_ll", "msfuse", "window_attention"]
+        + (["conv3d_k3"] if full else []))}
 
     def step():
         with torch.no_grad():

@@ -234,9 +234,11 @@ def test_gemm_tn_vs_fp64(M, N, K, pad):
                                              (384, 192, (4, 4, 4), False)])
 def test_conv1x1_and_convtranspose2_autograd(cin, cout, S, bias):
     """The decoder's 1x1 convs (wfa.Conv1x1Fn) and 2^3 transposed convs (wfa.ConvT2Fn) in
-    training: fp32 GEMM forward / input gradient, weight gradient on wf_gemm_tn, bias by column
-    sums -- against fp64 CPU autograd: rel-L2 <= 2e-6 for the fp32 GEMMs' output / input
-    gradient, <= 1e-5 for the bf16x3 weight gradient."""
+    training: forward and input gradient on the streaming MFMA GEMM (bf16x3 operands; the
+    48 -> 4 head's input gradient has K = 4 and stays on torch.mm), weight gradient on
+    wf_gemm_tn, bias by column sums -- against fp64 CPU autograd: rel-L2 <= 1e-5 for the bf16x3
+    products (operands carried to 16 mantissa bits, fp32 accumulation; round 5 held the fp32
+    GEMMs to 2e-6), 2e-6 for the bias column sums."""
     from waveformer_amd import autograd as wfa
     x = seeded_randn((2, cin) + S, 50)
     conv = torch.nn.Conv3d(cin, cout, 1, bias=bias)
@@ -256,8 +258,8 @@ def test_conv1x1_and_convtranspose2_autograd(cin, cout, S, bias):
         xg = x.cuda().requires_grad_(True)
         y = wfa.conv_train(mc, xg)
         y.backward(g.cuda())
-        assert C.rel_l2(y, yd.detach()) <= 2e-6
-        assert C.rel_l2(xg.grad, xd.grad) <= 2e-6
+        assert C.rel_l2(y, yd.detach()) <= 1e-5
+        assert C.rel_l2(xg.grad, xd.grad) <= 1e-5
         assert C.rel_l2(mc.weight.grad, md.weight.grad) <= 1e-5
         if bias:
             assert C.rel_l2(mc.bias.grad, md.bias.grad) <= 2e-6

@@ -94,3 +94,39 @@ def test_data_write_seen_by_graph_replay():
     assert not torch.equal(before[0], static[0])
     for a, b in zip(static, want):
         assert torch.equal(a, b)
+
+
+def test_arenas_bounded_over_fresh_threads():
+    """one weight arena per thread identity, never freed.  Forwards on six
+    short-lived threads, one after another: the arenas of ended threads are retired at the next
+    scope entry, so the model holds at most this thread's and the last worker's.  Every thread
+    computes the same output."""
+    import threading
+
+    from waveformer_amd import ops
+    m = _encoder()
+    x = seeded_randn((1, 4, 32, 32, 32), 73).cuda()
+    with torch.no_grad():
+        want = _flat(m(x))
+    outs, errs = [], []
+
+    def work():
+        try:
+            with torch.no_grad():
+                outs.append(_flat(m(x)))
+            torch.cuda.synchronize()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    for _ in range(6):
+        t = threading.Thread(target=work)
+        t.start()
+        t.join()
+        assert ops.arena_count(m) <= 2
+    assert not errs, errs
+    with torch.no_grad():
+        m(x)  # the main thread's next forward retires the last worker's arena
+    assert ops.arena_count(m) == 1
+    for o in outs:
+        for a, b in zip(o, want):
+            assert torch.equal(a, b)

@@ -7,7 +7,8 @@ rel-L2 <= 1e-5 per tensor (fp32 CPU both sides); 3e-5 on the (sum, sum of square
 dot) summaries kept for the encoder / full model, whose long fp32 reductions differ in order.
 
 GPU: the product modules in autograd mode (HIP forward with the fp32-faithful bf16x3 MFMA
-operands, HIP/fp32 backward kernels, hipBLASLt fp32 GEMM gradients) against the same
+operands, HIP/fp32 backward kernels, GEMM gradients on the library's bf16x3 MFMA GEMMs since
+round 6 -- hipBLASLt fp32 before) against the same
 fixtures.  Tolerance rel-L2 <= 2e-4 per gradient tensor for modules, 2e-3 through the
 encoder (the forward's split-bf16 products carry ~2^-17 relative error each and the forward
 outputs are within 1e-4 of the reference; the backward recomputes the softmax from fp32 scores

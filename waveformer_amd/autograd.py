@@ -3,9 +3,14 @@
 The reference trains with PyTorch autograd through the same modules (3_train.py:99-135, fp32,
 trainer.py:454).  Here each hot-path op is one autograd.Function whose forward is the HIP
 forward kernel (saving what its backward needs) and whose backward is the HIP backward kernels
-of csrc/train.hip, with the dense GEMM gradients (dX = dY W, dW = dY^T X) on the platform
-BLAS (torch.mm -> hipBLASLt, fp32).  The modules in network_models switch to these Functions
-when autograd is recording (`needs_grad`); inference keeps the fused kernels.
+of csrc/train.hip.  The dense GEMMs of the step run on the library's own MFMA GEMMs at bf16x3
+(fp32-faithful operands, fp32 accumulation): the data gradients dX = dY W and the 1x1 /
+transposed-conv forwards on the streaming GEMM (ops.mm_rows / linear_rows_any /
+convtranspose2_cl), the weight gradients dW = dY^T X on wf_gemm_tn -- no hipBLASLt on the
+step, except the shapes those kernels do not take (a channel count not a multiple of 8 / 4:
+the 4-channel input and output convolutions), which fall back to torch.mm.  The modules in
+network_models switch to these Functions when autograd is recording (`needs_grad`);
+inference keeps the fused kernels.
 
 Training always computes in fp32-faithful mode (bf16x3 forward, fp32 backward): the forward
 workspaces the backward consumes are fp32 in that mode.
@@ -140,7 +145,7 @@ class PatchEmbedFn(torch.autograd.Function):
         if b is not None and ctx.needs_input_grad[2]:
             db = colsum(g)
         if ctx.needs_input_grad[0]:
-            drows = g.mm(w.reshape(Cout, Cin * 8))
+            drows = ops.mm_rows(g, w.reshape(Cout, Cin * 8))
             dx = torch.empty_like(x)
             _lib.call("wf_patchify", dx.data_ptr(), drows.data_ptr(), 1, B, Cin, D, H, W, _s())
         return dx, dw, db
@@ -248,7 +253,7 @@ def conv3d_k3(x, w, b=None):
 
 # ------------------------------------------------------------------------------------------
 # the decoder's other convolutions in training: depthwise 3^3 on HIP, 1x1 and the 2^3
-# transposed conv as channel-last GEMMs (hipBLASLt) -- no MIOpen convolution anywhere, so a
+# transposed conv as channel-last MFMA GEMMs -- no MIOpen convolution anywhere, so a
 # training step needs no MIOpen find / kernel compilation (minutes at B = 4 on a fresh box)
 # ------------------------------------------------------------------------------------------
 class DWConv3dK3(torch.autograd.Function):
@@ -322,17 +327,17 @@ def conv_train(conv: torch.nn.Module, x: torch.Tensor) -> torch.Tensor:
 
 
 class Conv1x1Fn(torch.autograd.Function):
-    """Conv3d(k=1) over channel-last position rows: y = x W^T + b (fp32 GEMM), dx = dy W (fp32
-    GEMM), dW = dy^T x on wf_gemm_tn (the platform BLAS put this long-K shape on a handful of
-    workgroups: 1.8-8 ms per call at 128^3), db = column sums (deterministic)."""
+    """Conv3d(k=1) over channel-last position rows: y = x W^T + b and dx = dy W on the
+    streaming MFMA GEMM (bf16x3; torch.mm for channel counts it does not take), dW = dy^T x on
+    wf_gemm_tn (the platform BLAS put this long-K shape on a handful of workgroups: 1.8-8 ms per
+    call at 128^3), db = column sums (deterministic)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         B, Cin, D, H, W = x.shape
         Cout = w.shape[0]
         rows = _rows(x).reshape(-1, Cin)
-        w2 = w.view(Cout, Cin)
-        y = torch.addmm(b, rows, w2.t()) if b is not None else rows.mm(w2.t())
+        y = ops.linear_rows_any(rows, w.view(Cout, Cin), b)
         ctx.save_for_backward(rows, w)
         ctx.has_bias, ctx.shape = b is not None, (B, D, H, W)
         return y.view(B, D, H, W, Cout).permute(0, 4, 1, 2, 3)
@@ -345,7 +350,7 @@ class Conv1x1Fn(torch.autograd.Function):
         gr = _rows(g).reshape(-1, Cout)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = gr.mm(w.view(Cout, Cin)).view(B, D, H, W, Cin).permute(0, 4, 1, 2, 3)
+            dx = ops.mm_rows(gr, w.view(Cout, Cin)).view(B, D, H, W, Cin).permute(0, 4, 1, 2, 3)
         if ctx.needs_input_grad[1]:
             dw = ops.gemm_tn(gr, rows).view_as(w)
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -355,21 +360,26 @@ class Conv1x1Fn(torch.autograd.Function):
 
 class ConvT2Fn(torch.autograd.Function):
     """ConvTranspose3d(k=2, s=2) (unetr_block.py:73-80) as one GEMM into the 8 sub-voxels:
-    y[2z+dz, 2y+dy, 2x+dx] = x W[:, :, dz, dy, dx] + b.  Backward: the sub-voxel gradient rows
-    (M, 8 Cout), dx = rows . Wr^T (fp32 GEMM), dW = x^T rows on wf_gemm_tn, db = column sums."""
+    y[2z+dz, 2y+dy, 2x+dx] = x W[:, :, dz, dy, dx] + b -- the MFMA GEMM whose epilogue stores
+    each sub-voxel + bias (wf_convtranspose2_cl, bf16x3).  Backward: the sub-voxel gradient
+    rows (M, 8 Cout), dx = rows . Wr^T on the streaming MFMA GEMM, dW = x^T rows on wf_gemm_tn,
+    db = column sums.  Channel counts the kernels do not take use torch.mm."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         B, Cin, d, h, ww = x.shape
         Cout = w.shape[1]
         rows = _rows(x).reshape(-1, Cin)
+        ctx.save_for_backward(rows, w)
+        ctx.has_bias, ctx.shape = b is not None, (B, d, h, ww)
+        if Cin % 8 == 0 and Cout % 4 == 0:
+            y = ops.empty_cl(B, Cout, 2 * d, 2 * h, 2 * ww, x.device)
+            return ops.convtranspose2_cl(x, w.detach(), None if b is None else b.detach(), y)
         wr = w.permute(0, 2, 3, 4, 1).reshape(Cin, 8 * Cout)
         y = (rows @ wr).view(B, d, h, ww, 2, 2, 2, Cout)
         y = y.permute(0, 1, 4, 2, 5, 3, 6, 7).reshape(B, 2 * d, 2 * h, 2 * ww, Cout)
         if b is not None:
             y = y + b
-        ctx.save_for_backward(rows, w)
-        ctx.has_bias, ctx.shape = b is not None, (B, d, h, ww)
         return y.permute(0, 4, 1, 2, 3)
 
     @staticmethod
@@ -383,7 +393,7 @@ class ConvT2Fn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             wr = w.permute(0, 2, 3, 4, 1).reshape(Cin, 8 * Cout)
-            dx = gsub.mm(wr.t()).view(B, d, h, ww, Cin).permute(0, 4, 1, 2, 3)
+            dx = ops.mm_rows(gsub, wr.t()).view(B, d, h, ww, Cin).permute(0, 4, 1, 2, 3)
         if ctx.needs_input_grad[1]:
             dw = ops.gemm_tn(rows, gsub).view(Cin, 2, 2, 2, Cout).permute(0, 4, 1, 2, 3)
         if ctx.has_bias and ctx.needs_input_grad[2]:

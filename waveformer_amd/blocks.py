@@ -7,8 +7,8 @@ These are the decoder's full-resolution 3^3 convolutions.  In
 (ops.conv3d_k3), InstanceNorm statistics and one fused norm + residual + LeakyReLU pass
 (ops.instnorm_stats / ops.norm_act), the 1x1 residual conv as one GEMM.  Training (autograd)
 runs every convolution through wfa.conv_train: the 3^3 convs on the HIP forward / input- /
-weight-gradient kernels, 1x1 and 2^3 transposed convs as hipBLASLt GEMMs -- no MIOpen
-convolution, hence no MIOpen find.  norm_name is always "instance" (InstanceNorm3d, affine=False) and the
+weight-gradient kernels, 1x1 and 2^3 transposed convs on the library's MFMA GEMMs -- no MIOpen
+convolution, hence no MIOpen find, and no hipBLASLt but for the 4-channel shapes.  norm_name is always "instance" (InstanceNorm3d, affine=False) and the
 activation LeakyReLU(0.01), as Waveformer builds them.
 """
 from __future__ import annotations
@@ -285,8 +285,9 @@ class UnetrUpBlock(nn.Module):
     @staticmethod
     def _upsample_cat(inp, skip, tc, skip_in_place=False):
         """ConvTranspose3d(k=2, s=2) + torch.cat((out, skip), 1) into one channel-last buffer:
-        the transposed conv is one fp32 GEMM (positions x Cin) . (Cin x 8 Cout) whose columns
-        are the 8 sub-voxels, scattered straight into the buffer's first Cout channels."""
+        the transposed conv is one GEMM (positions x Cin) . (Cin x 8 Cout) whose columns are the
+        8 sub-voxels, stored straight into the buffer's first Cout channels (the MFMA GEMM's
+        sub-voxel epilogue; an fp32 torch GEMM + scatter for channel counts it does not take)."""
         B, Cin, d, h, w = inp.shape
         Cout = tc.out_channels
         if tuple(skip.shape) != (B, skip.shape[1], 2 * d, 2 * h, 2 * w):

@@ -505,6 +505,29 @@ __device__ __forceinline__ int kswz(int row) {  // 16-B chunk XOR of a K row (se
 #ifndef WF_ATTN_T4  // 1: bias quads as single ds_read_b128 (A/B; 0: four scalar reads)
 #define WF_ATTN_T4 1
 #endif
+// WF_ATTN_LAZY (round 6): the running max is kept while no score of a 64-key tile exceeds it
+// by more than 2^WF_ATTN_TAU in the exp2 domain (a lane-local max + one wave ballot); only then
+// does the tile pay the cross-group max exchange (two ds_bpermute round trips on the
+// critical path), the alpha exponential and the o / l rescale.  The exponentials of a kept tile
+// are at most 2^TAU; the normalisation o / l is the same quotient, so this changes only fp32
+// rounding.  0: the max is exchanged and the rescale applied on every tile (round 5).
+#ifndef WF_ATTN_LAZY
+#define WF_ATTN_LAZY 1
+#endif
+#ifndef WF_ATTN_TAU
+#define WF_ATTN_TAU 16.0f
+#endif
+// WF_ATTN_DOT2 (round 6, bf16x3): the split's lo part of a pair of probabilities is
+// bf16(p - hi) with p - hi from one v_dot2c_f32_bf16 per value (the packed hi pair against
+// (-1, 0) / (0, -1), accumulated onto p) instead of unpacking hi back to fp32 and subtracting
+// (two VALU ops per value).  p - hi is exact in fp32, so the operands are bitwise the same.
+#ifndef WF_ATTN_DOT2
+#define WF_ATTN_DOT2 1
+#endif
+// WF_ATTN_QP (round 6): two 16-query sub-tiles per wave in one loop (see the kernel); 0: one
+#ifndef WF_ATTN_QP
+#define WF_ATTN_QP 1
+#endif
 template <int P>
 __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict__ qkv,
                                                           const float* __restrict__ table,
@@ -519,15 +542,24 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
   // contiguous inside one block
   constexpr int VB = HD * 4 + 4;
   constexpr int VQ = (N / 4) * VB;
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[N * KS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vq[2 * VQ];
+  // one LDS block, the table first: its quads then sit below the 64-KiB reach of the ds_read
+  // offset field, so a tile's 4 bias reads are one base register + immediates (separate
+  // __shared__ arrays were placed table-last, 72 KB up: one address add per read)
 #if WF_ATTN_T4
   // the reversed table as overlapping quads: tq[i] = {tbr[i], tbr[i+1], tbr[i+2], tbr[i+3]},
   // so a lane's 4 consecutive bias values are one aligned ds_read_b128
-  __shared__ __attribute__((aligned(16))) f32x4 tq[TBLN];
+  constexpr int TQ_BYTES = TBLN * 16;
 #else
-  __shared__ __attribute__((aligned(16))) float tbr[TBLN + 1];  // reversed, x log2 e
+  constexpr int TQ_BYTES = ((TBLN + 1) * 4 + 15) / 16 * 16;
 #endif
+  __shared__ __attribute__((aligned(16))) uint8_t lds_tbl[TQ_BYTES + N * KS * 2 + 2 * VQ * 2];
+#if WF_ATTN_T4
+  f32x4* tq = reinterpret_cast<f32x4*>(lds_tbl);
+#else
+  float* tbr = reinterpret_cast<float*>(lds_tbl);  // reversed, x log2 e
+#endif
+  uint16_t* Ks = reinterpret_cast<uint16_t*>(lds_tbl + TQ_BYTES);
+  uint16_t* Vq = Ks + N * KS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int qs, h;
   int64_t bw;
@@ -581,6 +613,125 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
   const short one = (short)op_cvt<P>(1.0f);
   const bf16x8 ones = bf16x8{one, one, one, one, one, one, one, one};
   const int nsub = N / 16 / qsplit;  // 16-query sub-tiles of this workgroup
+#if WF_ATTN_QP
+  static_assert(WF_ATTN_LAZY && WF_ATTN_MFMA_SUM && WF_ATTN_T4 && WF_ATTN_BPERMUTE,
+                "the query-pair loop implements the default options only");
+  if (nsub >= 16) {
+    // two independent 16-query sub-tiles per wave (st and st + 8): every K / V fragment read
+    // from LDS feeds both, and the two sub-tiles' dependency chains (scores -> max -> exp ->
+    // PV) interleave -- the single-sub-tile loop left the SIMDs waiting on those chains with
+    // four waves each (LDS caps the workgroups at two per CU)
+    constexpr int NQ = 2;
+    for (int st = wid; st < nsub; st += 8 * NQ) {
+      int qq[NQ], rbq[NQ];
+      bf16x8 b1[NQ], b2[NQ];
+      f32x4 o[NQ], l4[NQ];
+      float mrun[NQ];
+#pragma unroll
+      for (int u = 0; u < NQ; ++u) {
+        const int q = qs * (N / qsplit) + (st + 8 * u) * 16 + l15;
+        qq[u] = q;
+        bf16x8 hi = z8, lo = z8;
+        load8_split_scaled<P>(qkv, (row0 + q) * ld + h * HD + 8 * (g4 & 1), scale_log2, hi, lo);
+        b1[u] = hi;
+        b2[u] = (SPLIT && g4 < 2) ? lo : z8;
+        const int qz = q >> 6, qy = (q >> 3) & 7, qx = q & 7;
+        rbq[u] = (TBLN - 1) - ((qz + 7) * 23 + (qy + 7) * 15 + (qx + 7)) +
+                 ((g4 >> 1) * 15 + 4 * (g4 & 1));
+        o[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        l4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mrun[u] = -INFINITY;
+      }
+      for (int t = 0; t < 8; ++t) {
+        f32x4 s[NQ][4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ks[(t * 64 + kt * 16 + l15) * KS + kch]);
+#pragma unroll
+          for (int u = 0; u < NQ; ++u) {
+            s[u][kt] = mma32<P>(a, b1[u], tq[rbq[u] + 23 * t + 30 * kt]);
+            if (SPLIT) s[u][kt] = mma32<P>(a, b2[u], s[u][kt]);
+          }
+        }
+        float lmax[NQ];
+        bool big = false;
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+          lmax[u] = s[u][0][0];
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int i = (kt == 0 ? 1 : 0); i < 4; ++i) lmax[u] = fmaxf(lmax[u], s[u][kt][i]);
+          big = big || lmax[u] > mrun[u] + WF_ATTN_TAU;
+        }
+        if (__builtin_amdgcn_ballot_w64(big) != 0) {  // wave-uniform
+#pragma unroll
+          for (int u = 0; u < NQ; ++u) {
+            float tmax = fmaxf(mrun[u], lmax[u]);
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+            tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+            const float alpha = __builtin_amdgcn_exp2f(mrun[u] - tmax);  // 0 on the first tile
+            mrun[u] = tmax;
+            o[u] *= alpha;
+            l4[u] *= alpha;
+          }
+        }
+        uint32_t ph[NQ][4][2], pl[NQ][4][2];
+#pragma unroll
+        for (int u = 0; u < NQ; ++u)
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int i = 0; i < 4; i += 2)
+              split_pair<P>(__builtin_amdgcn_exp2f(s[u][kt][i] - mrun[u]),
+                            __builtin_amdgcn_exp2f(s[u][kt][i + 1] - mrun[u]), ph[u][kt][i >> 1],
+                            pl[u][kt][i >> 1]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int o1 = (16 * t + 8 * j + g4) * VB + l15 * 4;
+          const int o2 = (16 * t + 8 * j + 4 + g4) * VB + l15 * 4;
+          const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(&Vq[o1]);
+          const bf16x4 v2 = *reinterpret_cast<const bf16x4*>(&Vq[o2]);
+          const bf16x8 vh = bf16x8{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+          bf16x8 vl = z8;
+          if (SPLIT) {
+            const bf16x4 w1 = *reinterpret_cast<const bf16x4*>(&Vq[VQ + o1]);
+            const bf16x4 w2 = *reinterpret_cast<const bf16x4*>(&Vq[VQ + o2]);
+            vl = bf16x8{w1[0], w1[1], w1[2], w1[3], w2[0], w2[1], w2[2], w2[3]};
+          }
+#pragma unroll
+          for (int u = 0; u < NQ; ++u) {
+            const bf16x8 pb = __builtin_bit_cast(
+                bf16x8, u32x4{ph[u][2 * j][0], ph[u][2 * j][1], ph[u][2 * j + 1][0], ph[u][2 * j + 1][1]});
+            if (SPLIT) {
+              const bf16x8 plb = __builtin_bit_cast(
+                  bf16x8, u32x4{pl[u][2 * j][0], pl[u][2 * j][1], pl[u][2 * j + 1][0], pl[u][2 * j + 1][1]});
+              o[u] = mma32<P>(vl, pb, o[u]);
+              o[u] = mma32<P>(vh, plb, o[u]);
+              l4[u] = mma32<P>(ones, plb, l4[u]);
+            }
+            o[u] = mma32<P>(vh, pb, o[u]);
+            l4[u] = mma32<P>(ones, pb, l4[u]);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NQ; ++u) {
+        const float inv = 1.f / l4[u][0];
+        const int64_t off = (row0 + qq[u]) * C + h * HD + 4 * g4;
+        if (store32(P)) {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off) = o[u] * inv;
+        } else {
+          bf16x4 r;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) r[i] = (short)f2bf(o[u][i] * inv);
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(out) + off) = r;
+        }
+      }
+    }
+    return;
+  }
+#endif
   for (int st = wid; st < nsub; st += 8) {
     const int q = qs * (N / qsplit) + st * 16 + l15;
     // B operands of S: slots 8 g4 .. +7 <- Q'[q][8 (g4 & 1) ..]: [Q'h | Q'h] and [Q'l | 0]
@@ -625,6 +776,27 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
     for (int t = 0; t < 8; ++t) {  // 64-key tiles (one z slice of the window each)
       f32x4 s[4];
       scores(t, s);
+#if WF_ATTN_LAZY
+      float lmax = s[0][0];  // a chain, so the compiler pairs it into v_max3_f32
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = (kt == 0 ? 1 : 0); i < 4; ++i) lmax = fmaxf(lmax, s[kt][i]);
+      if (__builtin_amdgcn_ballot_w64(lmax > mrun + WF_ATTN_TAU) != 0) {  // wave-uniform
+        float tmax = fmaxf(mrun, lmax);
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float alpha = __builtin_amdgcn_exp2f(mrun - tmax);  // 0 on the first tile
+        mrun = tmax;
+        o *= alpha;
+#if WF_ATTN_MFMA_SUM
+        l4 *= alpha;
+#else
+        lsum *= alpha;
+#endif
+      }
+      const float mnew = mrun;
+#else
       float tmax = mrun;  // a chain, so the compiler pairs it into v_max3_f32
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
@@ -649,43 +821,53 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
       const float mnew = tmax;
       const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
       mrun = mnew;
-      bf16x4 ph[4], pl[4];
+      o *= alpha;
+#if WF_ATTN_MFMA_SUM
+      l4 *= alpha;
+#else
+      lsum *= alpha;
+#endif
+#endif  // WF_ATTN_LAZY
+      // P^T operand words: pairs of 16-bit values, hi and (bf16x3) lo parts
+      uint32_t ph[4][2], pl[4][2];
 #if !WF_ATTN_MFMA_SUM
       float ps[4];
 #endif
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = __builtin_amdgcn_exp2f(s[kt][i] - mnew);
-          const uint16_t hb = op_cvt<P>(p);
-          ph[kt][i] = (short)hb;
-          pl[kt][i] = op_lo<P>(p, hb);
+        for (int i = 0; i < 4; i += 2) {
+          const float p0 = __builtin_amdgcn_exp2f(s[kt][i] - mnew);
+          const float p1 = __builtin_amdgcn_exp2f(s[kt][i + 1] - mnew);
+          if (WF_ATTN_DOT2) {
+            split_pair<P>(p0, p1, ph[kt][i >> 1], pl[kt][i >> 1]);
+          } else {
+            const uint16_t hb0 = op_cvt<P>(p0), hb1 = op_cvt<P>(p1);
+            ph[kt][i >> 1] = (uint32_t)hb0 | ((uint32_t)hb1 << 16);
+            pl[kt][i >> 1] = (uint32_t)(uint16_t)op_lo<P>(p0, hb0) |
+                             ((uint32_t)(uint16_t)op_lo<P>(p1, hb1) << 16);
+          }
 #if !WF_ATTN_MFMA_SUM
-          ps[i] = kt == 0 ? p : ps[i] + p;  // 4 chains over the key sub-tiles
+          ps[i] = kt == 0 ? p0 : ps[i] + p0;  // 4 chains over the key sub-tiles
+          ps[i + 1] = kt == 0 ? p1 : ps[i + 1] + p1;
 #endif
         }
       }
 #if !WF_ATTN_MFMA_SUM
-      lsum = lsum * alpha + ((ps[0] + ps[1]) + (ps[2] + ps[3]));
-#endif
-      o *= alpha;
-#if WF_ATTN_MFMA_SUM
-      l4 *= alpha;
+      lsum += (ps[0] + ps[1]) + (ps[2] + ps[3]);
 #endif
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const bf16x8 pb = bf16x8{ph[2 * j][0], ph[2 * j][1], ph[2 * j][2], ph[2 * j][3],
-                                 ph[2 * j + 1][0], ph[2 * j + 1][1], ph[2 * j + 1][2], ph[2 * j + 1][3]};
+        const bf16x8 pb = __builtin_bit_cast(
+            bf16x8, u32x4{ph[2 * j][0], ph[2 * j][1], ph[2 * j + 1][0], ph[2 * j + 1][1]});
         const int o1 = (16 * t + 8 * j + g4) * VB + l15 * 4;
         const int o2 = (16 * t + 8 * j + 4 + g4) * VB + l15 * 4;
         const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(&Vq[o1]);
         const bf16x4 v2 = *reinterpret_cast<const bf16x4*>(&Vq[o2]);
         const bf16x8 vh = bf16x8{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
         if (SPLIT) {
-          const bf16x8 plb = bf16x8{pl[2 * j][0], pl[2 * j][1], pl[2 * j][2], pl[2 * j][3],
-                                    pl[2 * j + 1][0], pl[2 * j + 1][1], pl[2 * j + 1][2],
-                                    pl[2 * j + 1][3]};
+          const bf16x8 plb = __builtin_bit_cast(
+              bf16x8, u32x4{pl[2 * j][0], pl[2 * j][1], pl[2 * j + 1][0], pl[2 * j + 1][1]});
           const bf16x4 w1 = *reinterpret_cast<const bf16x4*>(&Vq[VQ + o1]);
           const bf16x4 w2 = *reinterpret_cast<const bf16x4*>(&Vq[VQ + o2]);
           const bf16x8 vl = bf16x8{w1[0], w1[1], w1[2], w1[3], w2[0], w2[1], w2[2], w2[3]};

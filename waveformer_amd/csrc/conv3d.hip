@@ -226,12 +226,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
       f32x4 v = sa[XH ? 0 : j];
       if (!cok || !((gmask >> j) & 1u)) v = f32x4{0, 0, 0, 0};
       bf16x4 h, l;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint16_t hb = op_cvt<P>(v[e]);
-        h[e] = (short)hb;
-        l[e] = op_lo<P>(v[e], hb);
-      }
+      split4<P>(v, h, l);
       *reinterpret_cast<bf16x4*>(s_hi + pos * PS + 4 * q) = h;
       if (SPLIT) *reinterpret_cast<bf16x4*>(s_lo + pos * PS + 4 * q) = l;
     }
@@ -558,12 +553,7 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
         if (mine) {
           const f32x4 v = ok ? sa[j] : f32x4{0, 0, 0, 0};
           bf16x4 h, l;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const uint16_t hb = op_cvt<P>(v[e]);
-            h[e] = (short)hb;
-            l[e] = op_lo<P>(v[e], hb);
-          }
+          split4<P>(v, h, l);
           *reinterpret_cast<bf16x4*>(s_act + paddr(pos) + 8 * (q & 1)) = h;
           *reinterpret_cast<bf16x4*>(s_act + paddr(pos) + 16 + 8 * (q & 1)) = l;
         }

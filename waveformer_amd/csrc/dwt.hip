@@ -26,14 +26,16 @@ __global__ __launch_bounds__(256) void dwt3d_haar_fwd_kernel(
     float ln_eps, float* __restrict__ bands, int B, int C, int D, int H, int W) {
   const int C4 = C >> 2;
   const int d = D >> 1, h = H >> 1, w = W >> 1;
-  const int64_t P = (int64_t)d * h * w;           // output positions per batch
-  const int64_t total = (int64_t)B * P;
+  // output positions in 32 bits (the host's element bound keeps them below 2^28): the
+  // position decode is three 32-bit divisions instead of the software 64-bit ones
+  const uint32_t P = (uint32_t)d * h * w;         // output positions per batch
+  const uint32_t total = (uint32_t)B * P;
   const int lane = threadIdx.x & 63;
   const int gl = lane & (G - 1);
   const int groups_per_block = blockDim.x / G;
-  const int64_t gid0 = (int64_t)blockIdx.x * groups_per_block + threadIdx.x / G;
-  const int64_t gstride = (int64_t)gridDim.x * groups_per_block;
-  const int64_t band_stride = total * C;          // elements per band
+  const uint32_t gid0 = blockIdx.x * (uint32_t)groups_per_block + threadIdx.x / G;
+  const uint32_t gstride = gridDim.x * (uint32_t)groups_per_block;
+  const int64_t band_stride = (int64_t)total * C;  // elements per band
 
   bool live[V];
   f32x4 gw[V], gb[V];
@@ -47,13 +49,13 @@ __global__ __launch_bounds__(256) void dwt3d_haar_fwd_kernel(
     }
   }
 
-  for (int64_t g = gid0; g < total; g += gstride) {
+  for (uint32_t g = gid0; g < total; g += gstride) {
     const int b = (int)(g / P);
-    int64_t p = g - (int64_t)b * P;
-    const int ox = (int)(p % w);
-    p /= w;
-    const int oy = (int)(p % h);
-    const int oz = (int)(p / h);
+    uint32_t p = g - (uint32_t)b * P;
+    const int ox = (int)(p % (uint32_t)w);
+    p /= (uint32_t)w;
+    const int oy = (int)(p % (uint32_t)h);
+    const int oz = (int)(p / (uint32_t)h);
 
     f32x4 v[8][V];
 #pragma unroll
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256) void dwt3d_haar_fwd_kernel(
         }
       }
     }
-    const int64_t obase = g * C;
+    const int64_t obase = (int64_t)g * C;
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       f32x4* dst = reinterpret_cast<f32x4*>(bands + k * band_stride + obase);
@@ -233,15 +235,17 @@ __global__ __launch_bounds__(256) void idwt3d_haar_cl4_kernel(IdwtArgs a, int64_
   if (t >= total) return;
   const int L = a.levels, C4 = a.C >> 2;
   const int w1 = a.w << (L - 1), h1 = a.h << (L - 1), d1 = a.d << (L - 1);
-  int64_t r = t;
-  const int c = 4 * (int)(r % C4);
-  r /= C4;
-  const int x1 = (int)(r % w1);
-  r /= w1;
-  const int y1 = (int)(r % h1);
-  r /= h1;
-  const int z1 = (int)(r % d1);
-  const int b = (int)(r / d1);
+  // decoded in 32 bits (the host launches this kernel for total < 2^31): 64-bit divisions are
+  // software routines, five of them per 256 B moved
+  uint32_t r = (uint32_t)t;
+  const int c = 4 * (int)(r % (uint32_t)C4);
+  r /= (uint32_t)C4;
+  const int x1 = (int)(r % (uint32_t)w1);
+  r /= (uint32_t)w1;
+  const int y1 = (int)(r % (uint32_t)h1);
+  r /= (uint32_t)h1;
+  const int z1 = (int)(r % (uint32_t)d1);
+  const int b = (int)(r / (uint32_t)d1);
   auto coef4 = [&](int l, int k, int z, int y, int x) {
     const int64_t Wl = (int64_t)a.w << l;
     const int64_t off = b * a.ds[4 * l] + c + z * a.ds[4 * l + 2] + ((int64_t)y * Wl + x) * a.ds[4 * l + 3];
@@ -504,11 +508,13 @@ static int idwt_launch(const float* ll, int64_t ll_bstride, int64_t ll_cs, int64
                    ldo % 4 == 0 && ldo >= 2 * C && al16(skip) && skip_ld % 4 == 0 &&
                    skip_ld >= C && skip_bstride % 4 == 0,
                "fused concat: channel-last LL / details / skip / output, 16-B aligned, C % 4 == 0");
+    WF_REQUIRE(B * d1 * h1 * w1 * (C / 4) < ((int64_t)1 << 31), "fused concat: volume too large");
     a.skip = skip;
     a.skip_bstride = skip_bstride;
     a.skip_ld = skip_ld;
   }
-  if (vec && cl && ll_cs == 1 && ll_ps % 4 == 0 && ll_bstride % 4 == 0 && al16(ll) && ldo % 4 == 0) {
+  if (vec && cl && ll_cs == 1 && ll_ps % 4 == 0 && ll_bstride % 4 == 0 && al16(ll) && ldo % 4 == 0 &&
+      B * d1 * h1 * w1 * (C / 4) < ((int64_t)1 << 31)) {
     const int64_t total = B * d1 * h1 * w1 * (C / 4);
     if (skip)
       hipLaunchKernelGGL(idwt3d_haar_cl4_kernel<true>, dim3((unsigned)cdiv(total, 256)),

@@ -1332,15 +1332,11 @@ __global__ __launch_bounds__(768, 1) void ffn_dwfc2_kernel(DwFcArgs a) {
       const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + cc);
       const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + cc);
       const f32x4 y = gelu_half4((v[j] * rstd + nmr) * lw4 + lb4);
-      bf16x4 hi4, lo4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint16_t hb = op_cvt<P>(y[e]);
-        hi4[e] = (short)hb;
-        lo4[e] = op_lo<P>(y[e], hb);
-      }
-      *reinterpret_cast<bf16x4*>(rowh + cc) = hi4;
-      if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + cc) = lo4;
+      uint32_t h0, h1, l0, l1;  // hi / lo operand words (split_pair: lo from v_dot2c)
+      split_pair<P>(y[0], y[1], h0, l0);
+      split_pair<P>(y[2], y[3], h1, l1);
+      *reinterpret_cast<u32x2*>(rowh + cc) = u32x2{h0, h1};
+      if (SPLIT) *reinterpret_cast<u32x2*>(rowh + HID + cc) = u32x2{l0, l1};
     }
   };
   // depthwise input rows scattered before barrier B by the F waves (sF) and waves 6, 7 (sG)

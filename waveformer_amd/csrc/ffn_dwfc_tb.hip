@@ -460,7 +460,13 @@ namespace tb4 {
 constexpr int C = 48, HID = 192, TY = 4, TX = 8;
 constexpr int PY = TY + 2, PX = TX + 2, PP = PY * PX;  // 6 x 10
 constexpr int NPOS = TY * TX;                          // 32
-constexpr int HS = HID + 4;
+// h2 rows are HID + 8 floats apart (50 16-B quads, 2 mod 16): the fc's B-fragment reads (16
+// rows x 4 k-quads per ds_read_b128) then meet 16 distinct 4-bank groups in every lane group,
+// and LN2 lane lg of row r takes the channel quads m, m + 16, m + 32 with m = (lg - 2 r) & 15,
+// which cancels the row's bank offset, so its reads (and its bf16 hi / lo writes) are
+// conflict-free as well.  Round 5's HID + 4 rows with 12 contiguous channels per LN2 lane had
+// 0.95 bank-conflict cycles per LDS instruction.
+constexpr int HS = HID + 8;
 constexpr int PLANE_F = PP * HID;
 constexpr int H2F = NPOS * HS;
 constexpr int NV = HID / 4;
@@ -468,7 +474,8 @@ constexpr int NPC = (PP * NV + 63) / 64;               // 45 LDS-DMA pieces
 constexpr int NPCE = (NPC + 3) / 4;
 constexpr int KS = HID / 32;
 constexpr int FWL_BYTES = (C / 16) * KS * 64 * 16;
-constexpr size_t LDS_BYTES = (size_t)(2 * PLANE_F + 2 * H2F + 2 * HID + 3 * C) * 4 + FWL_BYTES;
+// vectors: LN2 affine (HID each), fc bias + norm2 bias folded into one (C), norm2 weight (C)
+constexpr size_t LDS_BYTES = (size_t)(2 * PLANE_F + 2 * H2F + 2 * HID + 2 * C) * 4 + FWL_BYTES;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 }  // namespace tb4
 
@@ -481,13 +488,12 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
   // fragments the E waves read, instead of waiting for every DMA before any LDS read
   __shared__ __attribute__((aligned(16))) float planes[2 * PLANE_F];  // [2][PP][HID]
   __shared__ __attribute__((aligned(16))) float h2b[2 * H2F];         // [2][NPOS][HS]
-  __shared__ __attribute__((aligned(16))) float vecs[2 * HID + 3 * C];
+  __shared__ __attribute__((aligned(16))) float vecs[2 * HID + 2 * C];
   __shared__ bf16x8 fwlo[FWL_BYTES / 16];
   float* lnw = vecs;                       // [HID] (halved: GELU from x / 2)
   float* lnb = lnw + HID;
-  float* fcb = lnb + HID;
-  float* n2w = fcb + C;
-  float* n2b = n2w + C;
+  float* fcl = lnb + HID;                  // [C] fc bias (+ norm2 bias when stats are given)
+  float* n2w = fcl + C;                    // [C]
   __shared__ int simd_cnt[4];
 
   const int tid = threadIdx.x;
@@ -512,9 +518,8 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
     lnb[i] = 0.5f * a.ln2_b[i];
   }
   for (int i = tid; i < C; i += 1024) {
-    fcb[i] = a.fc_b ? a.fc_b[i] : 0.f;
+    fcl[i] = (a.fc_b ? a.fc_b[i] : 0.f) + (a.stats ? a.n2_b[i] : 0.f);
     n2w[i] = a.stats ? a.n2_w[i] : 1.f;
-    n2b[i] = a.stats ? a.n2_b[i] : 0.f;
   }
   if (SPLIT) {
     for (int i = tid; i < (C / 16) * KS * 64; i += 1024) {
@@ -547,8 +552,10 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
     for (int s = 0; s < 3; ++s)
 #pragma unroll
       for (int o = 0; o < TY; ++o) acc[s][o][0] = acc[s][o][1] = 0.f;
-    // LN2 (slots 0, 1): positions 8 cp + 4 kslot + (lane >> 4), channels 12 (lane & 15) ..
+    // LN2 (slots 0, 1): position 8 cp + 4 kslot + (lane >> 4), channel quads m, m + 16, m + 32
+    // of its row, m = (lg - 2 lpos) & 15 (conflict-free banks, see HS)
     const int lpos = 8 * cp + 4 * kslot + (lane >> 4), lg = lane & 15;
+    const int cm = 4 * ((lg - 2 * lpos) & 15);
     __syncthreads();  // (prologue) weights read out of the plane buffer
     __syncthreads();  // (prologue) plane z0-1 staged
 
@@ -558,7 +565,7 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
       float v[LNC];
 #pragma unroll
       for (int j = 0; j < LNC / 4; ++j) {
-        const f32x4 u = *reinterpret_cast<const f32x4*>(row + lg * LNC + 4 * j);
+        const f32x4 u = *reinterpret_cast<const f32x4*>(row + cm + 64 * j);
         v[4 * j] = u.x;
         v[4 * j + 1] = u.y;
         v[4 * j + 2] = u.z;
@@ -580,20 +587,16 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
       uint16_t* rowh = reinterpret_cast<uint16_t*>(row);
 #pragma unroll
       for (int j = 0; j < LNC / 4; ++j) {
-        const int cc = lg * LNC + 4 * j;
+        const int cc = cm + 64 * j;
         const f32x4 lw4 = *reinterpret_cast<const f32x4*>(lnw + cc);
         const f32x4 lb4 = *reinterpret_cast<const f32x4*>(lnb + cc);
         const f32x4 y = gelu_half4((f32x4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]} *
                                     rstd + nmr) * lw4 + lb4);
-        bf16x4 hi4, lo4;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint16_t hb = op_cvt<P>(y[k]);
-          hi4[k] = (short)hb;
-          lo4[k] = op_lo<P>(y[k], hb);
-        }
-        *reinterpret_cast<bf16x4*>(rowh + cc) = hi4;
-        if (SPLIT) *reinterpret_cast<bf16x4*>(rowh + HID + cc) = lo4;
+        uint32_t h0, h1, l0, l1;
+        split_pair<P>(y[0], y[1], h0, l0);
+        split_pair<P>(y[2], y[3], h1, l1);
+        *reinterpret_cast<u32x2*>(rowh + cc) = u32x2{h0, h1};
+        if (SPLIT) *reinterpret_cast<u32x2*>(rowh + HID + cc) = u32x2{l0, l1};
       }
     };
     auto rows = [&](const float (&vin)[PY][4], auto SAc, auto SBc, auto SCc, auto LOc, auto HIc) {
@@ -630,17 +633,20 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
       const bool live = p <= z1 && !(a.dbg & 1);
       const bool ln = p - 2 >= z0 && p - 2 < z1 && !(a.dbg & 2);
       float vin[PY][4];
-      if (live) {
-        const float* q0 = planes + ((p - z0 + 1) & 1) * PLANE_F + 2 * cp * HID + c;
+      const float* q0 = planes + ((p - z0 + 1) & 1) * PLANE_F + 2 * cp * HID + c;
+      auto load_plane = [&]() {
 #pragma unroll
         for (int r = 0; r < PY; ++r)
 #pragma unroll
           for (int k = 0; k < 4; ++k) vin[r][k] = q0[(r * PX + k) * HID];
-      }
-      // ---- phase 1
+      };
+      // ---- phase 1.  The LN2 slots read their plane inputs after the LN2 (issued before the
+      // barrier, consumed after it), so the 24 input registers are not live beside LN2's
       if (kslot < 2) {
         if (ln) ln2_rows(h2b + ((p - 2 - z0) & 1) * H2F);
+        if (live) load_plane();
       } else if (live) {
+        load_plane();
         rows(vin, SA(), SB(), SC(), I0(), IS());
       }
       __syncthreads();  // 1 -> 2: LN2'd tile (p-2) visible to the fc
@@ -775,12 +781,11 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
       }
       acc = mma32<P>(fwh[ks], bh, acc);
     }
-    f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+    // fc + bias (+ norm2's bias, folded) and, with stats, norm2's normalised x * weight
+    f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcl + col);
     if (a.stats) {
       const f32x4 lw = *reinterpret_cast<const f32x4*>(n2w + col);
-      const f32x4 lb = *reinterpret_cast<const f32x4*>(n2b + col);
-      const f32x4 n2 = (xv - ev.x) * ev.y * lw + lb;
-      v = xv + (n2 + v) * bs;
+      v = xv + ((xv - ev.x) * ev.y * lw + v) * bs;
     } else {
       v = xv + v * bs;
     }
@@ -850,14 +855,12 @@ __global__ __launch_bounds__(1024, 1) void ffn_dwfc_tb4_kernel(DwFcArgs a) {
       }
       acc = mma32<P>(fwh[ks], bh, acc);
     }
-    f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcb + col);
+    f32x4 v = acc + *reinterpret_cast<const f32x4*>(fcl + col);
     const f32x4 xv = xr[rt];
     if (a.stats) {
       const f32x4 lw = *reinterpret_cast<const f32x4*>(n2w + col);
-      const f32x4 lb = *reinterpret_cast<const f32x4*>(n2b + col);
       const float em = es[rt].x, er = es[rt].y;
-      const f32x4 n2 = (xv - em) * er * lw + lb;
-      v = xv + (n2 + v) * bs;
+      v = xv + ((xv - em) * er * lw + v) * bs;
     } else {
       v = xv + v * bs;
     }

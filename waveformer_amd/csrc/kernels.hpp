@@ -43,6 +43,40 @@ __device__ __forceinline__ f32x4 mma16(bf16x4 a, bf16x4 b, f32x4 c) {  // 16x16x
                                                  __builtin_bit_cast(f16x4, b), c, 0, 0, 0);
   else return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
+// The operand words of a pair of values (first value in the low half): hi = op_cvt, lo = the
+// split's lo part (PREC_SPLIT) or 0.  For PREC_SPLIT, y - hi comes from v_dot2c_f32_bf16 of the
+// packed hi pair against (-1, 0) / (0, -1) accumulated onto y -- one VALU op per value instead
+// of unpacking hi back to fp32 and subtracting; y - hi is exact in fp32, so the words are
+// bitwise op_cvt / op_lo's.
+// The two constant pairs go through SGPRs the compiler cannot see into: hipcc encodes the
+// pair (-1, 0) as the inline constant -1.0, which gfx950 applies to BOTH bf16 halves
+// (tools/probe_dot2.hip: p0 - hi0 - hi1 instead of p0 - hi0).
+typedef __bf16 bf16v2 __attribute__((ext_vector_type(2)));
+template <int P>
+__device__ __forceinline__ void split_pair(float y0, float y1, uint32_t& hi, uint32_t& lo) {
+  if constexpr (P == PREC_SPLIT) {
+    uint32_t m0, m1;
+    asm("s_mov_b32 %0, 0xbf80" : "=s"(m0));      // (-1, 0)
+    asm("s_mov_b32 %0, 0xbf800000" : "=s"(m1));  // (0, -1)
+    const bf16v2 h = bf16v2{(__bf16)y0, (__bf16)y1};  // v_cvt_pk_bf16_f32 (RNE, as f2bf)
+    const float r0 = __builtin_amdgcn_fdot2_f32_bf16(h, __builtin_bit_cast(bf16v2, m0), y0, false);
+    const float r1 = __builtin_amdgcn_fdot2_f32_bf16(h, __builtin_bit_cast(bf16v2, m1), y1, false);
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = __builtin_bit_cast(uint32_t, bf16v2{(__bf16)r0, (__bf16)r1});
+  } else {
+    hi = (uint32_t)op_cvt<P>(y0) | ((uint32_t)op_cvt<P>(y1) << 16);
+    lo = 0;
+  }
+}
+// four values: the hi / lo operand quads (op_cvt / op_lo of each, bitwise)
+template <int P>
+__device__ __forceinline__ void split4(f32x4 v, bf16x4& h, bf16x4& l) {
+  uint32_t h0, h1, l0, l1;
+  split_pair<P>(v[0], v[1], h0, l0);
+  split_pair<P>(v[2], v[3], h1, l1);
+  h = __builtin_bit_cast(bf16x4, u32x2{h0, h1});
+  l = __builtin_bit_cast(bf16x4, u32x2{l0, l1});
+}
 // fp32 storage of the GEMM-to-GEMM intermediates (workspaces): every mode but PREC_BF16
 __host__ __device__ constexpr bool store32(int p) { return p != PREC_BF16; }
 inline bool valid_prec(int p) { return p == PREC_BF16 || p == PREC_SPLIT || p == PREC_FP16; }

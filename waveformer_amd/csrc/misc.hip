@@ -29,13 +29,14 @@ __global__ __launch_bounds__(256) void patch_embed_lane_kernel(
   __shared__ __attribute__((aligned(16))) float tile[4][64 * RS];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t p0 = (int64_t)blockIdx.x * 256 + wv * 64;     // first position of this wave
-  const int64_t p = min(p0 + lane, total - 1);                // (b, z, y, x) raster position
-  const int xo = (int)(p % W);
-  int64_t t = p / W;
-  const int yo = (int)(t % H);
-  t /= H;
-  const int zo = (int)(t % D);
-  const int64_t b = t / D;
+  // (b, z, y, x) raster position, decoded in 32 bits (the host keeps total below 2^31)
+  const uint32_t p = (uint32_t)min(p0 + lane, total - 1);
+  const int xo = (int)(p % (uint32_t)W);
+  uint32_t t = p / (uint32_t)W;
+  const int yo = (int)(t % (uint32_t)H);
+  t /= (uint32_t)H;
+  const int zo = (int)(t % (uint32_t)D);
+  const int64_t b = t / (uint32_t)D;
   const int W2 = 2 * W, H2 = 2 * H, D2 = 2 * D;
   float v[K];
 #pragma unroll
@@ -798,7 +799,8 @@ extern "C" int wf_patch_embed_fwd(const float* x, const float* w, const float* b
   WF_REQUIRE(row_lds <= 64 * 1024, "PatchEmbed row tile exceeds 64 KB of LDS");
   static const bool one_shot = getenv("WF_PE_ONESHOT") != nullptr;  // A/B: the kernel below
   static const bool rowstream = getenv("WF_PE_ROWSTREAM") != nullptr;  // A/B: the row stream
-  if (!one_shot && !rowstream && Cout == 48 && (Cin == 4 || Cin == 1)) {
+  if (!one_shot && !rowstream && Cout == 48 && (Cin == 4 || Cin == 1) &&
+      B * D * H * W < ((int64_t)1 << 31)) {
     const int64_t total = B * D * H * W;
     const unsigned blocks = (unsigned)cdiv(total, 256);
     if (Cin == 4)

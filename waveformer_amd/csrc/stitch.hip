@@ -48,35 +48,45 @@ __device__ __forceinline__ void cover(const int* st, int n, int r, int p, int& l
 // == rank, local patch row g / world), summed in window order; out is (B, C + 1, D, H, W):
 // channels [0, C) the weighted sums, channel C the summed weights -- no division (the ranks'
 // partials are all-reduced first, then wf_sliding_window_normalize divides)
+// Index arithmetic in 32 bits (the host checks every count fits): the round-5 kernel decoded
+// the voxel and mapped each window to its patch row with 64-bit divisions (a software routine
+// each), which set its time at 23 % of HBM.  World 1 (one rank) needs no row mapping at all.
 template <bool PARTIAL>
 __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
   // hipcc contracts a*b+c into an FMA by default (also across the inlined __fmul_rn /
   // __fadd_rn intrinsics); the reference rounds the product and the sum separately, so the
   // arithmetic below uses plain operators under contract(off)
 #pragma clang fp contract(off)
-  const int64_t total = (int64_t)a.B * a.D * a.H * a.W;
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t total = (uint32_t)a.B * a.D * a.H * a.W;
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
   if (idx >= total) return;
-  int64_t t = idx;
-  const int x = (int)(t % a.W);
-  t /= a.W;
-  const int y = (int)(t % a.H);
-  t /= a.H;
-  const int z = (int)(t % a.D);
-  const int b = (int)(t / a.D);
+  uint32_t t = idx;
+  const int x = (int)(t % (uint32_t)a.W);
+  t /= (uint32_t)a.W;
+  const int y = (int)(t % (uint32_t)a.H);
+  t /= (uint32_t)a.H;
+  const int z = (int)(t % (uint32_t)a.D);
+  const int b = (int)(t / (uint32_t)a.D);
   int z0, z1, y0, y1, x0, x1;
   cover(a.starts[0], a.n[0], a.rd, z, z0, z1);
   cover(a.starts[1], a.n[1], a.rh, y, y0, y1);
   cover(a.starts[2], a.n[2], a.rw, x, x0, x1);
-  const int64_t R3 = (int64_t)a.rd * a.rh * a.rw;
-  const int64_t nwin = (int64_t)a.n[0] * a.n[1] * a.n[2];
+  const int R3 = a.rd * a.rh * a.rw;
+  const int nwin = a.n[0] * a.n[1] * a.n[2];
   const int64_t S = (int64_t)a.D * a.H * a.W;
   const int CO = PARTIAL ? a.C + 1 : a.C;
   float* dst = a.out + (int64_t)b * CO * S + ((int64_t)z * a.H + y) * a.W + x;
-  auto mine = [&](int iz, int iy, int ix) {
-    if (!PARTIAL) return true;
-    const int64_t g = (int64_t)b * nwin + ((int64_t)iz * a.n[1] + iy) * a.n[2] + ix;
-    return g % a.world == a.rank;
+  const uint32_t world = (uint32_t)a.world;
+  const int gb = b * nwin;
+  auto mine = [&](int g) { return !PARTIAL || world == 1 || (uint32_t)g % world == (uint32_t)a.rank; };
+  // patch row of global window g (batch-major, then the 'ij' meshgrid order of
+  // dense_patch_slices): the gathered shards' order, or the local slot of a partial stitch
+  auto row_of = [&](int g) -> int {
+    if (world == 1) return g;
+    const uint32_t r = (uint32_t)g % world, j = (uint32_t)g / world;
+    if (PARTIAL) return (int)j;
+    const uint32_t sb = (uint32_t)a.sb;
+    return (int)(((j / sb) * world + r) * sb + (j % sb));
   };
 
   // count map: sum of the window weights in window order (monai/inferers/utils.py:262-269)
@@ -84,9 +94,9 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
   for (int iz = z0; iz <= z1; ++iz)
     for (int iy = y0; iy <= y1; ++iy)
       for (int ix = x0; ix <= x1; ++ix) {
-        if (!mine(iz, iy, ix)) continue;
-        const int64_t loc = ((int64_t)(z - a.starts[0][iz]) * a.rh + (y - a.starts[1][iy])) * a.rw +
-                            (x - a.starts[2][ix]);
+        if (!mine(gb + (iz * a.n[1] + iy) * a.n[2] + ix)) continue;
+        const int loc = ((z - a.starts[0][iz]) * a.rh + (y - a.starts[1][iy])) * a.rw +
+                        (x - a.starts[2][ix]);
         cnt = cnt + a.map[loc];
       }
   if (PARTIAL) dst[(int64_t)a.C * S] = cnt;
@@ -97,21 +107,16 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
     for (int iz = z0; iz <= z1; ++iz)
       for (int iy = y0; iy <= y1; ++iy)
         for (int ix = x0; ix <= x1; ++ix) {
-          if (!mine(iz, iy, ix)) continue;
-          const int64_t loc =
-              ((int64_t)(z - a.starts[0][iz]) * a.rh + (y - a.starts[1][iy])) * a.rw +
-              (x - a.starts[2][ix]);
+          const int g = gb + (iz * a.n[1] + iy) * a.n[2] + ix;
+          if (!mine(g)) continue;
+          const int loc = ((z - a.starts[0][iz]) * a.rh + (y - a.starts[1][iy])) * a.rw +
+                          (x - a.starts[2][ix]);
           const float w = a.map[loc];
-          // global window index (batch-major, then the 'ij' meshgrid order of
-          // dense_patch_slices) -> row of the gathered patch tensor (PARTIAL: the local slot)
-          const int64_t g = (int64_t)b * nwin + ((int64_t)iz * a.n[1] + iy) * a.n[2] + ix;
-          const int64_t r = g % a.world, j = g / a.world;
-          const int64_t row = PARTIAL ? j : ((j / a.sb) * a.world + r) * a.sb + (j % a.sb);
-          const float* p = a.patches + (row * a.C + c0) * R3 + loc;
+          const float* p = a.patches + ((int64_t)row_of(g) * a.C + c0) * R3 + loc;
 #pragma unroll
           for (int c = 0; c < 4; ++c)
             if (c < nc) {
-              const float prod = p[c * R3] * w;  // rounded on its own (no FMA)
+              const float prod = p[(int64_t)c * R3] * w;  // rounded on its own (no FMA)
               acc[c] = acc[c] + prod;
             }
         }
@@ -285,6 +290,10 @@ static int stitch_launch(const float* patches, int64_t world, int64_t slots_per_
     off += nwin[ax];
   }
   const int64_t total = B * D * H * W;
+  // the kernel's 32-bit index arithmetic
+  WF_REQUIRE(total < ((int64_t)1 << 31) && rd * rh * rw < ((int64_t)1 << 31) &&
+                 B * nwin[0] * nwin[1] * nwin[2] < ((int64_t)1 << 31),
+             "sliding-window stitch: more than 2^31 voxels or windows");
   if (partial)
     hipLaunchKernelGGL(stitch_kernel<true>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
                        (hipStream_t)stream, a);

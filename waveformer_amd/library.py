@@ -275,7 +275,8 @@ def window_attn_backward(gout: Tensor, x: Tensor, ln_w: Optional[Tensor],
                          scale: float) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor,
                                                 Tensor, Tensor]:
     """(dx, d ln_w, d ln_b, d wqkv, d bqkv, d table, d wproj, d bproj) of a train=True
-    window_attn: the proj / qkv GEMM gradients in fp32 on the platform BLAS, the core backward
+    window_attn: the proj / qkv data gradients on the streaming MFMA GEMM (bf16x3), the weight
+    gradients on wf_gemm_tn, the core backward
     with the softmax recomputed from the saved log-sum-exp (wf_window_attention_bwd_core),
     the bias-table scatter (wf_rel_pos_bias_bwd) and the norm1 backward.  Absent inputs get
     empty gradients."""
@@ -293,7 +294,7 @@ def window_attn_backward(gout: Tensor, x: Tensor, ln_w: Optional[Tensor],
     # proj: out = o Wp^T + bp (rows in window-major order == the Q1 raster order)
     dwproj = _wgrad(g, o)
     dbproj = colsum(g) if bproj is not None else E()
-    do = g.mm(wproj)
+    do = ops.mm_rows(g, wproj)
     dqkv = torch.empty((rows, 3 * C), dtype=torch.float32, device=x.device)
     dbias = torch.empty((heads, N, N), dtype=torch.float32, device=x.device)
     bws = torch.empty(_lib.query("wf_window_attention_bwd_workspace_bytes", B, C, D1, H1, W1, ws,
@@ -310,7 +311,7 @@ def window_attn_backward(gout: Tensor, x: Tensor, ln_w: Optional[Tensor],
     xin = ln_fwd(x2, ln_w, ln_b, eps, False) if ln_w is not None else x2
     dwqkv = _wgrad(dqkv, xin)
     dbqkv = colsum(dqkv) if bqkv is not None else E()
-    dxin = dqkv.mm(wqkv)
+    dxin = ops.mm_rows(dqkv, wqkv)
     dlnw, dlnb = E(), E()
     if ln_w is not None:
         dx, dlnw, dlnb = ln_bwd(x2, ln_w, ln_b, eps, False, dxin)
@@ -475,8 +476,9 @@ def ccf_ffn_backward(gout: Tensor, xh: Tensor, n2w: Optional[Tensor], n2b: Optio
                                                         Tensor, Tensor, Tensor]:
     """(dx, d n2w, d n2b, d pww, d pwb, d l1w, d l1b, d dww, d dwb, d l2w, d l2b, d fcw, d fcb)
     of a train=True ccf_ffn from the kept h1 / h2: LN / GELU backward (wf_ln_act_bwd), the
-    depthwise data / weight gradients (wf_dwconv3d_cl flipped, wf_dwconv3d_wgrad), fp32 GEMM
-    gradients on the platform BLAS; absent inputs get empty gradients."""
+    depthwise data / weight gradients (wf_dwconv3d_cl flipped, wf_dwconv3d_wgrad), the GEMM
+    gradients on the library's MFMA GEMMs (data: streaming GEMM, weights: wf_gemm_tn; bf16x3);
+    absent inputs get empty gradients."""
     if work.numel() == 0:
         raise RuntimeError("waveformer::ccf_ffn: backward of a train=False call")
     B, D, H, W, C = xh.shape
@@ -493,7 +495,7 @@ def ccf_ffn_backward(gout: Tensor, xh: Tensor, n2w: Optional[Tensor], n2b: Optio
     u2 = ln_fwd(h2, l2w, l2b, eps2, True)
     dfcw = _wgrad(df, u2)
     dfcb = colsum(df) if fcb is not None else E()
-    du2 = df.mm(fcw)
+    du2 = ops.mm_rows(df, fcw)
     del u2
     dh2, dl2w, dl2b = ln_bwd(h2, l2w, l2b, eps2, True, du2)
     del du2
@@ -513,12 +515,12 @@ def ccf_ffn_backward(gout: Tensor, xh: Tensor, n2w: Optional[Tensor], n2b: Optio
     # pw: h1 = n2 Wpw^T + bpw, u1 = GELU(LN1(h1))
     n2 = ln_fwd(x2, n2w, n2b, n2eps, False) if block else x2
     wpw = pww.view(hid, C)
-    h1 = torch.addmm(pwb, n2, wpw.t()) if pwb is not None else n2.mm(wpw.t())
+    h1 = ops.linear_rows_any(n2, wpw, pwb)
     dh1, dl1w, dl1b = ln_bwd(h1, l1w, l1b, eps1, True, du1)
     del h1, du1
     dpww = _wgrad(dh1, n2).view_as(pww)
     dpwb = colsum(dh1) if pwb is not None else E()
-    dn2 = dh1.mm(wpw)
+    dn2 = ops.mm_rows(dh1, wpw)
     dn2w, dn2b = E(), E()
     if block:
         dn2 += df
@@ -585,8 +587,9 @@ def _merge_setup(ctx, inputs, output):
 def patch_merging_backward(gout: Tensor, x: Tensor, nw: Tensor, nb: Tensor, red: Tensor,
                            eps: float, v2: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """(dx, d norm.weight, d norm.bias, d reduction.weight) of patch_merging: gather of the 8
-    sub-lattices (wf_patch_merging_gather), LayerNorm backward, fp32 GEMM gradients, scatter
-    back (wf_patch_merging_scatter, the duplicated Q3 lattices accumulate)."""
+    sub-lattices (wf_patch_merging_gather), LayerNorm backward, GEMM gradients, scatter
+    back (wf_patch_merging_scatter, the duplicated Q3 lattices accumulate); the GEMMs on
+    the library's MFMA kernels (bf16x3)."""
     B, D, H, W, C = x.shape
     M = B * (D // 2) * (H // 2) * (W // 2)
     merged = torch.empty((M, 8 * C), dtype=torch.float32, device=x.device)
@@ -596,7 +599,7 @@ def patch_merging_backward(gout: Tensor, x: Tensor, nw: Tensor, nb: Tensor, red:
     g = _f32(gout).view(M, 2 * C)
     dred = _wgrad(g, z)
     del z
-    dz = g.mm(red)
+    dz = ops.mm_rows(g, red)
     dm, dnw, dnb = ln_bwd(merged, nw, nb, eps, False, dz)
     dx = torch.empty_like(x)
     _lib.call("wf_patch_merging_scatter", dm.data_ptr(), int(v2), dx.data_ptr(), B, C, D, H, W,

@@ -12,6 +12,7 @@ import ctypes
 import math
 import os
 import threading
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -197,6 +198,13 @@ class WeightArena:
         self.done.record(cur)
         self.done_stream = cur.cuda_stream
 
+    def retire(self) -> None:
+        """Dropped from its module: wait for the last forward that read the planes (it may
+        have run on a stream other than the buffer's allocation stream, whose cache the
+        memory returns to)."""
+        if self.done is not None:
+            self.done.synchronize()
+
 
 class _Scope:
     def __init__(self, arena: Optional[WeightArena]):
@@ -206,6 +214,15 @@ class _Scope:
 
 _tls = threading.local()  # the open weight_scope of THIS thread (two threads: two scopes)
 _arena_lock = threading.Lock()
+# module -> {thread: {f16: WeightArena}}; outside the module, so copies / pickles of a model
+# carry no arenas, and a dropped model drops its arenas
+_ARENAS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def arena_count(module: torch.nn.Module) -> int:
+    """The weight arenas `module` holds (one per live thread and operand format)."""
+    with _arena_lock:
+        return sum(len(per) for per in _ARENAS.get(module, {}).values())
 
 
 def _cur_scope() -> Optional[_Scope]:
@@ -248,19 +265,27 @@ class weight_scope:
             # forward, else bf16 hi / lo (training always runs fp32-faithful bf16x3)
             train = torch.is_grad_enabled() and any(p.requires_grad for p in params)
             f16 = get_precision() == "fp16" and not train
-            # one arena per (operand format, thread): two threads running forwards of one
+            # one arena per (thread, operand format): two threads running forwards of one
             # model on their own streams never share planes or the done / done_stream pair
-            # (ADVICE r3 #3); the dict itself is guarded by a lock
+            # (ADVICE r3 #3); the dict itself is guarded by a lock.  Keyed by the Thread
+            # object (an ident is reused by later threads); the arenas of threads that have
+            # ended, and an arena whose parameters moved, are retired at the next scope entry
+            # (one weight copy per thread identity, never freed)
             with _arena_lock:
-                arenas = getattr(self.module, "_wf_arenas", None)
+                arenas = _ARENAS.get(self.module)
                 if arenas is None:
                     arenas = {}
-                    object.__setattr__(self.module, "_wf_arenas", arenas)
-                akey = (f16, threading.get_ident())
-                arena = arenas.get(akey)
+                    _ARENAS[self.module] = arenas
+                for th in [t for t in arenas if not t.is_alive()]:
+                    for old in arenas.pop(th).values():
+                        old.retire()
+                per = arenas.setdefault(threading.current_thread(), {})
+                arena = per.get(f16)
                 if arena is None or arena.key != tuple((p.data_ptr(), p.numel()) for p in params):
+                    if arena is not None:
+                        arena.retire()
                     arena = WeightArena(params, f16)
-                    arenas[akey] = arena
+                    per[f16] = arena
             arena.refresh()
         _tls.scope = _Scope(arena)
         self.owner = True
@@ -350,12 +375,14 @@ def patch_embed_ll(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.T
                    ) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
     """patch_embed fused with the first Block's norm1 + Haar LL (wf_patch_embed_ll_fwd):
     (out, LL of LayerNorm(out)), or None when the shape is not the kernel's (Cin 1 / 4, Cout 48,
-    even output sizes, output W <= 64)."""
+    even output sizes, output W <= 64, fewer than 2^31 output elements) -- the caller then runs
+    patch_embed + the LL-only DWT."""
     B, Cin, D2, H2, W2 = x.shape
     Cout = weight.shape[0]
     D, H, W = D2 // 2, H2 // 2, W2 // 2
     if (Cout != 48 or Cin not in (1, 4) or tuple(weight.shape) != (Cout, Cin, 2, 2, 2)
-            or D2 % 2 or H2 % 2 or W2 % 2 or D % 2 or H % 2 or W % 2 or W > 64):
+            or D2 % 2 or H2 % 2 or W2 % 2 or D % 2 or H % 2 or W % 2 or W > 64
+            or B * D * H * W * Cout >= 1 << 31):  # the kernel's 32-bit element indexing
         return None
     _check(x, "x")
     _check(weight, "weight")
@@ -1059,14 +1086,28 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
     b = b if b.stride(1) == 1 and b.dtype == torch.float32 else b.float().contiguous()
     M, N = a.shape
     K = b.shape[1]
+    # rows must not overlap (an expanded stride-0 or short-stride view is copied, not clamped)
+    if a.stride(0) < N:
+        a = a.contiguous()
+    if b.stride(0) < K:
+        b = b.contiguous()
+    _check(a, "a", contiguous=False)
+    _check(b, "b", contiguous=False)
+    if b.device != a.device:
+        raise ValueError("gemm_tn: a and b must be on the same device")
     if out is None:
         out = torch.empty((N, K), dtype=torch.float32, device=a.device)
         accumulate = False
-    if tuple(out.shape) != (N, K) or out.stride(1) != 1:
+    # the kernel writes fp32 through out's pointer: a bf16 / fp16 or other-device `out` would be
+    # overrun or misread
+    if out.dtype != torch.float32 or out.device != a.device:
+        raise ValueError(f"gemm_tn: out must be float32 on {a.device}, got {out.dtype} on "
+                         f"{out.device}")
+    if tuple(out.shape) != (N, K) or out.stride(1) != 1 or out.stride(0) < K:
         raise ValueError("gemm_tn: out must be an (N, K) row matrix")
     ws = torch.empty(max(1, _lib.query("wf_gemm_tn_workspace_bytes", M, N, K)),
                      dtype=torch.uint8, device=a.device)
-    _lib.call("wf_gemm_tn", a.data_ptr(), max(a.stride(0), N), b.data_ptr(), max(b.stride(0), K),
+    _lib.call("wf_gemm_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
               out.data_ptr(), out.stride(0), int(accumulate), ws.data_ptr(), M, N, K, _stream())
     return out
 
@@ -1099,6 +1140,37 @@ def linear_rows(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Te
     _lib.call("wf_linear_fwd", x2d.data_ptr(), wb.data_ptr(), _ptr(bias), out.data_ptr(), M, K, N,
               int(bool(gelu_in)), pr, _stream())
     return out
+
+
+def mfma_gemm_ok(a: torch.Tensor, K: int, N: int) -> bool:
+    """True when a (M, K) row matrix times a (K, N) operand can run on the streaming MFMA GEMM
+    (wf_linear_fwd: K % 8 == 0, N % 4 == 0, a contiguous fp32 on the GPU)."""
+    return (a.is_cuda and a.dtype == torch.float32 and a.dim() == 2 and a.is_contiguous()
+            and K % 8 == 0 and K >= 8 and N % 4 == 0 and N >= 4)
+
+
+def mm_rows(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a (M, K) @ b (K, N) -- the data-gradient GEMMs of training (dX = dY W) -- on the
+    streaming MFMA GEMM at bf16x3 (fp32-faithful operands, fp32 accumulation; b^T is split
+    per call), instead of the platform BLAS (hipBLASLt).  Shapes the kernel does not take
+    (K % 8 or N % 4 nonzero) fall back to torch.mm."""
+    K, N = b.shape
+    if not mfma_gemm_ok(a, K, N):
+        return a.mm(b)
+    return linear_rows(a, b.detach().t().contiguous(), None, cache=False,
+                       prec=PRECISIONS["bf16x3"])
+
+
+def linear_rows_any(x2d: torch.Tensor, weight: torch.Tensor,
+                    bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bias + x2d @ weight^T (weight (N, K)) at bf16x3 on the streaming MFMA GEMM, or torch's
+    fp32 addmm for shapes it does not take."""
+    N, K = weight.shape[0], x2d.shape[1]
+    w2 = weight.reshape(N, K)
+    if not mfma_gemm_ok(x2d, K, N):
+        return torch.addmm(bias, x2d, w2.t()) if bias is not None else x2d.mm(w2.t())
+    return linear_rows(x2d, w2.detach().contiguous(), None if bias is None else bias.detach(),
+                       cache=False, prec=PRECISIONS["bf16x3"])
 
 
 def instnorm_stats(x: torch.Tensor, eps: float) -> torch.Tensor:
