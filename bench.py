@@ -139,6 +139,21 @@ def _attn_flops(a, kw, out):
     return 2 * T * C * 3 * C + 4 * T * N * C + 2 * T * C * C
 
 
+def _dwt_grid(a, kw, out):
+    """Work-items of the Haar forward's launch on x = a[0] (dwt_haar_fwd in csrc/dwt.hip): one
+    row group of G lanes per output position, at most 8192 workgroups of 256 (grid-stride)."""
+    B, D, H, W, C = a[0].shape
+    c4 = C // 4
+    if C == 48:
+        G = 16
+    elif c4 % 3 == 0 and c4 // 3 in (1, 2, 4, 8, 16, 32, 64):
+        G = c4 // 3
+    else:
+        G = min(64, 1 << max(0, (c4 - 1).bit_length()))
+    total = B * D * H * W // 8
+    return min(-(-total // (256 // G)), 8192) * 256
+
+
 def _live_rows(a):
     """sliding_window_stitch(patches, map, starts, image_size, batch, ...): the number of real
     windows (the padded slots of the gathered buffer are never read)."""
@@ -181,6 +196,9 @@ class OpTimer:
                                                      + out.numel()) * 4,
     }
 
+    # launch size (work-items) of the timed launch, for the per-shape PMC lookup
+    GRID = {"dwt3d_haar": _dwt_grid, "dwt3d_haar_ll": _dwt_grid}
+
     def __init__(self, name):
         from waveformer_amd import ops
         self.ops, self.name = ops, name
@@ -203,7 +221,8 @@ class OpTimer:
             for _ in range(self.REPS):
                 self.orig(*a, **kw)
             e.record()
-            self.rec.append((self.WORK[name](a, kw, out), s, e, issue))
+            grid = self.GRID[name](a, kw, out) if name in self.GRID else None
+            self.rec.append((self.WORK[name](a, kw, out), s, e, issue, grid))
             return out
 
         setattr(ops, name, wrapped)
@@ -215,10 +234,11 @@ class OpTimer:
         if not self.rec:
             return None
         big = max(r[0] for r in self.rec)
-        sel = [(b, s.elapsed_time(e) / self.REPS, i) for b, s, e, i in self.rec if b == big]
-        avg_ms = sum(t for _, t, _ in sel) / len(sel)
+        sel = [(b, s.elapsed_time(e) / self.REPS, i, gr) for b, s, e, i, gr in self.rec if b == big]
+        avg_ms = sum(t for _, t, _, _ in sel) / len(sel)
         return {"work_per_launch": big, "avg_ms": avg_ms, "launches": len(sel),
-                "rate": big / (avg_ms * 1e-3), "issue": max(i for _, _, i in sel)}
+                "rate": big / (avg_ms * 1e-3), "issue": max(i for _, _, i, _ in sel),
+                "grid": sel[0][3]}
 
 
 def pmc_traffic(kernel_re, batch, grid=None):
@@ -308,11 +328,11 @@ def idwt_roofline(batch, dev, layout="cl"):
     ach = alg / (us * 1e-6) / 1e9
     del bands, ll, det, out, skip
     # the plain and the fused-concat launches are separate instantiations (<false> / <true>),
-    # so the counter summary tells them apart; the cl4 grid is one thread per finest
-    # 4-channel group
+    # so the counter summary tells them apart
     kname = {"cl": "idwt3d_haar_cl4_kernel<false>", "cat": "idwt3d_haar_cl4_kernel<true>",
              "ncdhw": "idwt3d_haar_nc4"}[layout]
-    grid = (-(-batch * 128 ** 3 * 12 // 256)) * 256 if layout != "ncdhw" else None
+    # one thread per finest 2x2x2 cube (64^3 of them per volume) x 4-channel group
+    grid = (-(-batch * 64 ** 3 * 12 // 256)) * 256 if layout != "ncdhw" else None
     return {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(kname, batch, grid), "algorithmic_bytes_per_launch": alg,
@@ -759,7 +779,7 @@ def main():
             ach = r["rate"] / 1e9
             d = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1),
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                 "traffic": pmc_traffic(PMC_KERNEL.get(name, name), args.batch),
+                 "traffic": pmc_traffic(PMC_KERNEL.get(name, name), args.batch, r.get("grid")),
                  "algorithmic_bytes_per_launch": r["work_per_launch"],
                  "avg_launch_us": round(r["avg_ms"] * 1e3, 2), "launches_timed": r["launches"]}
             if name == "ccf_ffn_dwconv":

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 17
+#define WF_ABI_VERSION 18
 
 enum { WF_PREC_BF16 = 0, WF_PREC_BF16X3 = 1, WF_PREC_FP16 = 2 };
 
@@ -332,6 +332,13 @@ int wf_upsample_dwconv3d_stats_cl(const float* in, const float* w, const float* 
  * into the NCDHW out (B, N, P).  K % 4 == 0, K <= 120, N <= 16; fp32 FMAs.                  */
 int wf_conv1x1_head_cl(const float* x, int64_t ldx, const float* weight, const float* bias,
                        float* out, int64_t B, int64_t K, int64_t N, int64_t P, void* stream);
+/* y (M, N) = x (M, K) . w (N, K)^T + bias for K in [1, 7] (ABI 18): the shapes the MFMA GEMM
+ * (wf_linear_fwd, K % 8 == 0) does not take -- in training, UnetResBlock's 1x1 residual conv of
+ * the 4-channel input (dynunet_block.py:77-80) and the input gradient of the 4-class
+ * UnetOutBlock (:188-210).  Row strides ldx / ldy floats; N % 4 == 0, y 16-B aligned; exact
+ * fp32 FMAs (bias first, then k in order).                                                   */
+int wf_linear_smallk_fwd(const float* x, int64_t ldx, const float* w, const float* bias,
+                         float* y, int64_t ldy, int64_t M, int64_t K, int64_t N, void* stream);
 /* Depthwise Conv3d(C, C, 3, padding 1, groups C) + bias of a dense channel-last fp32 tensor
  * (ProjectionUpsample.conv1, wave_helper.py:43-46) with the per-(sample, channel) fp64 {sum, sum
  * of squares} of its output accumulated in the epilogue into stats_acc (B, C, 2) (zeroed here)

@@ -231,11 +231,12 @@ def test_gemm_tn_vs_fp64(M, N, K, pad):
 
 
 @pytest.mark.parametrize("cin,cout,S,bias", [(96, 48, (6, 5, 7), True), (48, 4, (8, 8, 8), True),
-                                             (384, 192, (4, 4, 4), False)])
+                                             (384, 192, (4, 4, 4), False), (4, 48, (5, 6, 7), True)])
 def test_conv1x1_and_convtranspose2_autograd(cin, cout, S, bias):
     """The decoder's 1x1 convs (wfa.Conv1x1Fn) and 2^3 transposed convs (wfa.ConvT2Fn) in
-    training: forward and input gradient on the streaming MFMA GEMM (bf16x3 operands; the
-    48 -> 4 head's input gradient has K = 4 and stays on torch.mm), weight gradient on
+    training: forward and input gradient on the streaming MFMA GEMM (bf16x3 operands; K < 8 --
+    the 48 -> 4 head's input gradient, the 4 -> 48 stem conv's forward -- on the small-K fp32
+    kernel wf_linear_smallk_fwd), weight gradient on
     wf_gemm_tn, bias by column sums -- against fp64 CPU autograd: rel-L2 <= 1e-5 for the bf16x3
     products (operands carried to 16 mantissa bits, fp32 accumulation; round 5 held the fp32
     GEMMs to 2e-6), 2e-6 for the bias column sums."""

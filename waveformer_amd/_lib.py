@@ -51,6 +51,7 @@ SIGNATURES = {
     "wf_norm_act_h_cl": (_I, [_P, _I64, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "wf_upsample_trilinear_add_cl": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I, _P]),
     "wf_conv1x1_head_cl": (_I, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
+    "wf_linear_smallk_fwd": (_I, [_P, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "wf_dwconv3d_stats_cl": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _P]),
     "wf_norm_act_lin_cl": (_I, [_P, _I64, _P, _P, _I64, _I64, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "wf_dwt3d_fwd": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _I, _P]),
@@ -134,7 +135,7 @@ SIGNATURES = {
     "wf_transpose_cs": (_I, [_P, _P, _I64, _I64, _I64, _P]),
 }
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 _lock = threading.Lock()
 _lib = None
 _err = None

@@ -358,6 +358,42 @@ class Conv1x1Fn(torch.autograd.Function):
         return dx, dw, db
 
 
+class LinearFn(torch.autograd.Function):
+    """nn.Linear over (M, K) rows (ChannelCalibration's squeeze-excitation fc1 / fc2,
+    network_backbone.py:66-128): y = x W^T + b and dx = dy W on the streaming MFMA GEMM
+    (bf16x3), dW = dy^T x on wf_gemm_tn, db = column sums -- the step's last platform-BLAS
+    GEMMs (M = batch)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.contiguous()
+        ctx.save_for_backward(x2, w)
+        ctx.has_bias = b is not None
+        return ops.linear_rows_any(x2, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, w = ctx.saved_tensors
+        g = _f32(g).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.mm_rows(g, w)
+        if ctx.needs_input_grad[1]:
+            dw = ops.gemm_tn(g, x2)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = colsum(g)
+        return dx, dw, db
+
+
+def linear(lin: torch.nn.Linear, x: torch.Tensor) -> torch.Tensor:
+    """lin(x) for 2-D fp32 GPU rows on the library's GEMMs (autograd-aware); else the module."""
+    if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and type(lin) is torch.nn.Linear:
+        if needs_grad(x, lin.weight, lin.bias):
+            return LinearFn.apply(x, lin.weight, lin.bias)
+        return ops.linear_rows_any(x.contiguous(), lin.weight, lin.bias)
+    return lin(x)
+
+
 class ConvT2Fn(torch.autograd.Function):
     """ConvTranspose3d(k=2, s=2) (unetr_block.py:73-80) as one GEMM into the 8 sub-voxels:
     y[2z+dz, 2y+dy, 2x+dx] = x W[:, :, dz, dy, dx] + b -- the MFMA GEMM whose epilogue stores

@@ -261,12 +261,11 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
         if (g.a_gelu) {
           gelu_erf8(v[rt]);
         }
+        {
+          float xs[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = kv ? v[rt][j] : 0.f;
-          const uint16_t h = op_cvt<P>(x);
-          ah[rt][j] = (short)h;
-          al[rt][j] = op_lo<P>(x, h);
+          for (int j = 0; j < 8; ++j) xs[j] = kv ? v[rt][j] : 0.f;
+          split8<P>(xs, ah[rt], al[rt]);
         }
       }
     }

@@ -212,12 +212,11 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
         gelu_erf8(v);
       }
       bf16x8 ah, al;
+      {
+        float xs[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = kv ? v[j] : 0.f;
-        const uint16_t h = op_cvt<P>(x);
-        ah[j] = (short)h;
-        al[j] = op_lo<P>(x, h);
+        for (int j = 0; j < 8; ++j) xs[j] = kv ? v[j] : 0.f;
+        split8<P>(xs, ah, al);
       }
       // transposed product C^T = Wt . A^T: the weight fragment is the A operand (rows =
       // output channels), the activation fragment the B operand (columns = positions), so

@@ -77,6 +77,15 @@ __device__ __forceinline__ void split4(f32x4 v, bf16x4& h, bf16x4& l) {
   h = __builtin_bit_cast(bf16x4, u32x2{h0, h1});
   l = __builtin_bit_cast(bf16x4, u32x2{l0, l1});
 }
+// eight values (an MFMA K-octet): the hi / lo operand octets
+template <int P>
+__device__ __forceinline__ void split8(const float (&x)[8], bf16x8& h, bf16x8& l) {
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) split_pair<P>(x[2 * j], x[2 * j + 1], hw[j], lw[j]);
+  h = __builtin_bit_cast(bf16x8, u32x4{hw[0], hw[1], hw[2], hw[3]});
+  l = __builtin_bit_cast(bf16x8, u32x4{lw[0], lw[1], lw[2], lw[3]});
+}
 // fp32 storage of the GEMM-to-GEMM intermediates (workspaces): every mode but PREC_BF16
 __host__ __device__ constexpr bool store32(int p) { return p != PREC_BF16; }
 inline bool valid_prec(int p) { return p == PREC_BF16 || p == PREC_SPLIT || p == PREC_FP16; }

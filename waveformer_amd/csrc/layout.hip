@@ -133,6 +133,39 @@ static unsigned grid_for(int64_t total) {
   return (unsigned)(blocks < 1 ? 1 : blocks);
 }
 
+// y (M, N) = x (M, K) . w (N, K)^T + bias for K < 8 -- the shapes the MFMA GEMM's K-octet loader
+// does not take: the 4-channel stem / head convolutions of the full model in training (UnetResBlock
+// conv3 4 -> 48 forward, UnetOutBlock 48 -> 4 input gradient).  One thread per (row, 4 outputs),
+// exact fp32 FMAs in k order from the bias; the N / 4 threads of a row write its y row as one
+// contiguous run, the x row (<= 32 B) is shared through the cache.
+template <int K>
+__global__ __launch_bounds__(256) void linear_smallk_kernel(
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
+    const float* __restrict__ bias, float* __restrict__ y, int64_t ldy, uint32_t M, int N) {
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // [N][K], then bias [N]
+  for (int i = threadIdx.x; i < N * K; i += 256) wl[i] = w[i];
+  for (int i = threadIdx.x; i < N; i += 256) wl[N * K + i] = bias ? bias[i] : 0.f;
+  __syncthreads();
+  const uint32_t N4 = (uint32_t)N >> 2;
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t row = idx / N4, j = idx - row * N4;
+  if (row >= M) return;
+  const float* xr = x + (int64_t)row * ldx;
+  float xv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) xv[k] = xr[k];
+  float acc[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const float* wr = wl + (4 * j + n) * K;
+    float a = wl[N * K + 4 * j + n];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a = fmaf(xv[k], wr[k], a);
+    acc[n] = a;
+  }
+  *reinterpret_cast<f32x4*>(y + (int64_t)row * ldy + 4 * j) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+}
+
 }  // namespace wf
 
 using namespace wf;
@@ -172,6 +205,29 @@ extern "C" int wf_subvoxel_scatter_cl(const float* g, const float* bias, float* 
                      FastDiv((uint32_t)w), FastDiv((uint32_t)h), FastDiv((uint32_t)d),
                      (uint32_t)total);
   return check_launch("wf_subvoxel_scatter_cl");
+}
+
+extern "C" int wf_linear_smallk_fwd(const float* x, int64_t ldx, const float* w,
+                                    const float* bias, float* y, int64_t ldy, int64_t M,
+                                    int64_t K, int64_t N, void* stream) {
+  WF_REQUIRE(M >= 0 && K >= 1 && K <= 7 && N >= 4 && N % 4 == 0 && N <= 4096,
+             "small-K linear: K in [1, 7], N a multiple of 4 up to 4096");
+  WF_REQUIRE(ldx >= K && ldy >= N && ldy % 4 == 0, "ldx >= K, ldy >= N a multiple of 4");
+  WF_REQUIRE(M * (N / 4) < ((int64_t)1 << 31), "small-K linear: too many outputs");
+  WF_REQUIRE_PTR(x);
+  WF_REQUIRE_PTR(w);
+  WF_REQUIRE_PTR(y);
+  WF_REQUIRE(aligned16(y), "y must be 16-byte aligned");
+  if (M == 0) return WF_OK;
+  const size_t lds = (size_t)N * (K + 1) * sizeof(float);
+  const dim3 grid((unsigned)cdiv(M * (N / 4), 256));
+  hipStream_t s = (hipStream_t)stream;
+  switch (K) {
+#define WF_SK(k) case k: hipLaunchKernelGGL(linear_smallk_kernel<k>, grid, dim3(256), lds, s, x, ldx, w, bias, y, ldy, (uint32_t)M, (int)N); break;
+    WF_SK(1) WF_SK(2) WF_SK(3) WF_SK(4) WF_SK(5) WF_SK(6) WF_SK(7)
+#undef WF_SK
+  }
+  return check_launch("wf_linear_smallk_fwd");
 }
 
 extern "C" int wf_conv1x1_head_cl(const float* x, int64_t ldx, const float* weight,

@@ -131,15 +131,17 @@ __global__ __launch_bounds__(64 * MR_WAVES, 1) void merge_res_kernel(GemmArgs g)
       const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
       bf16x8 ah, al;
+      {
+        float xs[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float xv = (a[ks][j] - mean) * rstd * wv[j] + bv[j];
-        // fp16: the fp32 value first (gemm_kc's double rounding), not a v_fma_mix straight to
-        // fp16, so the two paths stay bit-identical
-        if (!SPLIT) asm volatile("" : "+v"(xv));
-        const uint16_t h = op_cvt<P>(xv);
-        ah[j] = (short)h;
-        al[j] = op_lo<P>(xv, h);
+        for (int j = 0; j < 8; ++j) {
+          float xv = (a[ks][j] - mean) * rstd * wv[j] + bv[j];
+          // fp16: the fp32 value first (gemm_kc's double rounding), not a v_fma_mix straight
+          // to fp16, so the two paths stay bit-identical
+          if (!SPLIT) asm volatile("" : "+v"(xv));
+          xs[j] = xv;
+        }
+        split8<P>(xs, ah, al);
       }
 #pragma unroll
       for (int t = 0; t < MR_NT; ++t) {

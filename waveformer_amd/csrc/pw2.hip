@@ -109,12 +109,17 @@ __global__ __launch_bounds__(64 * NW, 1) void pw2_res_kernel(GemmArgs g) {
           const f32x4 lb = *reinterpret_cast<const f32x4*>(ab + k + 4 * hq);
           v = (v - mu) * rs * lw + lb;
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint16_t hb = op_cvt<P>(v[e]);
-          ah[ks][4 * hq + e] = (short)hb;
-          al[ks][4 * hq + e] = op_lo<P>(v[e], hb);
-        }
+        uint32_t h0, h1, l0, l1;
+        split_pair<P>(v[0], v[1], h0, l0);
+        split_pair<P>(v[2], v[3], h1, l1);
+        ah[ks][4 * hq] = (short)(h0 & 0xFFFF);
+        ah[ks][4 * hq + 1] = (short)(h0 >> 16);
+        ah[ks][4 * hq + 2] = (short)(h1 & 0xFFFF);
+        ah[ks][4 * hq + 3] = (short)(h1 >> 16);
+        al[ks][4 * hq] = (short)(l0 & 0xFFFF);
+        al[ks][4 * hq + 1] = (short)(l0 >> 16);
+        al[ks][4 * hq + 2] = (short)(l1 & 0xFFFF);
+        al[ks][4 * hq + 3] = (short)(l1 >> 16);
       }
     }
     // the next tile's rows, in flight across this tile's MFMAs and epilogue

@@ -89,6 +89,59 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
     return (int)(((j / sb) * world + r) * sb + (j % sb));
   };
 
+  // overlap <= 0.5 (the inferer's default): at most 2 windows per axis cover a voxel.  Their
+  // patch rows, map offsets and weights are gathered first, so all of a voxel's loads are in
+  // flight at once (the window loops below issue them one window at a time, a memory latency
+  // each); the sums are formed in the same window order either way.
+  if (!PARTIAL && z1 - z0 <= 1 && y1 - y0 <= 1 && x1 - x0 <= 1) {
+    constexpr int MW = 8;
+    int nw = 0;
+    int locs[MW];
+    int64_t base[MW];
+#pragma unroll
+    for (int u = 0; u < MW; ++u) {
+      const int iz = z0 + (u >> 2), iy = y0 + ((u >> 1) & 1), ix = x0 + (u & 1);
+      const bool ok = iz <= z1 && iy <= y1 && ix <= x1;
+      const int izc = ok ? iz : z0, iyc = ok ? iy : y0, ixc = ok ? ix : x0;
+      const int g = gb + (izc * a.n[1] + iyc) * a.n[2] + ixc;
+      locs[u] = ((z - a.starts[0][izc]) * a.rh + (y - a.starts[1][iyc])) * a.rw +
+                (x - a.starts[2][ixc]);
+      base[u] = ok ? (int64_t)row_of(g) * a.C * R3 + locs[u] : -1;
+      nw += ok;
+    }
+    float wv[MW];
+#pragma unroll
+    for (int u = 0; u < MW; ++u) wv[u] = base[u] >= 0 ? a.map[locs[u]] : 0.f;
+    float cnt = 0.f;
+#pragma unroll
+    for (int u = 0; u < MW; ++u)
+      if (base[u] >= 0) cnt = cnt + wv[u];
+    for (int c0 = 0; c0 < a.C; c0 += 4) {
+      const int nc = min(4, a.C - c0);
+      float pv[MW][4];
+#pragma unroll
+      for (int u = 0; u < MW; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          pv[u][c] = (base[u] >= 0 && c < nc) ? a.patches[base[u] + (int64_t)(c0 + c) * R3] : 0.f;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < MW; ++u)
+        if (base[u] >= 0) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float prod = pv[u][c] * wv[u];  // rounded on its own (no FMA)
+            acc[c] = acc[c] + prod;
+          }
+        }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < nc) dst[(int64_t)(c0 + c) * S] = __fdiv_rn(acc[c], cnt);
+    }
+    (void)nw;
+    return;
+  }
+
   // count map: sum of the window weights in window order (monai/inferers/utils.py:262-269)
   float cnt = 0.f;
   for (int iz = z0; iz <= z1; ++iz)

@@ -79,7 +79,9 @@ class ChannelCalibration(nn.Module):
         x = self.relu(self.norm_conv(cv(self.conv, x)))
         x = self.norm_expand(cv(self.expand, x))
         b, c = x.shape[:2]
-        se = self.sigmoid(self.fc2(F.relu(self.fc1(self.global_pool(x).view(b, c)))))
+        # fc1 / fc2 (M = batch rows) on the library's GEMMs too: no platform-BLAS call remains
+        se = self.sigmoid(wfa.linear(self.fc2, F.relu(wfa.linear(self.fc1,
+                                                                 self.global_pool(x).view(b, c)))))
         return self.relu(x * se.view(b, c, 1, 1, 1) + identity)
 
 

@@ -1142,19 +1142,57 @@ def linear_rows(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Te
     return out
 
 
+_GEMM_FALLBACK_TRACE = os.environ.get("WF_GEMM_FALLBACK_TRACE") == "1"  # diagnostics
+
+
 def mfma_gemm_ok(a: torch.Tensor, K: int, N: int) -> bool:
     """True when a (M, K) row matrix times a (K, N) operand can run on the streaming MFMA GEMM
     (wf_linear_fwd: K % 8 == 0, N % 4 == 0, a contiguous fp32 on the GPU)."""
-    return (a.is_cuda and a.dtype == torch.float32 and a.dim() == 2 and a.is_contiguous()
-            and K % 8 == 0 and K >= 8 and N % 4 == 0 and N >= 4)
+    ok = (a.is_cuda and a.dtype == torch.float32 and a.dim() == 2 and a.is_contiguous()
+          and K % 8 == 0 and K >= 8 and N % 4 == 0 and N >= 4)
+    if not ok and _GEMM_FALLBACK_TRACE:
+        import traceback
+        print(f"[wf] GEMM fallback: a {tuple(a.shape)} stride {a.stride()} {a.dtype} "
+              f"contiguous={a.is_contiguous()} K={K} N={N}", flush=True)
+        traceback.print_stack(limit=6)
+    return ok
+
+
+def smallk_ok(a: torch.Tensor, K: int, N: int) -> bool:
+    """True when a (M, K) row matrix times a (K, N) operand takes the small-K kernel
+    (wf_linear_smallk_fwd: K < 8, N % 4 == 0)."""
+    return (a.is_cuda and a.dtype == torch.float32 and a.dim() == 2 and a.stride(1) == 1
+            and 1 <= K <= 7 and N % 4 == 0 and 4 <= N <= 4096)
+
+
+def linear_smallk(x2d: torch.Tensor, w_nk: torch.Tensor,
+                  bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bias + x2d (M, K) . w_nk (N, K)^T for K < 8 (wf_linear_smallk_fwd, exact fp32 FMAs)."""
+    M, K = x2d.shape
+    N = w_nk.shape[0]
+    w = w_nk.detach().reshape(N, K).contiguous()
+    if x2d.stride(1) != 1 or x2d.stride(0) < K:  # overlapping / expanded rows: copy, not clamp
+        x2d = x2d.contiguous()
+    _check(x2d, "x", contiguous=False)
+    _check(w, "w")
+    if bias is not None:
+        bias = bias.detach().contiguous()
+        _check(bias, "bias")
+    out = torch.empty((M, N), dtype=torch.float32, device=x2d.device)
+    _lib.call("wf_linear_smallk_fwd", x2d.data_ptr(), x2d.stride(0), w.data_ptr(),
+              _ptr(bias), out.data_ptr(), N, M, K, N, _stream())
+    return out
 
 
 def mm_rows(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a (M, K) @ b (K, N) -- the data-gradient GEMMs of training (dX = dY W) -- on the
     streaming MFMA GEMM at bf16x3 (fp32-faithful operands, fp32 accumulation; b^T is split
-    per call), instead of the platform BLAS (hipBLASLt).  Shapes the kernel does not take
-    (K % 8 or N % 4 nonzero) fall back to torch.mm."""
+    per call), instead of the platform BLAS (hipBLASLt).  K < 8 (the 4-class head's input
+    gradient) runs on the small-K kernel; other shapes neither takes (N % 4 nonzero) fall back
+    to torch.mm."""
     K, N = b.shape
+    if smallk_ok(a, K, N):
+        return linear_smallk(a, b.t())
     if not mfma_gemm_ok(a, K, N):
         return a.mm(b)
     return linear_rows(a, b.detach().t().contiguous(), None, cache=False,
@@ -1163,10 +1201,13 @@ def mm_rows(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 def linear_rows_any(x2d: torch.Tensor, weight: torch.Tensor,
                     bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """bias + x2d @ weight^T (weight (N, K)) at bf16x3 on the streaming MFMA GEMM, or torch's
-    fp32 addmm for shapes it does not take."""
+    """bias + x2d @ weight^T (weight (N, K)) at bf16x3 on the streaming MFMA GEMM; K < 8 (the
+    4-channel stem's 1x1 residual conv) on the small-K kernel; torch's fp32 addmm for shapes
+    neither takes."""
     N, K = weight.shape[0], x2d.shape[1]
     w2 = weight.reshape(N, K)
+    if smallk_ok(x2d, K, N):
+        return linear_smallk(x2d, w2, bias)
     if not mfma_gemm_ok(x2d, K, N):
         return torch.addmm(bias, x2d, w2.t()) if bias is not None else x2d.mm(w2.t())
     return linear_rows(x2d, w2.detach().contiguous(), None if bias is None else bias.detach(),
