@@ -568,79 +568,37 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
   const int64_t row0 = bw * N;
   const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
 
-  // staging: every global load of this thread first (table entries, 2 K items, 1 V item) into
-  // registers, then the splits and LDS stores -- the round-5 loops waited one memory round trip
-  // per loop iteration in front of the barrier
-  struct Raw8 {  // 8 consecutive activation values as loaded: fp32 (a, b) or bf16 (a's bits)
-    f32x4 a, b;
-  };
-  auto ld8 = [&](int64_t off) -> Raw8 {
-    if (store32(P)) {
-      const f32x4* q = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(qkv) + off);
-      return Raw8{q[0], q[1]};
-    }
-    const u32x4 r = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(qkv) + off);
-    return Raw8{__builtin_bit_cast(f32x4, r), f32x4{0.f, 0.f, 0.f, 0.f}};
-  };
-  auto sp8 = [&](const Raw8& r, bf16x8& hi, bf16x8& lo) {
-    if (store32(P)) {
-      const float v[8] = {r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w};
-      split8<P>(v, hi, lo);
-    } else {
-      hi = __builtin_bit_cast(bf16x8, r.a);
-      lo = z8;
-    }
-  };
-  constexpr int NTU = (TBLN + 511) / 512, NKU = N * 2 / 512;
-  static_assert((N / 4) * 2 <= 512 && N * 2 % 512 == 0, "staging items per thread");
-  const bool vthr = tid < (N / 4) * 2;
-  float tv[NTU];
-  Raw8 kr[NKU], vr[4];
-#pragma unroll
-  for (int u = 0; u < NTU; ++u) {
-    const int i = tid + 512 * u;
-    tv[u] = i < TBLN ? table[(int64_t)i * heads + h] * 1.4426950408889634f : 0.f;
-  }
-#pragma unroll
-  for (int u = 0; u < NKU; ++u) {  // K: (key, 8-value chunk)
-    const int it = tid + 512 * u;
-    kr[u] = ld8((row0 + (it >> 1)) * ld + C + h * HD + (it & 1) * 8);
-  }
-  if (vthr) {  // V: (key quad, 8-value chunk)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) vr[r] = ld8((row0 + 4 * (tid >> 1) + r) * ld + 2 * C + h * HD + (tid & 1) * 8);
-  }
-#pragma unroll
-  for (int u = 0; u < NTU; ++u) {
-    const int i = tid + 512 * u;
-    if (i >= TBLN) break;
-    const float v = tv[u];
+  for (int i = tid; i < TBLN; i += 512)
 #if WF_ATTN_T4
+  {
     // tq[j].c = tbr[j + c] = table[TBLN - 1 - j - c] (0 past the end: never read)
+    const float v = table[(int64_t)i * heads + h] * 1.4426950408889634f;
     const int j = TBLN - 1 - i;
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       if (j - c >= 0) reinterpret_cast<float*>(&tq[j - c])[c] = v;
     if (j >= TBLN - 3)
       for (int c = TBLN - j; c < 4; ++c) reinterpret_cast<float*>(&tq[j])[c] = 0.f;
-#else
-    tbr[TBLN - 1 - i] = v;
-#endif
   }
-#pragma unroll
-  for (int u = 0; u < NKU; ++u) {
-    const int it = tid + 512 * u;
+#else
+    tbr[TBLN - 1 - i] = table[(int64_t)i * heads + h] * 1.4426950408889634f;
+#endif
+  for (int it = tid; it < N * 2; it += 512) {  // K: (key, 8-value chunk)
     const int key = it >> 1, ch = it & 1, sw = kswz(key);
-    bf16x8 hi, lo;
-    sp8(kr[u], hi, lo);
+    bf16x8 hi = z8, lo = z8;
+    load8_split<P>(qkv, (row0 + key) * ld + C + h * HD + ch * 8, hi, lo);
     *reinterpret_cast<bf16x8*>(&Ks[key * KS + 8 * (ch ^ sw)]) = hi;
     *reinterpret_cast<bf16x8*>(&Ks[key * KS + 8 * ((2 + ch) ^ sw)]) = SPLIT ? lo : z8;
   }
-  if (vthr) {
-    const int k4 = tid >> 1, ch = tid & 1;
+  for (int it = tid; it < (N / 4) * 2; it += 512) {  // V: (key quad, 8-value chunk)
+    const int k4 = it >> 1, ch = it & 1;
     bf16x8 vh[4], vl[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sp8(vr[r], vh[r], vl[r]);
+    for (int r = 0; r < 4; ++r) {
+      vh[r] = z8;
+      vl[r] = z8;
+      load8_split<P>(qkv, (row0 + 4 * k4 + r) * ld + 2 * C + h * HD + ch * 8, vh[r], vl[r]);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int o = k4 * VB + (ch * 8 + j) * 4;

@@ -17,6 +17,10 @@
 // (identity / window gather / PatchMerging gather) and the epilogue are template parameters
 // so each call site compiles to straight-line code with 32-bit index math.
 #include "gemm_common.hpp"
+// cache policy of the staged (1-KB-per-instruction) output stores: 0 default, 2 nt (A/B)
+#ifndef WF_ROWS_STORE_POLICY
+#define WF_ROWS_STORE_POLICY 0
+#endif
 
 #ifndef WF_ROWS_DBG  // 1: timing-experiment build (GemmArgs::dbg phase skips; never the shipped library)
 #define WF_ROWS_DBG 0
@@ -421,7 +425,8 @@ __global__ __launch_bounds__(NTH) void gemm_rows_kernel(GemmArgs g) {
 #endif
           __builtin_amdgcn_raw_buffer_store_b128(
               __builtin_bit_cast(u32x4, v), orsrc,
-              doff + (int)(((tile * 16 + half * SROWS + r) * g.ldo + 4 * c4) * 4), 0, 0);
+              doff + (int)(((tile * 16 + half * SROWS + r) * g.ldo + 4 * c4) * 4), 0,
+              WF_ROWS_STORE_POLICY);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

@@ -1184,6 +1184,16 @@ def linear_smallk(x2d: torch.Tensor, w_nk: torch.Tensor,
     return out
 
 
+def _rows_dense(a: torch.Tensor) -> torch.Tensor:
+    """A channel slice of a wider channel-last tensor (unit column stride, rows further apart
+    than K -- e.g. the gradient of one input of a channel concatenation) as dense rows: one
+    copy, instead of handing the product to the platform BLAS (the streaming GEMM reads rows K
+    apart)."""
+    if a.dim() == 2 and a.stride(1) == 1 and not a.is_contiguous():
+        return a.contiguous()
+    return a
+
+
 def mm_rows(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a (M, K) @ b (K, N) -- the data-gradient GEMMs of training (dX = dY W) -- on the
     streaming MFMA GEMM at bf16x3 (fp32-faithful operands, fp32 accumulation; b^T is split
@@ -1193,6 +1203,7 @@ def mm_rows(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     K, N = b.shape
     if smallk_ok(a, K, N):
         return linear_smallk(a, b.t())
+    a = _rows_dense(a)
     if not mfma_gemm_ok(a, K, N):
         return a.mm(b)
     return linear_rows(a, b.detach().t().contiguous(), None, cache=False,
@@ -1208,6 +1219,7 @@ def linear_rows_any(x2d: torch.Tensor, weight: torch.Tensor,
     w2 = weight.reshape(N, K)
     if smallk_ok(x2d, K, N):
         return linear_smallk(x2d, w2, bias)
+    x2d = _rows_dense(x2d)
     if not mfma_gemm_ok(x2d, K, N):
         return torch.addmm(bias, x2d, w2.t()) if bias is not None else x2d.mm(w2.t())
     return linear_rows(x2d, w2.detach().contiguous(), None if bias is None else bias.detach(),
