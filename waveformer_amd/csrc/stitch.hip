@@ -29,6 +29,8 @@ struct StitchArgs {
   int n[3];              // windows per axis (z, y, x)
   int world, sb;         // row mapping of the gathered shards
   int rank;              // PARTIAL: this rank's windows only (g % world == rank), local rows
+  int buf;               // the patch rows fit a buffer resource (< 2^31 bytes): batched loads
+  uint32_t pbytes;       // their size in bytes
   int starts[3][SW_MAX_WIN];
 };
 
@@ -43,6 +45,26 @@ __device__ __forceinline__ void cover(const int* st, int n, int r, int p, int& l
     }
   }
 }
+// the same, also returning the starts of the first three covering windows (the loop index is
+// uniform, so the starts are scalar loads; indexing the kernel-argument table with a per-lane
+// window index instead would be a dependent memory load per window)
+__device__ __forceinline__ void cover3(const int* st, int n, int r, int p, int& lo, int& hi,
+                                       int (&s3)[3]) {
+  lo = n;
+  hi = -1;
+  s3[0] = s3[1] = s3[2] = 0;
+  for (int i = 0; i < n; ++i) {
+    const int s = st[i];
+    if (s <= p && p < s + r) {
+      if (hi < 0) lo = i;
+      const int k = i - lo;  // covering windows are consecutive (ascending starts)
+      if (k == 0) s3[0] = s;
+      else if (k == 1) s3[1] = s;
+      else if (k == 2) s3[2] = s;
+      hi = i;
+    }
+  }
+}
 
 // PARTIAL (the all-reduce exchange, ABI 14): only the windows this rank predicted (g % world
 // == rank, local patch row g / world), summed in window order; out is (B, C + 1, D, H, W):
@@ -51,6 +73,68 @@ __device__ __forceinline__ void cover(const int* st, int n, int r, int p, int& l
 // Index arithmetic in 32 bits (the host checks every count fits): the round-5 kernel decoded
 // the voxel and mapped each window to its patch row with 64-bit divisions (a software routine
 // each), which set its time at 23 % of HBM.  World 1 (one rank) needs no row mapping at all.
+// one voxel's covering windows: first / last index and the first three starts per axis
+struct StitchPos {
+  int z, y, x, z0, y0, x0, z1, y1, x1, gb, R3;
+  int sz[3], sy[3], sx[3];
+};
+
+// windows (z0 + dz0 + [0, MZ)) x (y0 + [0, MY)) x (x0 + [0, MX)) of one voxel, channels
+// [c0, c0 + 4): every load of the batch issued before the first use, then the products added in
+// window order (z, y, x) -- product and sum rounded separately, as the reference does.  Absent
+// windows / channels load 0 (offset past the buffer resource).
+template <int MZ, int MY, int MX>
+__device__ __forceinline__ void stitch_batch(const StitchArgs& a, const StitchPos& q, int dz0,
+                                             int c0, int nc, bool count, float (&acc)[4],
+                                             float& cnt) {
+#pragma clang fp contract(off)
+  constexpr int MB = MZ * MY * MX;
+  constexpr uint32_t NONE = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.patches), 0, (int)a.pbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.map), 0, q.R3 * 4, 0x00020000);
+  const uint32_t world = (uint32_t)a.world, sb = (uint32_t)a.sb;
+  const uint32_t cstride = (uint32_t)q.R3 * 4u;
+  uint32_t mo[MB], po[MB];
+#pragma unroll
+  for (int u = 0; u < MB; ++u) {
+    const int dz = dz0 + u / (MY * MX), dy = (u / MX) % MY, dx = u % MX;
+    const int iz = q.z0 + dz, iy = q.y0 + dy, ix = q.x0 + dx;
+    const int zs = dz == 0 ? q.sz[0] : dz == 1 ? q.sz[1] : q.sz[2];
+    const bool ok = iz <= q.z1 && iy <= q.y1 && ix <= q.x1;
+    const uint32_t g = (uint32_t)(q.gb + (iz * a.n[1] + iy) * a.n[2] + ix);
+    uint32_t row = g;
+    if (world != 1) {  // patch row of window g in the gathered shards (see row_of)
+      const uint32_t r = g % world, j = g / world;
+      row = ((j / sb) * world + r) * sb + (j % sb);
+    }
+    const uint32_t loc =
+        (uint32_t)(((q.z - zs) * a.rh + (q.y - q.sy[dy])) * a.rw + (q.x - q.sx[dx]));
+    mo[u] = ok ? loc * 4u : NONE;
+    po[u] = ok ? ((row * (uint32_t)a.C + (uint32_t)c0) * (uint32_t)q.R3 + loc) * 4u : NONE;
+  }
+  float wv[MB], pv[MB][4];
+  asm volatile("" ::: "memory");  // one batch in flight at a time (registers: occupancy)
+#pragma unroll
+  for (int u = 0; u < MB; ++u) {
+    wv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, mo[u], 0, 0));
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      pv[u][c] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rp, c < nc ? po[u] + c * cstride : NONE, 0, 0));
+  }
+#pragma unroll
+  for (int u = 0; u < MB; ++u) {
+    if (count) cnt = cnt + wv[u];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float prod = pv[u][c] * wv[u];  // rounded on its own (no FMA)
+      acc[c] = acc[c] + prod;
+    }
+  }
+}
+
 template <bool PARTIAL>
 __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
   // hipcc contracts a*b+c into an FMA by default (also across the inlined __fmul_rn /
@@ -67,10 +151,10 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
   t /= (uint32_t)a.H;
   const int z = (int)(t % (uint32_t)a.D);
   const int b = (int)(t / (uint32_t)a.D);
-  int z0, z1, y0, y1, x0, x1;
-  cover(a.starts[0], a.n[0], a.rd, z, z0, z1);
-  cover(a.starts[1], a.n[1], a.rh, y, y0, y1);
-  cover(a.starts[2], a.n[2], a.rw, x, x0, x1);
+  int z0, z1, y0, y1, x0, x1, sz[3], sy[3], sx[3];
+  cover3(a.starts[0], a.n[0], a.rd, z, z0, z1, sz);
+  cover3(a.starts[1], a.n[1], a.rh, y, y0, y1, sy);
+  cover3(a.starts[2], a.n[2], a.rw, x, x0, x1, sx);
   const int R3 = a.rd * a.rh * a.rw;
   const int nwin = a.n[0] * a.n[1] * a.n[2];
   const int64_t S = (int64_t)a.D * a.H * a.W;
@@ -89,56 +173,31 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
     return (int)(((j / sb) * world + r) * sb + (j % sb));
   };
 
-  // overlap <= 0.5 (the inferer's default): at most 2 windows per axis cover a voxel.  Their
-  // patch rows, map offsets and weights are gathered first, so all of a voxel's loads are in
-  // flight at once (the window loops below issue them one window at a time, a memory latency
-  // each); the sums are formed in the same window order either way.
-  if (!PARTIAL && z1 - z0 <= 1 && y1 - y0 <= 1 && x1 - x0 <= 1) {
-    constexpr int MW = 8;
-    int nw = 0;
-    int locs[MW];
-    int64_t base[MW];
-#pragma unroll
-    for (int u = 0; u < MW; ++u) {
-      const int iz = z0 + (u >> 2), iy = y0 + ((u >> 1) & 1), ix = x0 + (u & 1);
-      const bool ok = iz <= z1 && iy <= y1 && ix <= x1;
-      const int izc = ok ? iz : z0, iyc = ok ? iy : y0, ixc = ok ? ix : x0;
-      const int g = gb + (izc * a.n[1] + iyc) * a.n[2] + ixc;
-      locs[u] = ((z - a.starts[0][izc]) * a.rh + (y - a.starts[1][iyc])) * a.rw +
-                (x - a.starts[2][ixc]);
-      base[u] = ok ? (int64_t)row_of(g) * a.C * R3 + locs[u] : -1;
-      nw += ok;
-    }
-    float wv[MW];
-#pragma unroll
-    for (int u = 0; u < MW; ++u) wv[u] = base[u] >= 0 ? a.map[locs[u]] : 0.f;
+  // <= 3 covering windows per axis (overlap <= 0.5, the inferer's default, gives 2, and 3
+  // where the last window is shifted back to fit: [112, 128) of a 240-voxel axis lies in the
+  // windows at 0, 64 and 112): the covering windows' loads are issued in batches -- all 8 of a
+  // 2 x 2 x 2 cover at once, one batch of <= 3 x 3 (y, x) windows per z window otherwise --
+  // as buffer loads whose offsets for absent windows and channels fall outside the resource
+  // (they return 0; adding the +0 products to sums that start at +0 is exact), and summed in
+  // window order.  The generic loops below wait one memory round trip per window, twice.
+  if (!PARTIAL && a.buf && z1 - z0 <= 2 && y1 - y0 <= 2 && x1 - x0 <= 2) {
+    StitchPos q{z, y, x, z0, y0, x0, z1, y1, x1, gb, R3,
+                {sz[0], sz[1], sz[2]}, {sy[0], sy[1], sy[2]}, {sx[0], sx[1], sx[2]}};
+    const bool two = z1 - z0 <= 1 && y1 - y0 <= 1 && x1 - x0 <= 1;
     float cnt = 0.f;
-#pragma unroll
-    for (int u = 0; u < MW; ++u)
-      if (base[u] >= 0) cnt = cnt + wv[u];
     for (int c0 = 0; c0 < a.C; c0 += 4) {
       const int nc = min(4, a.C - c0);
-      float pv[MW][4];
-#pragma unroll
-      for (int u = 0; u < MW; ++u)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          pv[u][c] = (base[u] >= 0 && c < nc) ? a.patches[base[u] + (int64_t)(c0 + c) * R3] : 0.f;
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < MW; ++u)
-        if (base[u] >= 0) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float prod = pv[u][c] * wv[u];  // rounded on its own (no FMA)
-            acc[c] = acc[c] + prod;
-          }
-        }
+      if (two) {
+        stitch_batch<2, 2, 2>(a, q, 0, c0, nc, c0 == 0, acc, cnt);
+      } else {
+#pragma nounroll
+        for (int dz = 0; dz <= z1 - z0; ++dz) stitch_batch<1, 3, 3>(a, q, dz, c0, nc, c0 == 0, acc, cnt);
+      }
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         if (c < nc) dst[(int64_t)(c0 + c) * S] = __fdiv_rn(acc[c], cnt);
     }
-    (void)nw;
     return;
   }
 
@@ -347,6 +406,19 @@ static int stitch_launch(const float* patches, int64_t world, int64_t slots_per_
   WF_REQUIRE(total < ((int64_t)1 << 31) && rd * rh * rw < ((int64_t)1 << 31) &&
                  B * nwin[0] * nwin[1] * nwin[2] < ((int64_t)1 << 31),
              "sliding-window stitch: more than 2^31 voxels or windows");
+  {  // the batched loads' 32-bit byte offsets: every patch row the kernel can address
+    const int64_t R3 = rd * rh * rw, ng = B * nwin[0] * nwin[1] * nwin[2];
+    int64_t rows = 0;
+    for (int64_t g = 0; g < ng; ++g) {
+      const int64_t r = g % world, j = g / world;
+      const int64_t row = world == 1 ? g : ((j / slots_per_round) * world + r) * slots_per_round +
+                                               j % slots_per_round;
+      rows = std::max(rows, row + 1);
+    }
+    const int64_t bytes = rows * C * R3 * 4;
+    a.buf = !partial && bytes < ((int64_t)1 << 31) && R3 * 16 < ((int64_t)1 << 31);
+    a.pbytes = a.buf ? (uint32_t)bytes : 0u;
+  }
   if (partial)
     hipLaunchKernelGGL(stitch_kernel<true>, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
                        (hipStream_t)stream, a);
