@@ -86,7 +86,7 @@ struct StitchPos {
 template <int MZ, int MY, int MX>
 __device__ __forceinline__ void stitch_batch(const StitchArgs& a, const StitchPos& q, int dz0,
                                              int c0, int nc, bool count, float (&acc)[4],
-                                             float& cnt) {
+                                             float& cnt, int mz = 3, int my = 3, int mx = 3) {
 #pragma clang fp contract(off)
   constexpr int MB = MZ * MY * MX;
   constexpr uint32_t NONE = 0x80000000u;
@@ -118,6 +118,14 @@ __device__ __forceinline__ void stitch_batch(const StitchArgs& a, const StitchPo
   asm volatile("" ::: "memory");  // one batch in flight at a time (registers: occupancy)
 #pragma unroll
   for (int u = 0; u < MB; ++u) {
+    // mz / my / mx (wave-uniform): the widest cover of the wave per axis -- slots beyond it
+    // are absent for every lane, and their loads are skipped by a scalar branch
+    if (u / (MY * MX) >= mz || (u / MX) % MY >= my || u % MX >= mx) {
+      wv[u] = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pv[u][c] = 0.f;
+      continue;
+    }
     wv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, mo[u], 0, 0));
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -184,15 +192,23 @@ __global__ __launch_bounds__(256) void stitch_kernel(StitchArgs a) {
     StitchPos q{z, y, x, z0, y0, x0, z1, y1, x1, gb, R3,
                 {sz[0], sz[1], sz[2]}, {sy[0], sy[1], sy[2]}, {sx[0], sx[1], sx[2]}};
     const bool two = z1 - z0 <= 1 && y1 - y0 <= 1 && x1 - x0 <= 1;
+    // wave-uniform: does any lane of this path need a second window on the axis
+    const int mz = __any(two && z1 > z0) ? 2 : 1, my = __any(two && y1 > y0) ? 2 : 1,
+              mx = __any(two && x1 > x0) ? 2 : 1;
+    const int ny3 = __any(!two && y1 - y0 >= 2) ? 3 : __any(!two && y1 > y0) ? 2 : 1;
+    const int nx3 = __any(!two && x1 - x0 >= 2) ? 3 : __any(!two && x1 > x0) ? 2 : 1;
     float cnt = 0.f;
     for (int c0 = 0; c0 < a.C; c0 += 4) {
       const int nc = min(4, a.C - c0);
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
       if (two) {
-        stitch_batch<2, 2, 2>(a, q, 0, c0, nc, c0 == 0, acc, cnt);
+        // batch shape = the wave's widest cover per axis (z and y are nearly uniform over a
+        // wave, which runs along x): absent windows still cost a load instruction each
+        stitch_batch<2, 2, 2>(a, q, 0, c0, nc, c0 == 0, acc, cnt, mz, my, mx);
       } else {
 #pragma nounroll
-        for (int dz = 0; dz <= z1 - z0; ++dz) stitch_batch<1, 3, 3>(a, q, dz, c0, nc, c0 == 0, acc, cnt);
+        for (int dz = 0; dz <= z1 - z0; ++dz)
+          stitch_batch<1, 3, 3>(a, q, dz, c0, nc, c0 == 0, acc, cnt, 1, ny3, nx3);
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c)

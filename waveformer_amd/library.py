@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -242,6 +243,7 @@ def _attn_setup(ctx, inputs, output):
     _, work, lse = output
     ctx.meta = (ws, heads, float(scale), float(eps), bool(train))
     ctx.save_for_backward(x, ln_w, ln_b, wqkv, bqkv, table, index, wproj, bproj, work, lse)
+    ctx.set_materialize_grads(False)  # no zero gradients for the workspace / lse outputs
 
 
 _BLAS_WGRAD = os.environ.get("WF_TRAIN_BLAS_WGRAD") == "1"
@@ -255,15 +257,28 @@ def _wgrad(dy: Tensor, x: Tensor) -> Tensor:
     return ops.gemm_tn(dy, x)
 
 
+_INDEX_GROUPS: dict = {}
+
+
 def _index_groups(index: Tensor, rows: int) -> Tuple[Tensor, Tensor]:
     """The relative-position index (attention.py:40-56) grouped by table row for the
     deterministic bias-table gather (wf_rel_pos_bias_bwd): `perm` = the flat positions in a
-    stable sort by row, `offsets` (rows + 1) the group boundaries."""
+    stable sort by row, `offsets` (rows + 1) the group boundaries.  The index is a constant
+    buffer: the grouping is kept per (tensor, version) instead of a device sort per backward
+    (a weak reference checks that the cached entry is still that tensor)."""
+    key = (index.data_ptr(), index._version, tuple(index.shape), rows, str(index.device))
+    hit = _INDEX_GROUPS.get(key)
+    if hit is not None and hit[0]() is index:
+        return hit[1], hit[2]
     flat = index.reshape(-1)
     vals, perm = torch.sort(flat, stable=True)
     offsets = torch.searchsorted(vals, torch.arange(rows + 1, device=index.device,
                                                     dtype=vals.dtype))
-    return perm.contiguous(), offsets.to(torch.int64).contiguous()
+    perm, offsets = perm.contiguous(), offsets.to(torch.int64).contiguous()
+    if len(_INDEX_GROUPS) >= 64:
+        _INDEX_GROUPS.clear()
+    _INDEX_GROUPS[key] = (weakref.ref(index), perm, offsets)
+    return perm, offsets
 
 
 @torch.library.custom_op("waveformer::window_attn_backward", mutates_args=(),
@@ -330,6 +345,8 @@ def _(gout, x, ln_w, ln_b, wqkv, bqkv, table, index, wproj, bproj, work, lse, ep
 
 def _attn_bwd(ctx, gout, _gwork, _glse):
     x, ln_w, ln_b, wqkv, bqkv, table, index, wproj, bproj, work, lse = ctx.saved_tensors
+    if gout is None:  # grads are not materialized (see _attn_setup)
+        gout = torch.zeros_like(x)
     ws, heads, scale, eps, train = ctx.meta
     if not train:
         raise RuntimeError("waveformer::window_attn: backward of a train=False call")
@@ -367,6 +384,8 @@ def _(srcs, shortcut, branch_scale, ln_eps, want_stats):
 def _msfuse_setup(ctx, inputs, output):
     srcs, shortcut, branch_scale, ln_eps, want_stats = inputs
     ctx.save_for_backward(branch_scale, *srcs)
+    ctx.shortcut_like = (shortcut.shape, shortcut.dtype, shortcut.device)
+    ctx.set_materialize_grads(False)  # no zero gradient for the statistics output
 
 
 @torch.library.custom_op("waveformer::msfuse_backward", mutates_args=(), device_types="cuda")
@@ -404,6 +423,9 @@ def _(gxh, branch_scale, srcs):
 
 def _msfuse_bwd(ctx, gxh, _gstats):
     s_attn, *srcs = ctx.saved_tensors
+    if gxh is None:  # grads are not materialized (see _msfuse_setup)
+        shape, dtype, device = ctx.shortcut_like
+        gxh = torch.zeros(shape, dtype=dtype, device=device)
     return torch.ops.waveformer.msfuse_backward(gxh, s_attn, srcs), gxh, None, None, None
 
 
@@ -462,6 +484,9 @@ def _ffn_setup(ctx, inputs, output):
      eps2, prec, train) = inputs
     ctx.block = stats is not None
     ctx.meta = (n2eps, eps1, eps2, bool(train))
+    # the workspace output never receives a gradient: without this, autograd fills a zero
+    # gradient of its full size (hundreds of MB per block) before calling the backward
+    ctx.set_materialize_grads(False)
     ctx.save_for_backward(xh, n2w, n2b, pww, pwb, l1w, l1b, dww, l2w, l2b, fcw, fcb, s_mlp,
                           output[1])
 
@@ -544,6 +569,8 @@ def _(gout, xh, n2w, n2b, pww, pwb, l1w, l1b, dww, l2w, l2b, fcw, fcb, s_mlp, wo
 
 def _ffn_bwd(ctx, gout, _gwork):
     xh, n2w, n2b, pww, pwb, l1w, l1b, dww, l2w, l2b, fcw, fcb, s_mlp, work = ctx.saved_tensors
+    if gout is None:  # grads are not materialized (see _ffn_setup)
+        gout = torch.zeros_like(xh)
     n2eps, eps1, eps2, train = ctx.meta
     if not train:
         raise RuntimeError("waveformer::ccf_ffn: backward of a train=False call")

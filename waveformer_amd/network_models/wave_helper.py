@@ -366,7 +366,7 @@ class WaveletTransform3D(nn.Module):
         cur = x.permute(0, 2, 3, 4, 1).contiguous()
         yh = []
         for _ in range(level):
-            bands = _OPS.dwt3d(cur, None, None, 0.0)
+            bands = _OPS.dwt3d(cur, None, None, 0.0).unbind(0)  # one stack in backward
             cur = bands[0]
             yh.append(ops.bands_to_coeffs(bands)[1])
         return cur.permute(0, 4, 1, 2, 3), list(reversed(yh))
@@ -488,11 +488,14 @@ class Block(nn.Module):
         return lls
 
     def _levels(self, x, ln1, n):
-        """n one-level Haar DWTs (norm1 fused into the first): [band buffers], fine -> coarse."""
+        """n one-level Haar DWTs (norm1 fused into the first): per level the 8 band views
+        (LL first) of its band buffer, fine -> coarse.  The buffer is unbound once, so its
+        gradient is assembled by one stack in backward instead of eight select-backward
+        zero-fills, copies and full-buffer accumulations."""
         bands, cur = [], x
         for i in range(n):
             b = _OPS.dwt3d(cur, ln1[0] if i == 0 else None, ln1[1] if i == 0 else None,
-                           float(ln1[2]) if i == 0 else 0.0)
+                           float(ln1[2]) if i == 0 else 0.0).unbind(0)
             bands.append(b)
             cur = b[0]
         return bands
@@ -527,7 +530,7 @@ class Block(nn.Module):
                 with torch.cuda.stream(side):
                     cur, rest = bands[0][0], []
                     for _ in range(n - 1):
-                        b = _OPS.dwt3d(cur, None, None, 0.0)
+                        b = _OPS.dwt3d(cur, None, None, 0.0).unbind(0)
                         rest.append(b)
                         cur = b[0]
                     rest_srcs = [self.attn.forward_raster(b[0]) for b in rest]

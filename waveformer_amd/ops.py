@@ -437,9 +437,10 @@ def dwt3d_haar_ll(x_cl: torch.Tensor, ln: Optional[Tuple[torch.Tensor, torch.Ten
     return ll
 
 
-def bands_to_coeffs(bands: torch.Tensor) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
-    """(8,B,d,h,w,C) bands -> (LL, detail dict) as NCDHW-shaped (channel-last strided) views,
-    the structure ptwt.wavedec3(level=1) returns (wave_helper.py:350-353)."""
+def bands_to_coeffs(bands) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+    """(8,B,d,h,w,C) bands (or their 8 unbound (B,d,h,w,C) views) -> (LL, detail dict) as
+    NCDHW-shaped (channel-last strided) views, the structure ptwt.wavedec3(level=1) returns
+    (wave_helper.py:350-353)."""
     ll = bands[0].permute(0, 4, 1, 2, 3)
     det = {k: bands[i + 1].permute(0, 4, 1, 2, 3) for i, k in enumerate(DETAIL_KEYS)}
     return ll, det
