@@ -525,6 +525,9 @@ __device__ __forceinline__ int kswz(int row) {  // 16-B chunk XOR of a K row (se
 #define WF_ATTN_DOT2 1
 #endif
 // WF_ATTN_QP (round 6): two 16-query sub-tiles per wave in one loop (see the kernel); 0: one
+#ifndef WF_ATTN_QP_VSUM
+#define WF_ATTN_QP_VSUM 1
+#endif
 #ifndef WF_ATTN_QP
 #define WF_ATTN_QP 1
 #endif
@@ -616,6 +619,14 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
 #if WF_ATTN_QP
   static_assert(WF_ATTN_LAZY && WF_ATTN_MFMA_SUM && WF_ATTN_T4 && WF_ATTN_BPERMUTE,
                 "the query-pair loop implements the default options only");
+  // WF_ATTN_QP_VSUM (split operands): the row sums as fp32 VALU adds of the exponentials (each
+  // lane's partial over its 4 keys per 16-key block, the 4 lanes of a query reduced once at
+  // the end) instead of the ones-operand MFMAs (4 of 18 per tile and sub-tile): 157.0 vs
+  // 159.6 us per B = 8 stage-1 launch, interleaved (profiles/r6/r6n_attn_vsum_ab.txt).  The
+  // sum is then of the fp32 exponentials rather than of their hi + lo splits (closer to exact
+  // by the split's 2^-16 residual).  Plain bf16 / fp16 keep the MFMA sums: their l must be
+  // the sum of the same rounded P the numerator uses.
+  constexpr bool VSUM = WF_ATTN_QP_VSUM && SPLIT;
   if (nsub >= 16) {
     // two independent 16-query sub-tiles per wave (st and st + 8): every K / V fragment read
     // from LDS feeds both, and the two sub-tiles' dependency chains (scores -> max -> exp ->
@@ -682,10 +693,12 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
 #pragma unroll
           for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-            for (int i = 0; i < 4; i += 2)
-              split_pair<P>(__builtin_amdgcn_exp2f(s[u][kt][i] - mrun[u]),
-                            __builtin_amdgcn_exp2f(s[u][kt][i + 1] - mrun[u]), ph[u][kt][i >> 1],
-                            pl[u][kt][i >> 1]);
+            for (int i = 0; i < 4; i += 2) {
+              const float e0 = __builtin_amdgcn_exp2f(s[u][kt][i] - mrun[u]);
+              const float e1 = __builtin_amdgcn_exp2f(s[u][kt][i + 1] - mrun[u]);
+              if (VSUM) l4[u][0] += e0 + e1;
+              split_pair<P>(e0, e1, ph[u][kt][i >> 1], pl[u][kt][i >> 1]);
+            }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int o1 = (16 * t + 8 * j + g4) * VB + l15 * 4;
@@ -708,15 +721,19 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
                   bf16x8, u32x4{pl[u][2 * j][0], pl[u][2 * j][1], pl[u][2 * j + 1][0], pl[u][2 * j + 1][1]});
               o[u] = mma32<P>(vl, pb, o[u]);
               o[u] = mma32<P>(vh, plb, o[u]);
-              l4[u] = mma32<P>(ones, plb, l4[u]);
+              if (!VSUM) l4[u] = mma32<P>(ones, plb, l4[u]);
             }
             o[u] = mma32<P>(vh, pb, o[u]);
-            l4[u] = mma32<P>(ones, pb, l4[u]);
+            if (!VSUM) l4[u] = mma32<P>(ones, pb, l4[u]);
           }
         }
       }
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
+        if (VSUM) {  // the 4 lanes (g4) of query l15
+          l4[u][0] += __shfl_xor(l4[u][0], 16, 64);
+          l4[u][0] += __shfl_xor(l4[u][0], 32, 64);
+        }
         const float inv = 1.f / l4[u][0];
         const int64_t off = (row0 + qq[u]) * C + h * HD + 4 * g4;
         if (store32(P)) {
