@@ -730,9 +730,14 @@ inline int conv3_ksplit(int64_t wgs, int nch) {
 // split-K; WF_CONV_WIDE=0 keeps the 8-channel kernels
 static bool conv3w_ok(const Conv3Args& a, int prec, int64_t wgs) {
   static const bool on = !getenv("WF_CONV_WIDE") || getenv("WF_CONV_WIDE")[0] != '0';
-  // Cin > 88: at 48 input channels (3 steps per tile) the exposed per-tile prologue of the one
-  // workgroup per CU costs more than the wider loads save (profiles/r5_conv_wide_ab.txt)
-  static const int min_cin = getenv("WF_CONV_WIDE_MINCIN") ? atoi(getenv("WF_CONV_WIDE_MINCIN")) : 89;
+  // Cin > 88 for fp16 / bf16: at 48 input channels (3 steps per tile) the exposed per-tile
+  // prologue of the one workgroup per CU costs more than the wider loads save
+  // (profiles/r5_conv_wide_ab.txt); the split's longer K loop (three MFMAs per product) hides
+  // it at 128^3: 48 -> 48 1607-1616 vs 1627-1655 us at B = 2 (profiles/r6/r6p_conv_wide48_ab.txt),
+  // 3523 vs 3590 at B = 4; at 64^3 (2048 workgroups, eight per CU in turn) it measured 5 %
+  // slower (profiles/r6/r6q.txt), so only planes wider than 64
+  static const int env_min = getenv("WF_CONV_WIDE_MINCIN") ? atoi(getenv("WF_CONV_WIDE_MINCIN")) : 0;
+  const int min_cin = env_min ? env_min : (prec == PREC_SPLIT && !a.xh && a.W > 64 ? 48 : 89);
   // fp16 input: 16-B loads of 8 channels (16-B aligned rows and channel offsets)
   return on && a.Cout % 48 == 0 && a.W > 32 && wgs >= 512 && a.Cin >= min_cin &&
          (!a.xh || (a.Cin % 8 == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.xh & 15) == 0));

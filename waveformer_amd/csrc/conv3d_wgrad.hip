@@ -12,7 +12,8 @@
 // A workgroup owns (48 or 16 output channels) x (16 input channels) x all 27 taps and walks a
 // contiguous range of position tiles (one z-plane x 4 rows x 32 columns = 128 positions = 4
 // K-steps of 32).  Per tile it stages, split into bf16 hi / lo:
-//   * g transposed to [co][position]       -> MFMA operand A (lane: 8 consecutive x of one co)
+//   * g transposed to [co][position]       -> MFMA operand A (lane: 8 consecutive x of one co;
+//     rows padded and swizzled against bank conflicts, see gsw)
 //   * the x halo (3 z x 6 y x 34 x) as [ci][z][y][x] -> operand B (8 consecutive x of one ci,
 //     at the tap's shifted row; the x shift of 1 or 2 elements is undone in registers: one
 //     16-B read + one 4-B read and a funnel shift (v_alignbit) instead of 8 scalar reads).
@@ -32,6 +33,16 @@ constexpr int WG_NPOS = WG_TX * WG_TY;           // 128 positions per tile
 constexpr int WG_CI = 16;                        // input channels per workgroup
 constexpr int WG_XPOS = 3 * WG_HY * WG_HX;       // 612 halo positions
 constexpr int WG_XROWS = 3 * WG_HY;              // 18 halo rows
+constexpr int WG_GP = WG_NPOS + 8;               // g tile row pitch in bf16: 272 B (see gsw)
+// g tile rows are 272 B apart (16-B chunk offset r mod 16) and chunk 4 s + g4 of row r sits at
+// 4 s + (g4 ^ gsw(r)): the A reads of the 16 rows l15 at chunk 4 s + g4 then meet 16 distinct
+// 4-bank groups in each of gfx950's ds_read_b128 lane groups ({0-3, 12-15 | g4 0; 20-27 |
+// g4 1} and the like: r + (g4 ^ gsw(r)) covers 0..15 once per group), with the K-step s
+// still an immediate offset.  256-B rows put 8 lanes of a group on the same banks (SQ: 5.8
+// conflict cycles per LDS instruction, profiles/r6/r6q.txt); an XOR of the whole chunk index
+// by the row removed them but cost the immediate offsets, spilled and measured 8 % slower
+// (profiles/r6/r6r.txt)
+__device__ __forceinline__ int gsw(int r) { return ((r + 4) >> 3) & 1; }
 
 struct WgArgs {
   const float* x;   // (B, D, H, W) positions, ldx floats apart, channels [0, Cin)
@@ -53,7 +64,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wgrad_kernel(WgArgs a) {
   constexpr int XITEMS = (WG_XPOS / 2) * (WG_CI / 4);  // halo position pairs x channel quads
   constexpr int NX = (XITEMS + 255) / 256;
   // LDS (bf16 words): g [2 planes][NCO][NPOS], x [2 planes][CI][18 rows][XR]
-  __shared__ __attribute__((aligned(16))) uint16_t gs[2 * NCO * WG_NPOS];
+  __shared__ __attribute__((aligned(16))) uint16_t gs[2 * NCO * WG_GP];
   __shared__ __attribute__((aligned(16))) uint16_t xs[2 * WG_CI * WG_XROWS * WG_XR];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -118,14 +129,10 @@ __global__ __launch_bounds__(256, 2) void conv3d_wgrad_kernel(WgArgs a) {
   };
   // split a pair of positions' 4 channels into (hi, lo) bf16 dwords: word e holds channel e
   // of position 0 (low half) and of position 1 (high half)
+  // (the residual x - hi on v_dot2c_f32_bf16: split_pair, kernels.hpp -- the same bits)
   auto pack = [](const f32x4& p0, const f32x4& p1, uint32_t (&hi)[4], uint32_t (&lo)[4]) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint16_t h0 = f2bf(p0[e]), h1 = f2bf(p1[e]);
-      const uint16_t q0 = f2bf(p0[e] - bf2f(h0)), q1 = f2bf(p1[e] - bf2f(h1));
-      hi[e] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-      lo[e] = (uint32_t)q0 | ((uint32_t)q1 << 16);
-    }
+    for (int e = 0; e < 4; ++e) split_pair<PREC_SPLIT>(p0[e], p1[e], hi[e], lo[e]);
   };
   auto commit = [&]() {
 #pragma unroll
@@ -137,9 +144,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_wgrad_kernel(WgArgs a) {
       pack(rg[j][0], rg[j][1], hi, lo);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        uint32_t* d = reinterpret_cast<uint32_t*>(gs + (4 * q + e) * WG_NPOS) + pp;
+        const int row = 4 * q + e, c = pp >> 2;  // 16-B chunk c = 4 s + g4 of the row
+        uint32_t* d = reinterpret_cast<uint32_t*>(gs + row * WG_GP) +
+                      4 * ((c & ~3) | ((c & 3) ^ gsw(row))) + (pp & 3);
         d[0] = hi[e];
-        d[NCO * WG_NPOS / 2] = lo[e];
+        d[NCO * WG_GP / 2] = lo[e];
       }
     }
 #pragma unroll
@@ -171,9 +180,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_wgrad_kernel(WgArgs a) {
       bf16x8 ah[CO_T], al[CO_T];
 #pragma unroll
       for (int m = 0; m < CO_T; ++m) {
-        const uint16_t* p = gs + (16 * m + l15) * WG_NPOS + s * WG_TX + 8 * g4;
+        const uint16_t* p = gs + (16 * m + l15) * WG_GP + 8 * (4 * s + (g4 ^ gsw(l15)));
         ah[m] = *reinterpret_cast<const bf16x8*>(p);
-        al[m] = *reinterpret_cast<const bf16x8*>(p + NCO * WG_NPOS);
+        al[m] = *reinterpret_cast<const bf16x8*>(p + NCO * WG_GP);
       }
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
