@@ -905,10 +905,14 @@ extern "C" int wf_proj_out_fwd(const float* x, float* out, int normalize, float 
   WF_REQUIRE(B >= 1 && S >= 1 && C >= 4 && C % 4 == 0, "C must be a positive multiple of 4");
   WF_REQUIRE_PTR(x);
   WF_REQUIRE_PTR(out);
-  int64_t TP = (48 * 1024 / 4) / C - 1;  // LDS [C][TP+1] within 48 KB
+  // LDS [C][TP+1] within 64 KB; TP + 1 odd, so the channel rows a group's lanes write (4 apart)
+  // spread over the banks (C = 384 gave TP + 1 = 32 and C = 192 64: every lane of a group on
+  // one bank, 29 / 16 conflict cycles per LDS instruction in profiles/r6/r6j_streaming_sq.txt)
+  int64_t TP = (64 * 1024 / 4) / C - 1;
   if (TP > 64) TP = 64;
   if (TP < 1) TP = 1;
   if (TP > S) TP = S;
+  if (TP > 1 && (TP + 1) % 2 == 0) --TP;
   const size_t lds = (size_t)C * (TP + 1) * sizeof(float);
   const int64_t blocks = B * cdiv(S, TP);
   return dispatch_gv(C / 4, [&](auto G_, auto V_) -> int {
