@@ -749,6 +749,9 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
     return;
   }
 #endif
+  // the query-pair loop's VALU row sums, in the same order, wherever it runs (the qsplit = 4
+  // launches of small grids take this loop: a volume's result must not depend on the batch)
+  constexpr bool VSUM1 = WF_ATTN_QP && WF_ATTN_QP_VSUM && SPLIT && WF_ATTN_MFMA_SUM && WF_ATTN_LAZY;
   for (int st = wid; st < nsub; st += 8) {
     const int q = qs * (N / qsplit) + st * 16 + l15;
     // B operands of S: slots 8 g4 .. +7 <- Q'[q][8 (g4 & 1) ..]: [Q'h | Q'h] and [Q'l | 0]
@@ -856,6 +859,9 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
         for (int i = 0; i < 4; i += 2) {
           const float p0 = __builtin_amdgcn_exp2f(s[kt][i] - mnew);
           const float p1 = __builtin_amdgcn_exp2f(s[kt][i + 1] - mnew);
+#if WF_ATTN_MFMA_SUM
+          if (VSUM1) l4[0] += p0 + p1;
+#endif
           if (WF_ATTN_DOT2) {
             split_pair<P>(p0, p1, ph[kt][i >> 1], pl[kt][i >> 1]);
           } else {
@@ -891,16 +897,20 @@ __global__ __launch_bounds__(512, 2) void attn_tbl_kernel(const void* __restrict
           o = mma32<P>(vl, pb, o);
           o = mma32<P>(vh, plb, o);
 #if WF_ATTN_MFMA_SUM
-          l4 = mma32<P>(ones, plb, l4);
+          if (!VSUM1) l4 = mma32<P>(ones, plb, l4);
 #endif
         }
         o = mma32<P>(vh, pb, o);
 #if WF_ATTN_MFMA_SUM
-        l4 = mma32<P>(ones, pb, l4);
+        if (!VSUM1) l4 = mma32<P>(ones, pb, l4);
 #endif
       }
     }
 #if WF_ATTN_MFMA_SUM
+    if (VSUM1) {  // the 4 lanes (g4) of query l15, as in the query-pair loop
+      l4[0] += __shfl_xor(l4[0], 16, 64);
+      l4[0] += __shfl_xor(l4[0], 32, 64);
+    }
     const float inv = 1.f / l4[0];
 #else
     lsum = xsum16(lsum);
