@@ -564,9 +564,12 @@ __global__ __launch_bounds__(256) void msfuse_kernel(MsfuseArgs a) {
 // then needs 2 LDS reads per source (x interpolation last; ATen interpolates x first, so the
 // fp32 rounding differs in the last bits).  Global traffic: the 4 source rows per source (L2)
 // plus one read of the shortcut row and one write of the output row.
-template <int G, int V>
+// COAL (round 6): the shortcut row is read and the output row written by contiguous 1-KB
+// instructions (lane = f32x4 index of the row) through an LDS image of the row, instead of
+// each instruction touching 16 positions' 64-B pieces (the compute mapping: G lanes per position)
+template <int G, int V, bool COAL = false>
 __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float R[];  // sum_s sw[s] * C
+  extern __shared__ __attribute__((aligned(16))) float R[];  // sum_s sw[s] * C [+ W * C: COAL]
   const int C = a.C, C4 = C >> 2;
   // XCD-contiguous row order: the hardware deals consecutive workgroups round-robin over the
   // 8 XCDs, which put neighbouring output rows -- which read the same 4 source rows per
@@ -585,7 +588,14 @@ __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
   const int64_t rowbase0 = (((int64_t)b * a.D + z) * a.H + y) * a.W;
   const int xf = tid / G;
   f32x4 scp[V];
-  if (xf < a.W) {
+  constexpr int NK = COAL ? 4 : 1;  // COAL: W * C4 <= 1024 f32x4 per row (host-checked)
+  f32x4 scv[NK];
+  const int nrow4 = a.W * C4;
+  if (COAL) {
+    const f32x4* sr = reinterpret_cast<const f32x4*>(a.shortcut + rowbase0 * C);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) scv[k] = sr[min(tid + 256 * k, nrow4 - 1)];
+  } else if (xf < a.W) {
     const f32x4* sc0 = reinterpret_cast<const f32x4*>(a.shortcut + (rowbase0 + xf) * C);
 #pragma unroll
     for (int j = 0; j < V; ++j) scp[j] = sc0[min(gl0 + j * G, C4 - 1)];
@@ -617,6 +627,12 @@ __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
     }
     ro += sw * C;
   }
+  f32x4* T = reinterpret_cast<f32x4*>(R + ro);  // COAL: the row image [W][C4]
+  if (COAL) {
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      if (tid + 256 * k < nrow4) T[tid + 256 * k] = scv[k];
+  }
   __syncthreads();
   const int lane = tid & 63, gl = lane & (G - 1);
   const int gpb = blockDim.x / G;
@@ -647,6 +663,12 @@ __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const int c4 = min(gl + j * G, C4 - 1);
+      if (COAL) {
+        const f32x4 o = T[x * C4 + c4] + acc[j] * bs;
+        v[j] = live[j] ? o : f32x4{0, 0, 0, 0};
+        if (live[j]) T[x * C4 + c4] = o;
+        continue;
+      }
       const f32x4 o = (x == xf ? scp[j] : sc[c4]) + acc[j] * bs;
       v[j] = live[j] ? o : f32x4{0, 0, 0, 0};
 #if MSF_DBG
@@ -663,6 +685,13 @@ __global__ __launch_bounds__(256) void msfuse_row_kernel(MsfuseArgs a) {
         a.stats[2 * (rowbase + x) + 1] = rstd;
       }
     }
+  }
+  if (COAL) {
+    __syncthreads();
+    f32x4* orow = reinterpret_cast<f32x4*>(a.out + rowbase * C);
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      if (tid + 256 * k < nrow4) orow[tid + 256 * k] = T[tid + 256 * k];
   }
 }
 
@@ -887,6 +916,15 @@ extern "C" int wf_msfuse_fwd(const float* const* src, const int64_t* src_dhw, in
   for (int s = 0; s < nsrc; ++s) rlds += (int64_t)a.sw[s] * C * 4;
   return dispatch_gv(C / 4, [&](auto G_, auto V_) -> int {
     constexpr int G = decltype(G_)::value, V = decltype(V_)::value;
+    // COAL for 4-lane groups only: stage 1 (C = 48) 231-233 -> 215-218 us; at C = 96 and
+    // wider it measured 2-5 % slower (profiles/r6/r6ab_msfuse_coal_ab.txt)
+    static const bool coal = !getenv("WF_MSF_COAL") || getenv("WF_MSF_COAL")[0] != '0';
+    if (G <= 4 && coal && W * (C / 4) <= 1024 && W <= 256 / G && rlds + W * C * 4 <= 64 * 1024 &&
+        B * D * H < ((int64_t)1 << 31)) {
+      hipLaunchKernelGGL((msfuse_row_kernel<G, V, true>), dim3((unsigned)(B * D * H)), dim3(256),
+                         (size_t)(rlds + W * C * 4), (hipStream_t)stream, a);
+      return check_launch("wf_msfuse_fwd");
+    }
     if (rlds <= 64 * 1024 && B * D * H < ((int64_t)1 << 31)) {
       hipLaunchKernelGGL((msfuse_row_kernel<G, V>), dim3((unsigned)(B * D * H)), dim3(256),
                          (size_t)rlds, (hipStream_t)stream, a);
