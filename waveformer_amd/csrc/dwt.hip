@@ -326,12 +326,20 @@ __global__ __launch_bounds__(256) void idwt3d_haar_nc4_kernel(IdwtArgs a) {
   const int L = a.levels;
   const int w1 = a.w << (L - 1), h1 = a.h << (L - 1), d1 = a.d << (L - 1);
   const int Wo = 2 * w1, Ho = 2 * h1, Do = 2 * d1, WP = Wo + 2, LP = w1 + 1;
-  int row = blockIdx.x;
+  // 1-D grid of (row, channel block) with the channel blocks of a row adjacent and every XCD
+  // given a contiguous run: the blocks of one row read disjoint channel slices of the same
+  // channel-last detail lines, which now meet in one XCD's L2 (dealt round-robin over the XCDs,
+  // each block's 64-B slices pulled every 192-B position line again: 1.44x the algorithmic
+  // bytes)
+  const int ncb = (a.C + a.CB - 1) / a.CB;
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+  const int lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  int row = lb / ncb;
   const int y1 = row % h1;
   row /= h1;
   const int z1 = row % d1;
   const int b = row / d1;
-  const int c0 = blockIdx.y * a.CB;
+  const int c0 = (lb - (lb / ncb) * ncb) * a.CB;
   const int CB = min(a.CB, a.C - c0);
   const int CB4 = CB >> 2;
   float* lds_ll = lds_nc + (size_t)a.CB * 4 * WP;
@@ -532,7 +540,8 @@ static int idwt_launch(const float* ll, int64_t ll_bstride, int64_t ll_cs, int64
     if (cb > C) cb = C;
     if (cb * per_c <= 64 * 1024) {
       a.CB = (int)cb;
-      dim3 grid((unsigned)(B * d1 * h1), (unsigned)cdiv(C, cb));
+      WF_REQUIRE(B * d1 * h1 * cdiv(C, cb) < ((int64_t)1 << 31), "wf_idwt3d_haar: grid too large");
+      dim3 grid((unsigned)(B * d1 * h1 * cdiv(C, cb)));
       hipLaunchKernelGGL(idwt3d_haar_nc4_kernel, grid, dim3(256), (size_t)(cb * per_c),
                          (hipStream_t)stream, a);
       return check_launch("wf_idwt3d_haar");
