@@ -41,6 +41,7 @@ struct TnArgs {
   int N, K;
   int ntn, ntk;     // column tiles of a / b
   int64_t chunk;    // rows per chunk (multiple of TN_KS)
+  int xcd;          // 1-D XCD-contiguous grid (see gemm_tn_kernel)
 };
 
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(TnArgs g) {
@@ -49,9 +50,20 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(TnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t bs[2 * 2 * TN_PLANE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l15 = lane & 15, g4 = lane >> 4;
-  const int tn = blockIdx.x % g.ntn, tk = blockIdx.x / g.ntn;
+  // g.xcd (1-D grid): the ntn x ntk tiles of one m chunk read the same rows of a and b (column
+  // slices of them), so they run adjacent on one XCD (XCD-contiguous runs of the linear id)
+  // instead of being dealt round-robin over the XCDs' separate L2s
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (g.xcd) {
+    const int nb = gridDim.x, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+    const int lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int nt = g.ntn * g.ntk;
+    bx = lb % nt;
+    by = lb / nt;
+  }
+  const int tn = bx % g.ntn, tk = bx / g.ntn;
   const int n0 = tn * TN_T, k0 = tk * TN_T;
-  const int64_t m_begin = (int64_t)blockIdx.y * g.chunk;
+  const int64_t m_begin = (int64_t)by * g.chunk;
   const int64_t m_end = std::min<int64_t>(m_begin + g.chunk, g.M);
   const int nsteps = (int)((m_end - m_begin + TN_KS - 1) / TN_KS);
   // this lane's gather columns (clamped: out-of-range columns load a valid address, zeroed)
@@ -123,7 +135,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(TnArgs g) {
   }
   // acc[t][i] = c[n0 + 16 wid + 4 g4 + i][k0 + 16 t + l15]  (MFMA 16x16 output layout:
   // lane holds rows 4 g4 .. 4 g4 + 3 of column l15)
-  float* pc = g.part + (int64_t)blockIdx.y * g.N * g.K;
+  float* pc = g.part + (int64_t)by * g.N * g.K;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int k = k0 + 16 * t + l15;
@@ -197,8 +209,13 @@ extern "C" int wf_gemm_tn(const float* a, int64_t lda, const float* b, int64_t l
   const int64_t nchunk = cdiv(M, g.chunk);
   WF_REQUIRE(nchunk <= 65535 && (int64_t)g.ntn * g.ntk < ((int64_t)1 << 31), "grid too large");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(gemm_tn_kernel, dim3((unsigned)(g.ntn * g.ntk), (unsigned)nchunk),
-                     dim3(256), 0, s, g);
+  static const bool xcd = !getenv("WF_TN_XCD") || getenv("WF_TN_XCD")[0] != '0';
+  g.xcd = xcd && g.ntn * g.ntk * nchunk < ((int64_t)1 << 31);
+  if (g.xcd)
+    hipLaunchKernelGGL(gemm_tn_kernel, dim3((unsigned)(g.ntn * g.ntk * nchunk)), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL(gemm_tn_kernel, dim3((unsigned)(g.ntn * g.ntk), (unsigned)nchunk),
+                       dim3(256), 0, s, g);
   int rc = check_launch("wf_gemm_tn");
   if (rc) return rc;
   const int64_t n_el = N * K;
