@@ -31,6 +31,9 @@
 
 namespace wf {
 
+#ifndef WF_C3W_WDMA  // 0: conv3d_k3w stages weights through registers (round-5 form; A/B only)
+#define WF_C3W_WDMA 1
+#endif
 #ifndef WF_CONV_DBG  // 1: timing-experiment build (Conv3Args::dbg phase skips; never the shipped library)
 #define WF_CONV_DBG 0
 #endif
@@ -385,7 +388,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_k3_kernel(Conv3Args a) {
 //     and each weight chunk in LDS serves 512 outputs instead of 256;
 //   * activations [position][16 ch] (32 B) with 16 B of padding after every 8 positions, so a
 //     ds_read_b128 over 16 consecutive positions touches 16 distinct 4-bank groups;
-//   * one workgroup per CU (108 KB of LDS), 2 waves per SIMD as before.
+//   * one workgroup per CU, 2 waves per SIMD as before;
+//   * (round 6) the weights by LDS-DMA into two step buffers (151 KB of LDS in all): step
+//     st + 1's fragments land under step st's MFMAs with no register round trip or LDS store
+//     of their own; 2839-2898 vs 2929-3018 us at bf16x3 96 -> 48 128^3, 3492-3508 vs
+//     3639-3678 us in the config-4 step (profiles/r6/r6ak_conv_wdma_*.txt).
 // The arithmetic per output is the 8-channel kernel's (same K order, same operands): outputs
 // are bitwise those of conv3d_k3_kernel (tests/test_gpu_decoder.py).
 //
@@ -403,7 +410,8 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
   constexpr int CW = 2 * kConvCC;                    // 16 channels staged per step
   constexpr int PB = CW * 2;                         // 32 B per position
   constexpr int NFRAG = 2 * kConvKS * CO_T;          // 42 weight fragments per step
-  constexpr int NW = (NFRAG * 64 + 511) / 512;       // 16-B weight pieces per thread
+  constexpr int NW = WF_C3W_WDMA ? 1 : (NFRAG * 64 + 511) / 512;  // 16-B weight pieces per thread
+  constexpr int NFW = (NFRAG + 7) / 8;               // WDMA: 1-KB fragments per wave
   constexpr int QN = XH ? CW / 8 : CW / 4;           // lanes per position (16 B each)
   constexpr int PSTEP = 512 / QN;
   constexpr int NJ = (NPOS * QN + 511) / 512;
@@ -506,6 +514,35 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
   // weight fragments of step st: f = (sub * 7 + step) * CO_T + m for chunks 2 st, 2 st + 1 (a
   // missing second chunk, odd nch, reads the first one's: never used); SPLIT: f = (step * 2 +
   // plane) * CO_T + m of chunk st, the packed order
+#if WF_C3W_WDMA
+  // weights by LDS-DMA (buffer_load_dwordx4 ... lds, no VGPR destination) into the buffer of
+  // step st's parity: wave w copies fragments w, w + 8, ... (1 KB each, lane-linear in both
+  // the packed global layout and the LDS image); the buffer was last read by step st - 1's
+  // K loop, which every wave left before the barrier that precedes this fetch
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.w), 0, (int)((int64_t)a.nch * kConvKS * 2 * cblk * 1024),
+      0x00020000);
+  auto fetch_w = [&](int st) {
+    uint16_t* dst = s_w + (st & 1) * (NFRAG * 512);
+#pragma unroll
+    for (int i = 0; i < NFW; ++i) {
+      const int f = wid + 8 * i;
+      if (NFRAG % 8 != 0 && f >= NFRAG) break;
+      const int m = f % CO_T, ss = f / CO_T;
+      int64_t frag;
+      if constexpr (SPLIT) {
+        frag = ((int64_t)st * kConvKS * 2 + ss) * cblk + co0 / 16 + m;
+      } else {
+        const int sub = ss / kConvKS, step = ss - sub * kConvKS;
+        const int ch = min(2 * st + sub, a.nch - 1);
+        frag = ((int64_t)(ch * kConvKS + step) * 2) * cblk + co0 / 16 + m;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wrs, (__attribute__((address_space(3))) void*)(dst + f * 512), 16,
+          (uint32_t)((frag * 64 + lane) * 16), 0, 0, 0);
+    }
+  };
+#else
   auto fetch_w = [&](int st) {
 #if WF_CONV_DBG
     if (a.dbg & 4) {
@@ -530,9 +567,12 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
       sw[w] = *reinterpret_cast<const bf16x8*>(a.w + (frag * 64 + ln) * 8);
     }
   };
+#endif
   auto fetch = [&](int st) {
+    // WDMA: the weights first, so the wait for the activations (issued after) covers them
+    if (WF_C3W_WDMA) fetch_w(st);
     if (!SPLIT || (st & 1) == 0) fetch_act(st);
-    fetch_w(st);
+    if (!WF_C3W_WDMA) fetch_w(st);
   };
   auto commit = [&](int st) {
     const int c = (SPLIT ? st / 2 : st) * CW + (XH ? 8 : 4) * q;
@@ -568,14 +608,20 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
         *reinterpret_cast<bf16x4*>(s_act + paddr(pos) + 8 * q) = h;
       }
     }
+#if WF_C3W_WDMA
+    (void)skip_w;
+    // this wave's weight DMA has landed (the barrier after commit makes every wave's visible)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
 #pragma unroll
     for (int w = 0; w < NW && !skip_w; ++w) {
       const int i = tid + 512 * w;
       if (w == NW - 1 && i >= NFRAG * 64) break;
       *reinterpret_cast<bf16x8*>(s_w + i * 8) = sw[w];
     }
+#endif
   };
-  const char* lw = reinterpret_cast<const char*>(s_w) + lane * 16;
+  const char* lw0 = reinterpret_cast<const char*>(s_w) + lane * 16;
 
   fetch(0);
   for (int st = 0; st < nst; ++st) {
@@ -583,6 +629,7 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
     commit(st);
     __syncthreads();
     if (st + 1 < nst) fetch(st + 1);
+    const char* lw = lw0 + (WF_C3W_WDMA ? (st & 1) * NFRAG * 1024 : 0);
 #if WF_CONV_DBG
     if (a.dbg & 16) {
       acc[0][0].x += (float)s_act[tid & 63] + (float)lw[0];
@@ -702,7 +749,9 @@ __global__ __launch_bounds__(512, 1) void conv3d_k3w_kernel(Conv3Args a) {
 
 static size_t conv3w_lds() {
   constexpr int NPOS = 3 * 10 * 66;
-  return (size_t)NPOS * 32 + (NPOS / 8 + 1) * 16 + (size_t)2 * kConvKS * 3 * 1024;
+  // activations + the weight fragments of one step (WDMA: of two, double-buffered)
+  return (size_t)NPOS * 32 + (NPOS / 8 + 1) * 16 +
+         (size_t)(WF_C3W_WDMA ? 2 : 1) * 2 * kConvKS * 3 * 1024;
 }
 
 // out[p][c] = sum_z part[z][p][c], z ascending (the split-K partials, bias in part[0])
