@@ -27,7 +27,10 @@ constexpr int MR_N = 2 * MR_C;                // 96
 constexpr int MR_NT = MR_N / 16;              // 6 column tiles
 constexpr int MR_KS = MR_K / 32;              // 12 k steps
 constexpr int MR_KP = MR_K + WF_LDS_KPAD;     // LDS row stride in bf16: 200 dwords, 8 mod 16
-constexpr int MR_WAVES = 12;
+#ifndef WF_MR_WAVES  // waves per merge_res workgroup: 8 measured 135.5-139.3 us against 141.8-143.8
+#define WF_MR_WAVES 8  // (12), 149.9-151.0 (6), 154.8-155.6 (4); 16 spills (r6/r6ap_merge_res_waves_ab.txt)
+#endif
+constexpr int MR_WAVES = WF_MR_WAVES;
 
 template <int P>
 __global__ __launch_bounds__(64 * MR_WAVES, 1) void merge_res_kernel(GemmArgs g) {
