@@ -763,6 +763,10 @@ extern "C" int wf_ccf_ffn_stage(int stage, const float* xh, const float* stats,
   f.out = out;
   f.out_bf16 = 0;
   f.ldo = C;
+  if (!keep) {  // h1 is dead once the depthwise conv has read it: the fc's split-K scratch
+    f.kpart = reinterpret_cast<float*>(h1);
+    f.kpart_bytes = one;
+  }
   return launch_gemm(f, s, "wf_ccf_ffn_fwd(fc)");
 }
 

@@ -53,6 +53,16 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
   const int K = g.K, N = g.N;
   const int M = (int)g.M;
   const int nks = (K + KC_BK - 1) / KC_BK;
+  // split-K (g.ksplit > 1, small grids): this workgroup runs k steps [ks0, ks1) and stores its
+  // raw fp32 partial sums to g.kpart; gemm_kc_reduce_kernel adds them in split order
+  const bool part = g.ksplit > 1;
+  int ks0 = 0, ks1 = nks;
+  if (part) {
+    const int per = (nks + g.ksplit - 1) / g.ksplit;
+    ks0 = (int)blockIdx.z * per;
+    ks1 = min(nks, ks0 + per);
+  }
+  const int kend = min(K, ks1 * KC_BK);
   const int c0 = blockIdx.y * NC;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l15 = lane & 15, g4 = lane >> 4;
@@ -211,7 +221,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
   // the in-order vmcnt behind the prefetches and drain them every step)
   // (sized for an even step count: the unrolled loop's extra step of an odd count reads
   // lnw / lnb at k >= K, zeros here, discarded by its kv select)
-  const int nks2 = (nks + 1) & ~1;
+  const int nks2 = part ? ((nks + 2) & ~1) : ((nks + 1) & ~1);  // kc_ln_steps
   float* lnw = reinterpret_cast<float*>(Wl + (size_t)2 * NPL * NC * KC_KP);
   float* lnb = lnw + nks2 * KC_BK;
   if (g.a_ln != LN_NONE) {
@@ -220,10 +230,10 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
       lnb[i] = i < K ? g.a_ln_b[i] : 0.f;
     }
   }
-  wfetch(0, wst[0]);
-  afetch(0, an[0]);
-  wfetch(min(1, nks - 1), wst[1]);
-  afetch(min(1, nks - 1), an[1]);
+  wfetch(ks0, wst[0]);
+  afetch(ks0, an[0]);
+  wfetch(min(ks0 + 1, ks1 - 1), wst[1]);
+  afetch(min(ks0 + 1, ks1 - 1), an[1]);
   wcommit(0, wst[0]);
   __syncthreads();
   // step ks runs on LDS buffer / register set S = ks & 1 (a compile-time slot: the k loop is
@@ -232,13 +242,13 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
     constexpr int S = decltype(slot)::value;
     const int buf = S;
     const int k = ks * KC_BK + 8 * g4;
-    const bool kv = k < K;
+    const bool kv = k < kend;
     float v[RT][8];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[rt][j] = vin[rt][j];
-    wfetch(min(ks + 2, nks - 1), wst[S]);  // two steps ahead (tail steps: unused re-reads)
+    wfetch(min(ks + 2, ks1 - 1), wst[S]);  // two steps ahead (tail steps: unused re-reads)
     bf16x8 ah[RT], al[RT];
     {
       float wv[8], bv[8];
@@ -271,7 +281,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
     }
     // the A set of this slot is consumed (split) before its next load is issued, so the load
     // can reuse its registers: no loop-carried copies (and load waits) at the barrier
-    afetch(min(ks + 2, nks - 1), an[S]);
+    afetch(min(ks + 2, ks1 - 1), an[S]);
     const uint16_t* Wb = Wl + (size_t)buf * NPL * NC * KC_KP;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -314,12 +324,25 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
     // count runs one extra step whose A operands are zeroed (k >= K: the kv select) against a
     // weight slice re-reading the last octet (finite), adding exact zeros
 #pragma unroll 1
-    for (int ks = 0; ks < nks; ks += 2) {
+    for (int ks = ks0; ks < ks1; ks += 2) {
       kbody(ks, Slot0{}, an[0]);
       kbody(ks + 1, Slot1{}, an[1]);
     }
   }
 
+  if (part) {  // raw partials (M, N) of split blockIdx.z; bias and epilogue in the reduce
+    float* pz = g.kpart + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int row = rbase + rt * 16 + l15;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int col = c0 + t * 16 + 4 * g4;
+        if (row < M && col < N) *reinterpret_cast<f32x4*>(pz + (int64_t)row * N + col) = acc[rt][t];
+      }
+    }
+    return;
+  }
   // ---- epilogue: acc[rt][t][i] = out[row rbase + 16 rt + l15][channel c0 + 16 t + 4 g4 + i]
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
@@ -415,6 +438,75 @@ __global__ __launch_bounds__(64 * WV) void gemm_kc_kernel(GemmArgs g) {
   }
 }
 
+constexpr int KC_MAX_SPLIT = 4;
+// split-K reduction: out = epilogue(sum over splits z = 0, 1, .. in order + bias), one thread
+// per 4 columns of a row (EPI_STORE without LayerNorm partials, EPI_RESID)
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_kc_reduce_kernel(GemmArgs g) {
+  const int N = g.N, n4 = N / 4, M = (int)g.M;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * n4) return;
+  const int row = i / n4, col = (i - row * n4) * 4;
+  const int64_t MN = (int64_t)M * N;
+  const float* p = g.kpart + (int64_t)row * N + col;
+  f32x4 q[KC_MAX_SPLIT];  // all partial loads in flight before the in-order sum
+#pragma unroll
+  for (int z = 0; z < KC_MAX_SPLIT; ++z)
+    if (z < g.ksplit) q[z] = *reinterpret_cast<const f32x4*>(p + z * MN);
+  f32x4 v = q[0];
+#pragma unroll
+  for (int z = 1; z < KC_MAX_SPLIT; ++z)
+    if (z < g.ksplit) v += q[z];
+  if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
+  if (EPI == EPI_RESID) {
+    const f32x4 xr = *reinterpret_cast<const f32x4*>(g.r_x + (int64_t)row * N + col);
+    const float bs = g.r_scale ? g.r_scale[row / (int)g.rows_per_sample] : 1.f;
+    if (g.r_stats) {
+      const float rm_ = g.r_stats[2 * row], rs_ = g.r_stats[2 * row + 1];
+      const f32x4 lw = *reinterpret_cast<const f32x4*>(g.r_ln_w + col);
+      const f32x4 lb = *reinterpret_cast<const f32x4*>(g.r_ln_b + col);
+      const f32x4 n2 = (xr - rm_) * rs_ * lw + lb;
+      v = xr + (n2 + v) * bs;  // as gemm_kc_kernel's EPI_RESID
+    } else {
+      v = xr + v * bs;
+    }
+  }
+  if (g.out_bf16) {
+    bf16x4 o;
+    o[0] = (short)f2bf(v.x);
+    o[1] = (short)f2bf(v.y);
+    o[2] = (short)f2bf(v.z);
+    o[3] = (short)f2bf(v.w);
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(g.out) + (int64_t)row * g.ldo + col) = o;
+  } else {
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(g.out) + (int64_t)row * g.ldo + col) = v;
+  }
+}
+
+// k splits for g (1 = none).  Only the GELU-loader fc of CCF_FFN at K >= 1536 (stage 4, 128
+// workgroups at B = 8), with a caller scratch: 64.6 -> 54 us per B = 8 launch incl. the reduce;
+// at stage 3 (K = 768, 512 workgroups) a split of 2 measured 71 -> 94 us, and the merging / qkv
+// loaders gain nothing (profiles/r6/r6ks*_ab.txt).  The split count is a function of K, N and the
+// precision only -- never of M -- so a row's sum order does not change with the batch (the B = 8
+// graph replay equals per-volume B = 1 forwards, test_gpu_bench_config.py).
+// (WF_KC_SPLIT: the largest split, A/B; 1 disables)
+static int kc_ksplit(const GemmArgs& g, bool areg) {
+  static const int maxs = getenv("WF_KC_SPLIT") ? std::max(1, atoi(getenv("WF_KC_SPLIT"))) : 4;
+  if (!g.kpart || areg || g.o_pstats || !g.a_gelu || (g.epi != EPI_STORE && g.epi != EPI_RESID))
+    return 1;
+  if (g.M * (int64_t)(g.N / 4) >= ((int64_t)1 << 31) || g.N % 4 != 0 || g.K < 1536) return 1;
+  const int nks = (g.K + KC_BK - 1) / KC_BK;
+  // scratch: the caller's kpart_bytes is a multiple of M (the fc's dead h1 = M x hidden), so the
+  // fit test below does not depend on M either
+  int s = 1;
+  while (2 * s <= std::min(maxs, KC_MAX_SPLIT) && nks / (2 * s) >= 6 &&
+         (int64_t)(2 * s) * g.M * g.N * 4 <= g.kpart_bytes)
+    s *= 2;
+  if (s == 1) return 1;
+  const int per = (nks + s - 1) / s;
+  return (nks + per - 1) / per;  // every split non-empty
+}
+
 template <int NT, int MAP, int EPI>
 static void go_kc(const GemmArgs& g, hipStream_t s) {
   typedef KcCfg<NT> C;
@@ -453,13 +545,24 @@ static void go_kc(const GemmArgs& g, hipStream_t s) {
       nthr = KcCfg<NT, 16>::NTHR;
     }
   }
+  GemmArgs gk = g;
+  gk.ksplit = 1;
+  if constexpr (EPI == EPI_STORE || EPI == EPI_RESID)
+    gk.ksplit = kc_ksplit(g, areg);
+  const int nks = (int)cdiv(g.K, KC_BK);
+  const int nks2 = gk.ksplit > 1 ? ((nks + 2) & ~1) : ((nks + 1) & ~1);  // as the kernel's
   const size_t lds = (size_t)2 * (split ? 2 : 1) * C::NC * KC_KP * 2 +
-                     (g.a_ln != LN_NONE ? (size_t)2 * ((cdiv(g.K, KC_BK) + 1) & ~1) * KC_BK * 4
-                                        : 0);
+                     (g.a_ln != LN_NONE ? (size_t)2 * nks2 * KC_BK * 4 : 0);
   if (lds > 64 * 1024)
     set_max_lds(reinterpret_cast<const void*>(kern), (int)lds);
-  const dim3 grid((unsigned)cdiv(g.M, rows), (unsigned)(g.N / C::NC));
-  hipLaunchKernelGGL(kern, grid, dim3(nthr), lds, s, g);
+  const dim3 grid((unsigned)cdiv(g.M, rows), (unsigned)(g.N / C::NC), (unsigned)gk.ksplit);
+  hipLaunchKernelGGL(kern, grid, dim3(nthr), lds, s, gk);
+  if constexpr (EPI == EPI_STORE || EPI == EPI_RESID) {
+    if (gk.ksplit > 1) {
+      const int64_t n = g.M * (g.N / 4);
+      hipLaunchKernelGGL(gemm_kc_reduce_kernel<EPI>, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, gk);
+    }
+  }
 }
 
 template <int MAP, int EPI>
@@ -485,7 +588,18 @@ int gemm_kc_pick_nt(const GemmArgs& g) {
   const int tiles = g.N / 16;
   static const int cand[] = {24, 12, 8, 6, 4, 3, 2, 1};
   // narrowest chunk the small-M search may go down to (WF_KC_MINNT, A/B; round 1-4: 3)
-  static const int minnt = getenv("WF_KC_MINNT") ? std::max(1, atoi(getenv("WF_KC_MINNT"))) : 3;
+  static const char* env_minnt = getenv("WF_KC_MINNT");
+  int minnt = env_minnt ? std::max(1, atoi(env_minnt)) : 3;
+  // loaders with a costly A transform (the fc's LayerNorm + GELU, the window gather + LN of qkv)
+  // redo it per column chunk: at N >= 384 (8+ chunks of 3 tiles) 6-tile chunks halve that work
+  // (stage-4 qkv 52.3 -> 39.0 us, the 576-column qkv 16.1 -> 13.4 us; plain loaders measured
+  // slower with fewer chunks, profiles/r6/r6ks2_ab.txt)
+  if (!env_minnt && (g.a_gelu || g.a_map == MAP_WINDOW) && g.N >= 384) minnt = 6;
+  // the split-K fc (kc_ksplit: GELU loader, K >= 1536, caller scratch): the widest chunk up to
+  // 12 tiles -- 2 chunks of 192 at stage 4, 256 workgroups with the 4 k splits: 55.5 -> 48.0 us
+  // per B = 8 launch against 6 tiles; at stage 3 (no split) one 12-tile chunk measured 71 -> 73.5
+  // (profiles/r6/r6ks4_ab.txt)
+  const bool fc_wide = g.a_gelu && g.kpart && g.K >= 1536 && store32(g.prec) && !g.a_bf16;
   // widest column chunk that divides N (fewest re-reads of A); then, for small M, narrower
   // chunks until the grid has ~2 workgroups per CU (the K loop is a serial chain per workgroup)
   auto blocks = [&](int c) { return cdiv(g.M, 128) * (tiles / c); };
@@ -493,11 +607,13 @@ int gemm_kc_pick_nt(const GemmArgs& g) {
   // with fp32 activations (PREC_SPLIT / PREC_FP16) NT = 12 / 24 need 150-210 VGPRs (two or
   // three waves per SIMD) -- at most 8 column tiles (<= 136 VGPRs) and the A rows re-read per
   // chunk from L2 instead
-  const int ntmax = (g.epi != EPI_LN_GELU && store32(g.prec) && !g.a_bf16) ? 8 : 24;
+  const int ntmax = fc_wide ? 12 : (g.epi != EPI_LN_GELU && store32(g.prec) && !g.a_bf16) ? 8 : 24;
   for (int c : cand) {
     if (tiles % c != 0 || c > ntmax) continue;
     if (g.epi == EPI_LN_GELU && c != tiles) continue;  // LayerNorm needs the full row
-    if (nt == 0 || (g.epi != EPI_LN_GELU && blocks(nt) < 512 && c >= minnt)) nt = c;
+    if (nt == 0 || (g.epi != EPI_LN_GELU && !fc_wide && blocks(nt) < 512 &&
+                    c >= minnt))
+      nt = c;
     if (blocks(nt) >= 512) break;
   }
   return nt;

@@ -142,6 +142,10 @@ struct GemmArgs {
   int dbg;               // timing experiments only (builds with WF_ROWS_DBG=1): phases skipped
   float* o_pstats;       // EPI_STORE (gemm_kc): if non-NULL, per (row, column chunk) {mean, M2}
                          //   of the stored values, (M, N / chunk, 2) -- LN statistics partials
+  float* kpart;          // gemm_kc split-K scratch (caller-owned, kpart_bytes), or NULL: small
+  int64_t kpart_bytes;   //   grids split the k loop over grid.z into (ksplit, M, N) fp32
+                         //   partials, summed in split order by a second kernel + epilogue
+  int ksplit;            // set by the launcher (kernel side), 1 = no split
 };
 
 int launch_gemm(const GemmArgs& g, hipStream_t s, const char* who);
