@@ -4,6 +4,7 @@
 
 #include <algorithm>
 
+#include "kernels.hpp"
 #include "rowgroup.hpp"
 
 namespace wf {
@@ -182,6 +183,131 @@ __global__ __launch_bounds__(256) void patch_embed_ll_kernel(
   }
   __syncthreads();
   // LL of the W/2 cubes x C4 channel quads: n = 4 dz + 2 dy + dx, butterflies x, y, z
+  const int wp = W >> 1;
+  const int64_t lbase = ((b * dp + zp) * hp + yp) * (int64_t)wp;
+  for (int it = threadIdx.x; it < wp * C4; it += 256) {
+    const int lx = it / C4, q4 = it - lx * C4;
+    const f32x4 gw = *reinterpret_cast<const f32x4*>(ln_w + 4 * q4);
+    const f32x4 gb = *reinterpret_cast<const f32x4*>(ln_b + 4 * q4);
+    f32x4 c[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int wn = ((n >> 2) << 1) | ((n >> 1) & 1), ln = 2 * lx + (n & 1);
+      const float2 ms = mst[wn][ln];
+      const f32x4 val = *reinterpret_cast<const f32x4*>(&tile[wn][ln * RS + 4 * q4]);
+      c[n] = (val - ms.x) * ms.y * gw + gb;
+    }
+    const f32x4 s01 = c[0] + c[1], s23 = c[2] + c[3], s45 = c[4] + c[5], s67 = c[6] + c[7];
+    const f32x4 r = ((s01 + s23) + (s45 + s67)) * 0.35355339059327373f;
+    *reinterpret_cast<f32x4*>(ll + (lbase + lx) * COUT + 4 * q4) = r;
+  }
+}
+
+// The same kernel with the 4 -> 48 convolution on the matrix cores (Cin = 4: K = 32, one
+// v_mfma_f32_16x16x32_bf16 K step): lane (l15, g4) of position tile pt holds input channel
+// ci = g4's 2 x 2 x 2 patch of output position x = 16 pt + l15 (four float2 loads, the same bytes
+// per thread as above), split to bf16 hi / lo (bf16x3: hi*hi + hi*lo + lo*hi, fp32-faithful
+// products, as every GEMM of the path); the weight fragments (output channel 16 rt + l15, k
+// octet g4) are split once per thread.  The FMA form ran 1536 fp32 FMAs per position -- ~80 us
+// of the 191 us launch at B = 8 in VALU issue alone (profiles/r6/r6pe_*).  The products land
+// as 4 consecutive channels of one position per lane, are written (+ bias) into the same LDS row
+// tile, and each lane then reads its own position's row back for norm1's moments; stores, LN
+// and LL are the FMA kernel's.
+__global__ __launch_bounds__(256) void patch_embed_ll_mfma_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ out, const float* __restrict__ ln_w, const float* __restrict__ ln_b,
+    float ln_eps, float* __restrict__ ll, int D, int H, int W) {
+  constexpr int CIN = 4, COUT = 48, K = 32;
+  constexpr int RS = COUT + 4;
+  constexpr int C4 = COUT / 4;
+  constexpr int RT = COUT / 16;  // output-channel tiles
+  __shared__ __attribute__((aligned(16))) float tile[4][64 * RS];
+  __shared__ float2 mst[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const int hp = H >> 1, dp = D >> 1;
+  int64_t t = blockIdx.x;
+  const int yp = (int)(t % hp);
+  t /= hp;
+  const int zp = (int)(t % dp);
+  const int64_t b = t / dp;
+  const int zo = 2 * zp + (wv >> 1), yo = 2 * yp + (wv & 1);
+  const int W2 = 2 * W, H2 = 2 * H, D2 = 2 * D;
+  // patches first (the loads in flight while the weights are split)
+  float v[4][8];
+  const float* xb = x + ((b * CIN + g4) * D2 + 2 * zo) * (int64_t)H2 * W2 + (int64_t)(2 * yo) * W2;
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const int xo = min(16 * pt + l15, W - 1);
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const float2 u = *reinterpret_cast<const float2*>(xb + ((int64_t)dz * H2 + dy) * W2 + 2 * xo);
+        v[pt][dz * 4 + dy * 2] = u.x;
+        v[pt][dz * 4 + dy * 2 + 1] = u.y;
+      }
+  }
+  bf16x8 wh[RT], wl[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(w + (16 * rt + l15) * K + 8 * g4);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(w + (16 * rt + l15) * K + 8 * g4 + 4);
+    const float wf[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    split8<PREC_SPLIT>(wf, wh[rt], wl[rt]);
+  }
+  f32x4 bq[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+    bq[rt] = bias ? *reinterpret_cast<const f32x4*>(bias + 16 * rt + 4 * g4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  float* tw = tile[wv];
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    bf16x8 ph, pl;
+    split8<PREC_SPLIT>(v[pt], ph, pl);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc = mma32<PREC_SPLIT>(wh[rt], pl, acc);
+      acc = mma32<PREC_SPLIT>(wl[rt], ph, acc);
+      acc = mma32<PREC_SPLIT>(wh[rt], ph, acc);
+      *reinterpret_cast<f32x4*>(tw + (16 * pt + l15) * RS + 16 * rt + 4 * g4) = acc + bq[rt];
+    }
+  }
+  __syncthreads();  // the wave's row tile complete (other lanes' products)
+  // norm1's moments of this lane's position (two-pass, as row_stats)
+  {
+    const float* row = tw + lane * RS;
+    f32x4 o[C4];
+#pragma unroll
+    for (int c4 = 0; c4 < C4; ++c4) o[c4] = *reinterpret_cast<const f32x4*>(row + 4 * c4);
+    float sm = 0.f;
+#pragma unroll
+    for (int c4 = 0; c4 < C4; ++c4) sm += (o[c4].x + o[c4].y) + (o[c4].z + o[c4].w);
+    const float mean = sm / (float)COUT;
+    float q = 0.f;
+#pragma unroll
+    for (int c4 = 0; c4 < C4; ++c4) {
+      const f32x4 d = o[c4] - mean;
+      q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+    }
+    mst[wv][lane] = float2{mean, rsqrtf(q / (float)COUT + ln_eps)};
+  }
+  // the activation row (W positions x COUT, contiguous channel-last) with 1 KB stores
+  {
+    const int64_t p0 = ((b * D + zo) * H + yo) * W;
+    float* dst = out + p0 * COUT;
+    const int nval = W * C4;
+#pragma unroll
+    for (int j = 0; j < C4; ++j) {
+      const int e = j * 64 + lane;
+      if (e < nval) {
+        const int pos = e / C4, c = (e - pos * C4) * 4;
+        *reinterpret_cast<f32x4*>(dst + 4 * (int64_t)e) = *reinterpret_cast<const f32x4*>(&tw[pos * RS + c]);
+      }
+    }
+  }
+  __syncthreads();
   const int wp = W >> 1;
   const int64_t lbase = ((b * dp + zp) * hp + yp) * (int64_t)wp;
   for (int it = threadIdx.x; it < wp * C4; it += 256) {
@@ -805,7 +931,12 @@ extern "C" int wf_patch_embed_ll_fwd(const float* x, const float* w, const float
   WF_REQUIRE_PTR(ln_b);
   WF_REQUIRE_PTR(ll);
   const unsigned blocks = (unsigned)(B * (D / 2) * (H / 2));
-  if (Cin == 4)
+  // (WF_PE_LL_VALU=1: the fp32-FMA kernel, A/B)
+  static const bool valu = getenv("WF_PE_LL_VALU") != nullptr;
+  if (Cin == 4 && !valu)
+    hipLaunchKernelGGL(patch_embed_ll_mfma_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       x, w, bias, out, ln_w, ln_b, ln_eps, ll, (int)D, (int)H, (int)W);
+  else if (Cin == 4)
     hipLaunchKernelGGL((patch_embed_ll_kernel<4, 48>), dim3(blocks), dim3(256), 0,
                        (hipStream_t)stream, x, w, bias, out, ln_w, ln_b, ln_eps, ll, (int)D,
                        (int)H, (int)W);
