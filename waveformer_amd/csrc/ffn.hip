@@ -228,15 +228,19 @@ struct Store2<uint16_t> {
 // the plane staging -- ln1_stats (M, 2) {mean, rstd} per position, ln1_w / ln1_b (Hd) -- so
 // the separate LayerNorm + GELU pass over h1 (read + write of the whole tensor) is gone
 // (stages 3 / 4 of the encoder); halo positions outside the volume stay zero.
-template <typename T, bool LN1, bool FLIP = false>
-__global__ __launch_bounds__(256) void dwconv3d_kernel(
+// CH_ / TX_: the channel chunk and tile width -- 32 x 16 by default; narrow volumes (W <= 8:
+// the stage-4 8^3 shapes, where half of a 16-wide tile's threads had no column) take 64 x 8
+// (two 32-channel statistics groups per workgroup)
+template <typename T, bool LN1, bool FLIP = false, int CH_ = DW_CH, int TX_ = DW_TX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void dwconv3d_kernel(
     const T* __restrict__ in, const float* __restrict__ w, const float* __restrict__ bias,
     T* __restrict__ out, float* __restrict__ pstats, int B, int Hd, int D, int H, int W, int ZS,
     double* __restrict__ cstats, const float* __restrict__ ln1_stats,
     const float* __restrict__ ln1_w, const float* __restrict__ ln1_b) {
   static_assert(!LN1 || sizeof(T) == 4, "LN1 staging: fp32 h1");
-  constexpr int CH = DW_CH, TX = DW_TX, TY = DW_TY;
-  static_assert(CH == DW_STAT_GROUP, "one statistics group per workgroup channel chunk");
+  constexpr int CH = CH_, TX = TX_, TY = DW_TY;
+  static_assert(CH % DW_STAT_GROUP == 0, "whole statistics groups per workgroup channel chunk");
+  constexpr int NG = CH / DW_STAT_GROUP;  // statistics groups per channel chunk
   static_assert(TX * (CH / 2) == 256, "one thread per (column, channel pair)");
   constexpr int PY = TY + 2, PX = TX + 2;
   typedef Vec16<T> V;
@@ -384,8 +388,9 @@ __global__ __launch_bounds__(256) void dwconv3d_kernel(
               cq0 += a0 * a0;
               cq1 += a1 * a1;
             }
-            if (pstats && cp == 0)
-              *reinterpret_cast<float2*>(pstats + (pos * ncc + cc) * 2) = float2{mu[o], m2[o]};
+            if (pstats && cp % (DW_STAT_GROUP / 2) == 0)
+              *reinterpret_cast<float2*>(pstats + (pos * (ncc * NG) + cc * NG + cp / (DW_STAT_GROUP / 2)) * 2) =
+                  float2{mu[o], m2[o]};
           }
         }
       }
@@ -427,11 +432,22 @@ int launch_dwconv3d(const void* in, const float* w, const float* b, void* out, f
     return fail(WF_E_SHAPE, "dwconv3d: the mirrored taps are for fp32 data without LN1 staging");
   // z segment: enough workgroups to fill 256 CUs ~8 deep, but long enough that the two halo
   // planes per segment stay a small overhead
-  const int64_t base = (int64_t)B * (Hd / DW_CH) * cdiv(H, DW_TY) * cdiv(W, DW_TX);
+  // narrow volumes (W <= 8): 64 channels x 8 columns per workgroup, z segments down to 4
+  // (WF_DW_NARROW=0: the 32 x 16 tiles, A/B)
+  static const bool narrow_ok = !(getenv("WF_DW_NARROW") && getenv("WF_DW_NARROW")[0] == '0');
+  const bool narrow = narrow_ok && W <= 8 && Hd % 64 == 0 && store32(prec) && !flip && !ln1_stats;
+  const int dch = narrow ? 64 : DW_CH, dtx = narrow ? 8 : DW_TX;
+  const int64_t base = (int64_t)B * (Hd / dch) * cdiv(H, DW_TY) * cdiv(W, dtx);
   int ZS = D;
-  while (ZS > 8 && base * cdiv(D, ZS) < 2048) ZS = (ZS + 1) / 2;
+  const int zmin = narrow ? 4 : 8;
+  while (ZS > zmin && base * cdiv(D, ZS) < 2048) ZS = (ZS + 1) / 2;
   const int64_t blocks = base * cdiv(D, ZS);
-  if (ln1_stats) {
+  if (narrow) {
+    hipLaunchKernelGGL((dwconv3d_kernel<float, false, false, 64, 8>), dim3((unsigned)blocks),
+                       dim3(256), 0, s, reinterpret_cast<const float*>(in), w, b,
+                       reinterpret_cast<float*>(out), pstats, B, Hd, D, H, W, ZS, cstats, nullptr,
+                       nullptr, nullptr);
+  } else if (ln1_stats) {
     if (!store32(prec) || !ln1_w || !ln1_b)
       return fail(WF_E_SHAPE, "dwconv3d: the LN1 staging needs fp32 h1 and LN1 weights");
     hipLaunchKernelGGL((dwconv3d_kernel<float, true>), dim3((unsigned)blocks), dim3(256), 0, s,
