@@ -328,6 +328,122 @@ __global__ __launch_bounds__(256) void patch_embed_ll_mfma_kernel(
   }
 }
 
+// v2: no LDS row tile.  norm1's moments of a position are reduced over the four lanes that hold
+// its 48 channels (xor 16 / 32), the activation is stored straight from the MFMA layout (per
+// store instruction 16 positions x 64 B; the three channel tiles complete each 192-B row), and
+// only the x-pair sums of the normalised values cross waves, through 24 KB of LDS (was 55 KB:
+// two workgroups per CU, now the waves' registers bound it).  The LL sums in the butterfly
+// order of the kernel above: ((s01 + s23) + (s45 + s67)) with s = the x pairs of the four rows.
+__global__ __launch_bounds__(256) void patch_embed_ll_mfma2_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ out, const float* __restrict__ ln_w, const float* __restrict__ ln_b,
+    float ln_eps, float* __restrict__ ll, int D, int H, int W) {
+  constexpr int CIN = 4, COUT = 48, K = 32, RT = COUT / 16;
+  __shared__ __attribute__((aligned(16))) float pairs[4][32 * COUT];  // [row][x pair][channel]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const int hp = H >> 1, dp = D >> 1;
+  int64_t t = blockIdx.x;
+  const int yp = (int)(t % hp);
+  t /= hp;
+  const int zp = (int)(t % dp);
+  const int64_t b = t / dp;
+  const int zo = 2 * zp + (wv >> 1), yo = 2 * yp + (wv & 1);
+  const int W2 = 2 * W, H2 = 2 * H, D2 = 2 * D;
+  float v[4][8];
+  const float* xb = x + ((b * CIN + g4) * D2 + 2 * zo) * (int64_t)H2 * W2 + (int64_t)(2 * yo) * W2;
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const int xo = min(16 * pt + l15, W - 1);
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const float2 u = *reinterpret_cast<const float2*>(xb + ((int64_t)dz * H2 + dy) * W2 + 2 * xo);
+        v[pt][dz * 4 + dy * 2] = u.x;
+        v[pt][dz * 4 + dy * 2 + 1] = u.y;
+      }
+  }
+  bf16x8 wh[RT], wl[RT];
+  f32x4 bq[RT], gw[RT], gb[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(w + (16 * rt + l15) * K + 8 * g4);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(w + (16 * rt + l15) * K + 8 * g4 + 4);
+    const float wf[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    split8<PREC_SPLIT>(wf, wh[rt], wl[rt]);
+    const int c = 16 * rt + 4 * g4;
+    bq[rt] = bias ? *reinterpret_cast<const f32x4*>(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    gw[rt] = *reinterpret_cast<const f32x4*>(ln_w + c);
+    gb[rt] = *reinterpret_cast<const f32x4*>(ln_b + c);
+  }
+  const int64_t p0 = ((b * D + zo) * H + yo) * W;
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    bf16x8 ph, pl;
+    split8<PREC_SPLIT>(v[pt], ph, pl);
+    f32x4 acc[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+      a = mma32<PREC_SPLIT>(wh[rt], pl, a);
+      a = mma32<PREC_SPLIT>(wl[rt], ph, a);
+      a = mma32<PREC_SPLIT>(wh[rt], ph, a);
+      acc[rt] = a + bq[rt];
+    }
+    const int xo = 16 * pt + l15;
+    if (xo < W) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        *reinterpret_cast<f32x4*>(out + (p0 + xo) * COUT + 16 * rt + 4 * g4) = acc[rt];
+    }
+    // moments over the position's 48 channels: 12 in this lane, the rest in lanes +-16, +-32
+    float sm = 0.f;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) sm += (acc[rt].x + acc[rt].y) + (acc[rt].z + acc[rt].w);
+    sm += __shfl_xor(sm, 16, 64);
+    sm += __shfl_xor(sm, 32, 64);
+    const float mean = sm * (1.f / COUT);
+    float q = 0.f;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const f32x4 d = acc[rt] - mean;
+      q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+    }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float rstd = rsqrtf(q * (1.f / COUT) + ln_eps);
+    // normalised, then the x pair (lanes l15, l15 ^ 1): s = c[2 lx] + c[2 lx + 1]
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const f32x4 n = (acc[rt] - mean) * rstd * gw[rt] + gb[rt];
+      f32x4 o;
+      o.x = __shfl_xor(n.x, 1, 64);
+      o.y = __shfl_xor(n.y, 1, 64);
+      o.z = __shfl_xor(n.z, 1, 64);
+      o.w = __shfl_xor(n.w, 1, 64);
+      if (!(l15 & 1)) {
+        const int lx = 8 * pt + (l15 >> 1);
+        *reinterpret_cast<f32x4*>(&pairs[wv][lx * COUT + 16 * rt + 4 * g4]) = n + o;
+      }
+    }
+  }
+  __syncthreads();
+  const int wp = W >> 1;
+  constexpr int C4 = COUT / 4;
+  const int64_t lbase = ((b * dp + zp) * hp + yp) * (int64_t)wp;
+  for (int it = threadIdx.x; it < wp * C4; it += 256) {
+    const int lx = it / C4, q4 = it - lx * C4;
+    const int o = lx * COUT + 4 * q4;
+    const f32x4 s01 = *reinterpret_cast<const f32x4*>(&pairs[0][o]);
+    const f32x4 s23 = *reinterpret_cast<const f32x4*>(&pairs[1][o]);
+    const f32x4 s45 = *reinterpret_cast<const f32x4*>(&pairs[2][o]);
+    const f32x4 s67 = *reinterpret_cast<const f32x4*>(&pairs[3][o]);
+    *reinterpret_cast<f32x4*>(ll + (lbase + lx) * COUT + 4 * q4) =
+        ((s01 + s23) + (s45 + s67)) * 0.35355339059327373f;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // PatchEmbed, streaming variant (Cin = 4, Cout % 4 == 0, W % 2 == 0: the encoder's 4 -> 48
 // stem): a persistent workgroup walks groups of R output rows; the next group's 2x2 input
@@ -933,7 +1049,11 @@ extern "C" int wf_patch_embed_ll_fwd(const float* x, const float* w, const float
   const unsigned blocks = (unsigned)(B * (D / 2) * (H / 2));
   // (WF_PE_LL_VALU=1: the fp32-FMA kernel, A/B)
   static const bool valu = getenv("WF_PE_LL_VALU") != nullptr;
-  if (Cin == 4 && !valu)
+  static const bool v1 = getenv("WF_PE_LL_V1") != nullptr;  // A/B: the LDS row-tile version
+  if (Cin == 4 && !valu && !v1)
+    hipLaunchKernelGGL(patch_embed_ll_mfma2_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       x, w, bias, out, ln_w, ln_b, ln_eps, ll, (int)D, (int)H, (int)W);
+  else if (Cin == 4 && !valu)
     hipLaunchKernelGGL(patch_embed_ll_mfma_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                        x, w, bias, out, ln_w, ln_b, ln_eps, ll, (int)D, (int)H, (int)W);
   else if (Cin == 4)
